@@ -1,0 +1,144 @@
+"""Synthetic mTCP frames (numpy) for tests, golden fixtures and bench.py.
+
+Frame geometry follows what mTCP emits:
+
+* Ethernet 14 B (``mtcp.h:42``), IPv4 20 B with ``ihl=5``, ``ttl=64``, DF,
+  ``check`` (``ip_out.c:143-153``);
+* TCP 20 B + options: non-SYN data/ACK segments carry NOP,NOP,TS(10) = 12 B,
+  so ``doff=8`` (``tcp_out.c:22-61, 117-124``);
+* payload up to 1448 B (``tcp_out.c:565``).
+
+The BASELINE.json configurations are:
+
+* C1: 64 B frames, ``tot_len=50``, ``doff=5``, 10 B payload, stride 64;
+* C2: 1500 B frames, ``tot_len=1486``, ``doff=8``, 1434 B payload, stride 1536;
+* C3: IMIX 64/576/1500 at 7:4:1, offsets = prefix sum of ALIGN(L, 64)
+  (``io_engine/lib/pslib.c:146``).
+
+Everything here is host-side numpy; checksum *values* are never computed
+here (the GPU compute kernel or, in tests, the oracle fills them).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+DEFAULT_SEED = 0x6D746370  # "mtcp" 
+
+ETH_LEN = 14
+IP_LEN = 20
+TCP_LEN = 20
+
+
+def align(x, a):
+    return (x + a - 1) // a * a
+
+
+def stride_for(frame_len: int) -> int:
+    """Slot stride for fixed-size frames: 64 B for small frames (two per
+    128 B line), else 128 B multiples (1500 B -> 1536 B)."""
+    return 64 if frame_len <= 64 else align(frame_len, 128)
+
+
+def _write_headers(buf2d: np.ndarray, rng: np.random.Generator, frame_len: np.ndarray,
+                   doff: np.ndarray, ihl: int = 5) -> None:
+    """Write Ethernet/IPv4/TCP headers into rows of ``buf2d`` (n x >=64)
+    in place.  ``frame_len``/``doff`` are per-row arrays.  Check fields are 0."""
+    n = buf2d.shape[0]
+    b = buf2d
+    b[:, 12] = 0x08
+    b[:, 13] = 0x00
+    b[:, 14] = 0x40 | ihl
+    b[:, 15] = 0
+    tot = (frame_len - ETH_LEN).astype(np.uint32)
+    b[:, 16] = (tot >> 8) & 0xFF
+    b[:, 17] = tot & 0xFF
+    # id: random (bytes 18-19 already random); frag_off = DF
+    b[:, 20] = 0x40
+    b[:, 21] = 0x00
+    b[:, 22] = 64
+    b[:, 23] = 6
+    b[:, 24] = 0
+    b[:, 25] = 0
+    # saddr/daddr 26..33 random already
+    ts = ETH_LEN + 4 * ihl
+    # ports, seq, ack random; doff byte, flags = ACK
+    b[:, ts + 12] = (doff.astype(np.uint8) << 4)
+    b[:, ts + 13] = 0x10
+    b[:, ts + 16] = 0
+    b[:, ts + 17] = 0
+    b[:, ts + 18] = 0
+    b[:, ts + 19] = 0
+    has_ts = doff >= 8
+    if has_ts.any():
+        rows = np.nonzero(has_ts)[0]
+        b[rows, ts + 20] = 1      # NOP
+        b[rows, ts + 21] = 1      # NOP
+        b[rows, ts + 22] = 8      # TCPOPT_TIMESTAMP
+        b[rows, ts + 23] = 10     # TCPOLEN_TIMESTAMP
+    del n
+
+
+def fixed_frames(n: int, frame_len: int, stride: int | None = None,
+                 seed: int = DEFAULT_SEED) -> tuple[np.ndarray, int]:
+    """``n`` frames of ``frame_len`` bytes at fixed ``stride`` (flat uint8
+    array of n*stride bytes, padding bytes random).  doff=5 for frames that
+    only fit a bare header (< 66 B), else 8 (NOP,NOP,TS)."""
+    stride = stride or stride_for(frame_len)
+    assert stride >= frame_len and stride % 16 == 0 and frame_len >= 54
+    rng = np.random.default_rng(seed)
+    buf = rng.integers(0, 256, size=n * stride, dtype=np.uint8)
+    b2 = buf.reshape(n, stride)
+    doff = np.full(n, 5 if frame_len < 66 else 8, dtype=np.uint32)
+    _write_headers(b2, rng, np.full(n, frame_len, dtype=np.uint32), doff)
+    return buf, stride
+
+
+def imix_lengths(n: int, seed: int = DEFAULT_SEED) -> np.ndarray:
+    """IMIX 64/576/1500 at 7:4:1 (BASELINE.json configs[3])."""
+    rng = np.random.default_rng(seed ^ 0x494D4958)
+    u = rng.integers(0, 12, size=n)
+    return np.where(u < 7, 64, np.where(u < 11, 576, 1500)).astype(np.uint16)
+
+
+def packed_offsets(lengths: np.ndarray, a: int = 64) -> tuple[np.ndarray, int]:
+    """pslib-style packing: offset[i] = sum of ALIGN(len[j], a), j < i."""
+    slots = (lengths.astype(np.uint64) + (a - 1)) // a * a
+    off = np.zeros(len(lengths), dtype=np.uint64)
+    if len(lengths) > 1:
+        np.cumsum(slots[:-1], out=off[1:])
+    total = int(off[-1] + slots[-1]) if len(lengths) else 0
+    return off, total
+
+
+def packed_frames(lengths: np.ndarray, seed: int = DEFAULT_SEED,
+                  ) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Variable-length TCP frames packed at 64 B-aligned offsets.  Returns
+    (buf, off[u64], len[u16]).  Every frame >= 54 B carries valid headers."""
+    lengths = np.asarray(lengths, dtype=np.uint16)
+    assert (lengths >= 54).all()
+    off, total = packed_offsets(lengths)
+    rng = np.random.default_rng(seed)
+    buf = rng.integers(0, 256, size=total + 64, dtype=np.uint8)
+    # header region of each frame as a gathered 2-D view, written back
+    idx = off[:, None].astype(np.int64) + np.arange(64)[None, :]
+    hdr = buf[idx]
+    doff = np.where(lengths < 66, 5, 8).astype(np.uint32)
+    _write_headers(hdr, rng, lengths.astype(np.uint32), doff)
+    buf[idx] = hdr
+    return buf, off, lengths
+
+
+def corrupt(buf: np.ndarray, off: np.ndarray, lengths: np.ndarray, frac_log2: int = 10,
+            seed: int = DEFAULT_SEED) -> np.ndarray:
+    """Flip one random byte (never the Ethernet header) in a seeded
+    1/2^frac_log2 of frames.  Returns the indices of corrupted frames."""
+    rng = np.random.default_rng(seed ^ 0xBAD)
+    n = len(off)
+    pick = np.nonzero(rng.integers(0, 1 << frac_log2, size=n) == 0)[0]
+    lengths = np.asarray(lengths)
+    for i in pick:
+        L = int(lengths[i] if lengths.ndim else lengths)
+        pos = int(rng.integers(ETH_LEN, L))
+        flip = int(rng.integers(1, 256))
+        buf[int(off[i]) + pos] ^= flip
+    return pick

@@ -1,0 +1,325 @@
+/*
+ * csum_ref.c -- CPU ORACLE (test infrastructure only; see csum_ref.h).
+ *
+ * Clean-room restatement of mTCP's --disable-hwcsum checksum path.  Compiled
+ * with the reference's own flags (-O3 -g -DNDEBUG -m64 -fgnu89-inline,
+ * mtcp/src/Makefile.in:44,50) so that it doubles as the "port" CPU baseline.
+ */
+#include "csum_ref.h"
+
+#include <pthread.h>
+#include <string.h>
+
+/* Little-endian loads from any alignment (the reference dereferences
+ * uint16_t* / u32* on x86, which is little-endian and unaligned-tolerant). */
+static inline uint32_t ld16(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
+static inline uint32_t ld32(const uint8_t *p)
+{
+	return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) |
+	       ((uint32_t)p[3] << 24);
+}
+static inline uint16_t bswap16(uint16_t v) { return (uint16_t)((v >> 8) | (v << 8)); }
+
+/* tcp_util.c:244-277.  32-bit accumulator of little-endian 16-bit words,
+ * odd tail = low byte of the last word (mask ntohs(0xFF00) == 0x00FF on LE,
+ * :262-263), pseudo-header halves of saddr/daddr as stored, htons(len),
+ * htons(IPPROTO_TCP), two-step fold (:271-272), complement (:274). */
+uint16_t ref_tcp_calc_checksum(const uint8_t *buf, uint16_t len,
+                               uint32_t saddr, uint32_t daddr)
+{
+	uint32_t sum = 0;
+	int nleft = len;
+	const uint8_t *w = buf;
+
+	while (nleft > 1) {
+		sum += ld16(w);
+		w += 2;
+		nleft -= 2;
+	}
+	if (nleft)
+		sum += w[0];            /* == *w & 0x00FF */
+
+	sum += (saddr & 0x0000FFFFu) + (saddr >> 16);
+	sum += (daddr & 0x0000FFFFu) + (daddr >> 16);
+	sum += bswap16(len);
+	sum += bswap16(6);          /* IPPROTO_TCP */
+
+	sum = (sum >> 16) + (sum & 0xFFFFu);
+	sum += (sum >> 16);
+	return (uint16_t)~sum;
+}
+
+/* ps.h:66-95, the x86 asm actually used on x86_64 builds:
+ *   movl (iph),sum ; subl $4,ihl ; jbe 2f   -> ihl<=4: raw low 16 bits of word 0
+ *   addl 4 ; adcl 8 ; adcl 12 ; loop adcl 16.. (ihl-4 times) ; adcl $0
+ *   fold: (sum>>16) +w low16(sum) with carry ; notl */
+uint16_t ref_ip_fast_csum(const uint8_t *iph, unsigned int ihl)
+{
+	uint32_t sum = ld32(iph);
+	uint64_t t;
+	uint32_t c;
+	unsigned int k;
+
+	if (ihl <= 4)
+		return (uint16_t)sum;
+
+	t = (uint64_t)sum + ld32(iph + 4);
+	sum = (uint32_t)t;
+	c = (uint32_t)(t >> 32);
+	for (k = 2; k < ihl; k++) {
+		t = (uint64_t)sum + ld32(iph + 4 * k) + c;
+		sum = (uint32_t)t;
+		c = (uint32_t)(t >> 32);
+	}
+	sum += c;                    /* adcl $0 (a carry out here is dropped) */
+
+	{
+		uint32_t r = (sum >> 16) + (sum & 0xFFFFu);   /* addw */
+		sum = (r & 0xFFFFu) + (r >> 16);               /* adcl $0 */
+	}
+	return (uint16_t)~sum;
+}
+
+/* RX verdict in the reference's order:
+ *   eth_in.c:35  ethertype == ETH_P_IP, else ARP/release (not checked)
+ *   ip_in.c:21-26  ip_len = ntohs(tot_len); ip_len < 20 -> ERROR
+ *   ip_in.c:35-36  ip_fast_csum(iph, ihl) != 0 -> ERROR
+ *   ip_in.c:47-50  version != 4 -> release, FALSE
+ *   ip_in.c:52-59  protocol: TCP -> ProcessTCPPacket, else not TCP
+ *   tcp_in.c:1221-1222  ip_len < (ihl+doff)<<2 -> ERROR
+ *   tcp_in.c:1231-1239  TCPCalcChecksum(tcph, doff*4+payloadlen = ip_len-ihl*4,
+ *                       saddr, daddr) != 0 -> tcph->check = 0, ERROR
+ * Reads the reference would make past `len` (undefined there) are DROP_TRUNC
+ * here; everything the reference can compute in-bounds is reproduced as is. */
+int ref_rx_verdict(uint8_t *f, uint32_t len, uint32_t flags)
+{
+	uint32_t ihl, version, proto, tot_len, doff, ts, tcplen;
+	uint8_t *iph, *tcph;
+
+	if (len < 14)
+		return REF_V_DROP_TRUNC;
+	if (ld16(f + 12) != 0x0008)              /* ntohs(h_proto) != 0x0800 */
+		return REF_V_NOT_IPV4;
+	if (len < 34)
+		return REF_V_DROP_TRUNC;
+	iph = f + 14;
+	ihl = iph[0] & 0x0F;
+	version = iph[0] >> 4;
+	tot_len = bswap16((uint16_t)ld16(iph + 2));
+	proto = iph[9];
+	if (tot_len < 20)
+		return REF_V_DROP_IPLEN;
+	if (ihl >= 5 && 14 + 4 * ihl > len)
+		return REF_V_DROP_TRUNC;
+	if (ref_ip_fast_csum(iph, ihl) != 0)
+		return REF_V_DROP_IPCSUM;
+	if (version != 4)
+		return REF_V_NOT_V4;
+	if (proto != 6)
+		return REF_V_NOT_TCP;
+	ts = 14 + 4 * ihl;
+	if (ts + 13 > len)                       /* doff byte lies past the frame */
+		return REF_V_DROP_TRUNC;
+	tcph = f + ts;
+	doff = tcph[12] >> 4;
+	if (tot_len < 4 * (ihl + doff))
+		return REF_V_DROP_TCPLEN;
+	if (14 + tot_len > len)
+		return REF_V_DROP_TRUNC;
+	tcplen = tot_len - 4 * ihl;
+	if (ref_tcp_calc_checksum(tcph, (uint16_t)tcplen, ld32(iph + 12),
+	                          ld32(iph + 16)) != 0) {
+		if (flags & REF_VF_ZERO_BAD_TCP_CHECK) {
+			tcph[16] = 0;
+			tcph[17] = 0;
+		}
+		return REF_V_DROP_TCPCSUM;
+	}
+	return REF_V_ACCEPT;
+}
+
+/* TX fill, mTCP order: IPOutput sets iph->check = 0 then stores
+ * ip_fast_csum(iph, ihl) (ip_out.c:153, :172); SendTCPPacket memsets the TCP
+ * header (check = 0, tcp_out.c:244) and stores TCPCalcChecksum(tcph,
+ * 20+optlen+payloadlen = tot_len - ihl*4, saddr, daddr) (tcp_out.c:323-333).
+ * Non-TCP IPv4 frames get only the IP check (ICMP: ip_out.c:90-92,100). */
+int ref_tx_fill(uint8_t *f, uint32_t len, uint32_t *csums)
+{
+	uint32_t ihl, proto, tot_len, ts;
+	uint16_t ipc, tcpc;
+	uint8_t *iph, *tcph;
+
+	if (csums)
+		*csums = 0;
+	if (len < 14 || ld16(f + 12) != 0x0008)
+		return REF_TX_NOT_IPV4;
+	if (len < 34)
+		return REF_TX_BAD_HDR;
+	iph = f + 14;
+	ihl = iph[0] & 0x0F;
+	if (ihl < 5 || 14 + 4 * ihl > len)
+		return REF_TX_BAD_HDR;
+	tot_len = bswap16((uint16_t)ld16(iph + 2));
+	proto = iph[9];
+
+	iph[10] = 0;
+	iph[11] = 0;
+	ipc = ref_ip_fast_csum(iph, ihl);
+	memcpy(iph + 10, &ipc, 2);
+	if (csums)
+		*csums = ipc;
+	if (proto != 6)
+		return REF_TX_IP_ONLY;
+	ts = 4 * ihl;
+	if (tot_len < ts + 20 || 14 + tot_len > len)
+		return REF_TX_BAD_TCPLEN;
+	tcph = iph + ts;
+	tcph[16] = 0;
+	tcph[17] = 0;
+	tcpc = ref_tcp_calc_checksum(tcph, (uint16_t)(tot_len - ts), ld32(iph + 12),
+	                             ld32(iph + 16));
+	memcpy(tcph + 16, &tcpc, 2);
+	if (csums)
+		*csums = (uint32_t)ipc | ((uint32_t)tcpc << 16);
+	return REF_TX_OK;
+}
+
+static int desc_ok(uint64_t buf_bytes, uint64_t off, uint32_t len)
+{
+	return (off & 15) == 0 && off <= buf_bytes && len <= buf_bytes - off;
+}
+
+void ref_verify_batch(uint8_t *buf, uint64_t buf_bytes, const uint64_t *off,
+                      const uint16_t *len, uint32_t n, uint8_t *verdict,
+                      uint32_t flags)
+{
+	uint32_t i;
+	for (i = 0; i < n; i++)
+		verdict[i] = desc_ok(buf_bytes, off[i], len[i])
+		                 ? (uint8_t)ref_rx_verdict(buf + off[i], len[i], flags)
+		                 : REF_V_BAD_DESC;
+}
+
+void ref_compute_batch(uint8_t *buf, uint64_t buf_bytes, const uint64_t *off,
+                       const uint16_t *len, uint32_t n, uint8_t *status,
+                       uint32_t *csums)
+{
+	uint32_t i;
+	for (i = 0; i < n; i++) {
+		int s;
+		if (!desc_ok(buf_bytes, off[i], len[i])) {
+			s = REF_TX_BAD_DESC;
+			if (csums)
+				csums[i] = 0;
+		} else {
+			s = ref_tx_fill(buf + off[i], len[i], csums ? &csums[i] : NULL);
+		}
+		if (status)
+			status[i] = (uint8_t)s;
+	}
+}
+
+void ref_verify_fixed(uint8_t *buf, uint64_t stride, uint32_t frame_len,
+                      uint32_t n, uint8_t *verdict, uint32_t flags)
+{
+	uint32_t i;
+	for (i = 0; i < n; i++)
+		verdict[i] = (uint8_t)ref_rx_verdict(buf + (uint64_t)i * stride, frame_len, flags);
+}
+
+void ref_compute_fixed(uint8_t *buf, uint64_t stride, uint32_t frame_len,
+                       uint32_t n, uint8_t *status, uint32_t *csums)
+{
+	uint32_t i;
+	for (i = 0; i < n; i++) {
+		int s = ref_tx_fill(buf + (uint64_t)i * stride, frame_len,
+		                    csums ? &csums[i] : NULL);
+		if (status)
+			status[i] = (uint8_t)s;
+	}
+}
+
+struct shard {
+	uint8_t *buf;
+	uint64_t stride;
+	uint32_t frame_len, lo, hi, flags;
+	uint8_t *out;
+	uint32_t *csums;
+	int compute;
+};
+
+static void *shard_main(void *arg)
+{
+	struct shard *s = (struct shard *)arg;
+	uint8_t *base = s->buf + (uint64_t)s->lo * s->stride;
+	uint32_t cnt = s->hi - s->lo;
+	if (s->compute)
+		ref_compute_fixed(base, s->stride, s->frame_len, cnt,
+		                  s->out ? s->out + s->lo : NULL,
+		                  s->csums ? s->csums + s->lo : NULL);
+	else
+		ref_verify_fixed(base, s->stride, s->frame_len, cnt, s->out + s->lo,
+		                 s->flags);
+	return NULL;
+}
+
+static void run_sharded(struct shard proto, uint32_t n, int threads)
+{
+	enum { MAXT = 256 };
+	pthread_t tid[MAXT];
+	int live[MAXT];
+	struct shard sh[MAXT];
+	int t;
+
+	if (threads < 1)
+		threads = 1;
+	if (threads > MAXT)
+		threads = MAXT;
+	for (t = 0; t < threads; t++) {
+		sh[t] = proto;
+		sh[t].lo = (uint32_t)((uint64_t)n * t / threads);
+		sh[t].hi = (uint32_t)((uint64_t)n * (t + 1) / threads);
+	}
+	for (t = 1; t < threads; t++) {
+		live[t] = pthread_create(&tid[t], NULL, shard_main, &sh[t]) == 0;
+		if (!live[t])
+			shard_main(&sh[t]);   /* could not spawn: run the shard inline */
+	}
+	shard_main(&sh[0]);
+	for (t = 1; t < threads; t++)
+		if (live[t])
+			pthread_join(tid[t], NULL);
+}
+
+void ref_verify_fixed_mt(uint8_t *buf, uint64_t stride, uint32_t frame_len,
+                         uint32_t n, uint8_t *verdict, uint32_t flags,
+                         int threads)
+{
+	struct shard p = {buf, stride, frame_len, 0, 0, flags, verdict, NULL, 0};
+	run_sharded(p, n, threads);
+}
+
+void ref_compute_fixed_mt(uint8_t *buf, uint64_t stride, uint32_t frame_len,
+                          uint32_t n, uint8_t *status, uint32_t *csums,
+                          int threads)
+{
+	struct shard p = {buf, stride, frame_len, 0, 0, 0, status, csums, 1};
+	run_sharded(p, n, threads);
+}
+
+void ref_tcp_checksum_batch(const uint8_t *buf, const uint64_t *off,
+                            const uint16_t *len, const uint32_t *saddr,
+                            const uint32_t *daddr, uint32_t n, uint16_t *out)
+{
+	uint32_t i;
+	for (i = 0; i < n; i++)
+		out[i] = ref_tcp_calc_checksum(buf + off[i], len[i], saddr[i], daddr[i]);
+}
+
+void ref_ip_checksum_batch(const uint8_t *buf, const uint64_t *off,
+                           const uint8_t *ihl, uint32_t n, uint16_t *out)
+{
+	uint32_t i;
+	for (i = 0; i < n; i++)
+		out[i] = ref_ip_fast_csum(buf + off[i], ihl[i]);
+}

@@ -1,0 +1,112 @@
+/*
+ * csum_ref.h -- CPU ORACLE for mTCP's software checksum path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing under oracle/ is part of the product:
+ * only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load or call it, and only as the checker / the timed CPU baseline.  The
+ * product path (mtcp_amd/, libmtcp_gpucsum.so) never links or calls it.
+ *
+ * This is a clean-room C restatement of the reference's algorithm (nothing
+ * copied).  Each function cites the reference file:line it follows:
+ *
+ *   ref_tcp_calc_checksum  mtcp/src/tcp_util.c:244-277   (TCPCalcChecksum)
+ *   ref_ip_fast_csum       io_engine/include/ps.h:66-95  (x86 ip_fast_csum,
+ *                          including the ihl<=4 early exit at :72-73)
+ *   ref_rx_verdict         mtcp/src/eth_in.c:35-47, ip_in.c:21-59,
+ *                          tcp_in.c:1208-1241            (RX verify order)
+ *   ref_tx_fill            mtcp/src/ip_out.c:143-173, tcp_out.c:244,323-333
+ *                          (TX: check fields zero when folded, then stored)
+ *
+ * Parity is pinned: tests/golden/ holds vectors produced by the reference's
+ * own compiled objects (oracle/_ref, built from /root/reference sources by
+ * oracle/Makefile), and tests/test_oracle_golden.py checks this file against
+ * them.  Verdict / status codes are numerically identical to the product's
+ * include/mtcp_gpucsum.h (a test asserts that).
+ */
+#ifndef MTCP_CSUM_REF_H
+#define MTCP_CSUM_REF_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* RX verdicts (same numbering as GCS_V_* in include/mtcp_gpucsum.h). */
+enum {
+	REF_V_ACCEPT = 0,       /* passes IP + TCP checksum: tcp_in.c:1243 onward */
+	REF_V_NOT_IPV4 = 1,     /* ethertype != 0x0800 (eth_in.c:35,39-46)        */
+	REF_V_DROP_IPLEN = 2,   /* tot_len < 20 (ip_in.c:25-26), ERROR            */
+	REF_V_DROP_IPCSUM = 3,  /* ip_fast_csum != 0 (ip_in.c:35-36), ERROR       */
+	REF_V_NOT_V4 = 4,       /* version != 4 (ip_in.c:47-50), released         */
+	REF_V_NOT_TCP = 5,      /* protocol != TCP (ip_in.c:52-59): IP csum only  */
+	REF_V_DROP_TCPLEN = 6,  /* ip_len < (ihl+doff)*4 (tcp_in.c:1221-1222)     */
+	REF_V_DROP_TCPCSUM = 7, /* TCPCalcChecksum != 0 (tcp_in.c:1231-1239)      */
+	REF_V_DROP_TRUNC = 8,   /* the reference would read past the frame (UB);
+	                           defined here as a drop                          */
+	REF_V_BAD_DESC = 9      /* descriptor misuse (offset/len outside buffer)  */
+};
+
+/* TX fill status (same numbering as GCS_TX_*). */
+enum {
+	REF_TX_OK = 0,          /* IP and TCP check written                       */
+	REF_TX_IP_ONLY = 1,     /* IPv4, not TCP: IP check written (ip_out.c:90)  */
+	REF_TX_NOT_IPV4 = 2,    /* untouched                                      */
+	REF_TX_BAD_HDR = 3,     /* ihl < 5 or header beyond frame: untouched      */
+	REF_TX_BAD_TCPLEN = 4,  /* IP written; TCP segment too short / truncated  */
+	REF_TX_BAD_DESC = 9
+};
+
+#define REF_VF_ZERO_BAD_TCP_CHECK 0x1u  /* tcp_in.c:1237 side effect */
+
+/* TCPCalcChecksum(buf, len, saddr, daddr): buf must be readable for
+ * len (+1 if odd: the reference reads the whole last halfword, tcp_util.c:262) */
+uint16_t ref_tcp_calc_checksum(const uint8_t *buf, uint16_t len,
+                               uint32_t saddr, uint32_t daddr);
+
+/* ip_fast_csum(iph, ihl), x86 semantics (ps.h:66-95). */
+uint16_t ref_ip_fast_csum(const uint8_t *iph, unsigned int ihl);
+
+/* One RX frame: verdict (REF_V_*).  May write tcph->check = 0 when flags
+ * has REF_VF_ZERO_BAD_TCP_CHECK and the verdict is DROP_TCPCSUM. */
+int ref_rx_verdict(uint8_t *frame, uint32_t len, uint32_t flags);
+
+/* One TX frame: fills iph->check / tcph->check in place; returns REF_TX_*.
+ * If csums != NULL it receives ip | tcp << 16 of what was written. */
+int ref_tx_fill(uint8_t *frame, uint32_t len, uint32_t *csums);
+
+/* Batches over a buffer with per-frame byte offsets and lengths. */
+void ref_verify_batch(uint8_t *buf, uint64_t buf_bytes, const uint64_t *off,
+                      const uint16_t *len, uint32_t n, uint8_t *verdict,
+                      uint32_t flags);
+void ref_compute_batch(uint8_t *buf, uint64_t buf_bytes, const uint64_t *off,
+                       const uint16_t *len, uint32_t n, uint8_t *status,
+                       uint32_t *csums);
+
+/* Fixed-stride batches (frame i at buf + i*stride, length frame_len). */
+void ref_verify_fixed(uint8_t *buf, uint64_t stride, uint32_t frame_len,
+                      uint32_t n, uint8_t *verdict, uint32_t flags);
+void ref_compute_fixed(uint8_t *buf, uint64_t stride, uint32_t frame_len,
+                       uint32_t n, uint8_t *status, uint32_t *csums);
+
+/* Same, split over `threads` pthreads (independent frame shards, like
+ * mTCP's per-core threads).  Used by bench.py's cpu_baseline. */
+void ref_verify_fixed_mt(uint8_t *buf, uint64_t stride, uint32_t frame_len,
+                         uint32_t n, uint8_t *verdict, uint32_t flags,
+                         int threads);
+void ref_compute_fixed_mt(uint8_t *buf, uint64_t stride, uint32_t frame_len,
+                          uint32_t n, uint8_t *status, uint32_t *csums,
+                          int threads);
+
+/* Element-wise function batches (one call of the reference function per item). */
+void ref_tcp_checksum_batch(const uint8_t *buf, const uint64_t *off,
+                            const uint16_t *len, const uint32_t *saddr,
+                            const uint32_t *daddr, uint32_t n, uint16_t *out);
+void ref_ip_checksum_batch(const uint8_t *buf, const uint64_t *off,
+                           const uint8_t *ihl, uint32_t n, uint16_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

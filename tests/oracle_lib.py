@@ -1,0 +1,174 @@
+"""ctypes bindings for the CPU checkers under oracle/ (test infrastructure).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module.  The product (mtcp_amd/, libmtcp_gpucsum.so) never does.
+
+* ``Oracle``    -> oracle/liboracle_csum.so   (clean-room restatement)
+* ``RefHarness``-> oracle/_ref/libref_mtcp_csum.so (the reference's own
+  TCPCalcChecksum + ip_fast_csum, built from /root/reference by
+  oracle/Makefile; absent on a box where it was never built)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "liboracle_csum.so")
+REF_SO = os.path.join(ORACLE_DIR, "_ref", "libref_mtcp_csum.so")
+
+_u8p = C.POINTER(C.c_uint8)
+
+
+def _p(a: np.ndarray | None):
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def build_oracle() -> None:
+    if not os.path.exists(ORACLE_SO):
+        subprocess.run(["make", "-C", ORACLE_DIR, "all"], check=True,
+                       stdout=subprocess.DEVNULL)
+
+
+class Oracle:
+    def __init__(self):
+        build_oracle()
+        L = C.CDLL(ORACLE_SO)
+        L.ref_tcp_calc_checksum.restype = C.c_uint16
+        L.ref_tcp_calc_checksum.argtypes = [C.c_void_p, C.c_uint16, C.c_uint32, C.c_uint32]
+        L.ref_ip_fast_csum.restype = C.c_uint16
+        L.ref_ip_fast_csum.argtypes = [C.c_void_p, C.c_uint]
+        L.ref_rx_verdict.restype = C.c_int
+        L.ref_rx_verdict.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+        L.ref_tx_fill.restype = C.c_int
+        L.ref_tx_fill.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
+        L.ref_verify_batch.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
+                                       C.c_uint32, C.c_void_p, C.c_uint32]
+        L.ref_compute_batch.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
+                                        C.c_uint32, C.c_void_p, C.c_void_p]
+        L.ref_verify_fixed.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32,
+                                       C.c_void_p, C.c_uint32]
+        L.ref_compute_fixed.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32,
+                                        C.c_void_p, C.c_void_p]
+        L.ref_verify_fixed_mt.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32,
+                                          C.c_void_p, C.c_uint32, C.c_int]
+        L.ref_compute_fixed_mt.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32,
+                                           C.c_void_p, C.c_void_p, C.c_int]
+        L.ref_tcp_checksum_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                             C.c_void_p, C.c_uint32, C.c_void_p]
+        L.ref_ip_checksum_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                            C.c_void_p]
+        self.L = L
+
+    # -- element functions -------------------------------------------------
+    def tcp_calc_checksum(self, buf: bytes, length: int, saddr: int, daddr: int) -> int:
+        b = np.frombuffer(bytes(buf) + b"\0\0", dtype=np.uint8).copy()
+        return self.L.ref_tcp_calc_checksum(_p(b), length, saddr, daddr)
+
+    def ip_fast_csum(self, hdr: bytes, ihl: int) -> int:
+        b = np.frombuffer(bytes(hdr) + b"\0" * 64, dtype=np.uint8).copy()
+        return self.L.ref_ip_fast_csum(_p(b), ihl)
+
+    # -- batches ----------------------------------------------------------
+    def verify_batch(self, buf, off, lens, flags=0):
+        n = len(off)
+        out = np.zeros(n, dtype=np.uint8)
+        self.L.ref_verify_batch(_p(buf), buf.nbytes, _p(np.ascontiguousarray(off, np.uint64)),
+                                _p(np.ascontiguousarray(lens, np.uint16)), n, _p(out), flags)
+        return out
+
+    def compute_batch(self, buf, off, lens):
+        n = len(off)
+        st = np.zeros(n, dtype=np.uint8)
+        cs = np.zeros(n, dtype=np.uint32)
+        self.L.ref_compute_batch(_p(buf), buf.nbytes, _p(np.ascontiguousarray(off, np.uint64)),
+                                 _p(np.ascontiguousarray(lens, np.uint16)), n, _p(st), _p(cs))
+        return st, cs
+
+    def verify_fixed(self, buf, stride, frame_len, n, flags=0, threads=1):
+        out = np.zeros(n, dtype=np.uint8)
+        if threads == 1:
+            self.L.ref_verify_fixed(_p(buf), stride, frame_len, n, _p(out), flags)
+        else:
+            self.L.ref_verify_fixed_mt(_p(buf), stride, frame_len, n, _p(out), flags, threads)
+        return out
+
+    def compute_fixed(self, buf, stride, frame_len, n, threads=1, want=True):
+        st = np.zeros(n, dtype=np.uint8) if want else None
+        cs = np.zeros(n, dtype=np.uint32) if want else None
+        if threads == 1:
+            self.L.ref_compute_fixed(_p(buf), stride, frame_len, n, _p(st), _p(cs))
+        else:
+            self.L.ref_compute_fixed_mt(_p(buf), stride, frame_len, n, _p(st), _p(cs), threads)
+        return st, cs
+
+    def tcp_checksum_batch(self, buf, off, lens, saddr, daddr):
+        n = len(off)
+        out = np.zeros(n, dtype=np.uint16)
+        self.L.ref_tcp_checksum_batch(_p(buf), _p(np.ascontiguousarray(off, np.uint64)),
+                                      _p(np.ascontiguousarray(lens, np.uint16)),
+                                      _p(np.ascontiguousarray(saddr, np.uint32)),
+                                      _p(np.ascontiguousarray(daddr, np.uint32)), n, _p(out))
+        return out
+
+    def ip_checksum_batch(self, buf, off, ihl):
+        n = len(off)
+        out = np.zeros(n, dtype=np.uint16)
+        self.L.ref_ip_checksum_batch(_p(buf), _p(np.ascontiguousarray(off, np.uint64)),
+                                     _p(np.ascontiguousarray(ihl, np.uint8)), n, _p(out))
+        return out
+
+
+class RefHarness:
+    """The reference's own fold code (oracle/_ref).  ``available()`` is False
+    where it was never built (e.g. a GPU box fed a snapshot without it)."""
+
+    @staticmethod
+    def available() -> bool:
+        return os.path.exists(REF_SO)
+
+    def __init__(self):
+        L = C.CDLL(REF_SO)
+        L.refx_tcp_calc_checksum.restype = C.c_uint16
+        L.refx_tcp_calc_checksum.argtypes = [C.c_void_p, C.c_uint16, C.c_uint32, C.c_uint32]
+        L.refx_ip_fast_csum.restype = C.c_uint16
+        L.refx_ip_fast_csum.argtypes = [C.c_void_p, C.c_uint]
+        L.refx_rx_verdict.restype = C.c_int
+        L.refx_rx_verdict.argtypes = [C.c_void_p, C.c_uint32]
+        L.refx_tx_fill.restype = C.c_int
+        L.refx_tx_fill.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
+        L.refx_verify_fixed.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32,
+                                        C.c_void_p]
+        L.refx_compute_fixed.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32,
+                                         C.c_void_p]
+        L.refx_run_fixed_mt.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32,
+                                        C.c_void_p, C.c_int, C.c_int]
+        self.L = L
+
+    def tcp_calc_checksum_at(self, buf: np.ndarray, pos: int, length: int, saddr: int,
+                             daddr: int) -> int:
+        return self.L.refx_tcp_calc_checksum(C.c_void_p(buf.ctypes.data + pos), length,
+                                             saddr, daddr)
+
+    def ip_fast_csum_at(self, buf: np.ndarray, pos: int, ihl: int) -> int:
+        return self.L.refx_ip_fast_csum(C.c_void_p(buf.ctypes.data + pos), ihl)
+
+    def rx_verdict_at(self, buf: np.ndarray, pos: int, length: int) -> int:
+        return self.L.refx_rx_verdict(C.c_void_p(buf.ctypes.data + pos), length)
+
+    def tx_fill_at(self, buf: np.ndarray, pos: int, length: int) -> tuple[int, int]:
+        cs = C.c_uint32(0)
+        st = self.L.refx_tx_fill(C.c_void_p(buf.ctypes.data + pos), length, C.byref(cs))
+        return st, cs.value
+
+    def run_fixed(self, buf, stride, frame_len, n, compute, threads=1):
+        out = np.zeros(n, dtype=np.uint8)
+        self.L.refx_run_fixed_mt(_p(buf), stride, frame_len, n, _p(out), int(compute), threads)
+        return out

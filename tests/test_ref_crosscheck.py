@@ -1,0 +1,68 @@
+"""Oracle restatement vs. the reference's own compiled code, on fresh random
+inputs beyond the committed fixtures (skipped where oracle/_ref was never
+built, i.e. outside the build container)."""
+import numpy as np
+import pytest
+
+from mtcp_amd import synth
+from oracle_lib import Oracle, RefHarness
+
+pytestmark = pytest.mark.skipif(not RefHarness.available(),
+                                reason="oracle/_ref not built (needs /root/reference)")
+
+
+@pytest.fixture(scope="module")
+def both():
+    return Oracle(), RefHarness()
+
+
+def test_ip_fast_csum_random_and_carry_edges(both):
+    O, R = both
+    rng = np.random.default_rng(7)
+    n = 20000
+    buf = rng.integers(0, 256, size=n * 64 + 64, dtype=np.uint8)
+    # bias a third of the headers to words of all-ones / small values
+    for i in range(0, n, 3):
+        w = rng.choice(np.array([0xFFFFFFFF, 0xFFFFFFFE, 0xFFFF0000, 1, 0], dtype=np.uint64), 16)
+        buf[i * 64: i * 64 + 64] = np.frombuffer(w.astype("<u4").tobytes(), dtype=np.uint8)
+    ihl = rng.integers(0, 16, size=n).astype(np.uint8)
+    off = np.arange(n, dtype=np.uint64) * 64 + 2
+    got = O.ip_checksum_batch(buf, off, ihl)
+    exp = np.array([R.ip_fast_csum_at(buf, int(off[i]), int(ihl[i])) for i in range(n)],
+                   dtype=np.uint16)
+    np.testing.assert_array_equal(got, exp)
+
+
+def test_tcp_checksum_random(both):
+    O, R = both
+    rng = np.random.default_rng(8)
+    n = 3000
+    lens = rng.integers(0, 3000, size=n).astype(np.uint16)
+    off = np.zeros(n, dtype=np.uint64)
+    np.cumsum((lens[:-1].astype(np.uint64) + 18) // 16 * 16, out=off[1:])
+    buf = rng.integers(0, 256, size=int(off[-1]) + 4096, dtype=np.uint8)
+    sa = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+    da = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+    got = O.tcp_checksum_batch(buf, off, lens, sa, da)
+    exp = np.array([R.tcp_calc_checksum_at(buf, int(off[i]), int(lens[i]), int(sa[i]),
+                                           int(da[i])) for i in range(n)], dtype=np.uint16)
+    np.testing.assert_array_equal(got, exp)
+
+
+@pytest.mark.parametrize("frame_len", [64, 576, 1500])
+def test_fixed_frames_rx_tx(both, frame_len):
+    O, R = both
+    n = 4096
+    buf, stride = synth.fixed_frames(n, frame_len, seed=11 + frame_len)
+    b1, b2 = buf.copy(), buf.copy()
+    st1, _ = O.compute_fixed(b1, stride, frame_len, n)
+    st2 = R.run_fixed(b2, stride, frame_len, n, compute=True)
+    np.testing.assert_array_equal(st1, st2)
+    np.testing.assert_array_equal(b1, b2)
+    bad = synth.corrupt(b1, np.arange(n, dtype=np.uint64) * stride, np.full(n, frame_len),
+                        frac_log2=4, seed=3)
+    assert len(bad) > 0
+    v1 = O.verify_fixed(b1, stride, frame_len, n)
+    v2 = R.run_fixed(b1, stride, frame_len, n, compute=False)
+    np.testing.assert_array_equal(v1, v2)
+    assert (v1[bad] != 0).all() and (np.delete(v1, bad) == 0).all()
