@@ -1,0 +1,326 @@
+#!/usr/bin/env python3
+"""bench.py -- mTCP software checksum path on MI355X (BASELINE.json metric).
+
+One step = one TX pass (gcs compute: fill iph->check / tcph->check in place,
+ip_out.c:143-173, tcp_out.c:323-333) over a TX batch plus one RX pass (gcs
+verify: one verdict byte per frame, ip_in.c:21-59, tcp_in.c:1208-1241) over a
+separate RX batch, both device-resident in HBM.  Every frame-checksum counts
+as one packet: value = (TX frames + RX frames) x N_gpus x steps / time.
+
+Workload: N=1 -> C2, 1M x 1500 B frames per batch at stride
+1536; N>1 -> C4, 4M x 1500 B frames per GPU (32M at 8 GPUs), sharded by frame
+range with no collective (the only torch.distributed calls are the timing
+barrier and the max-over-ranks reduction).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = ("Gpkt/s + GiB/s checksummed (device-resident), 64B & 1500B frames, 1/2/4/8 GPU")
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip parameters)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--frames-per-gpu", type=int, default=0,
+                   help="default: 1M at N=1 (C2), 4M at N>1 (C4)")
+    p.add_argument("--frame-len", type=int, default=1500)
+    p.add_argument("--cpu-seconds", type=float, default=8.0,
+                   help="CPU-baseline time budget (rank 0, N=1 only); 0 disables")
+    p.add_argument("--cpu-sample", type=int, default=1 << 18,
+                   help="frames in the CPU-baseline sample")
+    p.add_argument("--no-extras", action="store_true",
+                   help="skip the 64 B (C1) and PCIe-inclusive side measurements")
+    return p.parse_args()
+
+
+def dist_setup(args):
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(world, x: float) -> float:
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def make_batches(ctx, n, frame_len, seed, torch):
+    """TX batch (checks zero) and RX batch (= filled TX + 1/1024 frames with one
+    byte flipped), both resident in HBM."""
+    from mtcp_amd import synth
+    tx, stride = synth.fixed_frames_device(n, frame_len, seed=seed)
+    stream = torch.cuda.current_stream().cuda_stream
+    rx = tx.clone()
+    ctx.compute_fixed(rx, stride, frame_len, n, stream=stream)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed ^ 0xBAD)
+    pick = torch.nonzero(torch.randint(0, 1024, (n,), device="cuda", generator=g) == 0)[:, 0]
+    pos = torch.randint(14, frame_len, (pick.numel(),), device="cuda", generator=g)
+    flip = torch.randint(1, 256, (pick.numel(),), device="cuda", generator=g).to(torch.uint8)
+    idx = pick * stride + pos
+    rx[idx] = rx[idx] ^ flip
+    torch.cuda.synchronize()
+    return tx, rx, stride, int(pick.numel())
+
+
+def time_steps(ctx, tx, rx, stride, frame_len, n, steps, warmup, world, torch):
+    stream = torch.cuda.current_stream().cuda_stream
+    verdict = torch.empty(n, dtype=torch.uint8, device="cuda")
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record()
+        ctx.compute_fixed(tx, stride, frame_len, n, stream=stream)
+        if ev is not None:
+            ev[1].record()
+        ctx.verify_fixed(rx, stride, frame_len, n, verdict, stream=stream)
+        if ev is not None:
+            ev[2].record()
+
+    for _ in range(warmup):
+        step()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier(world)
+    tx_ms = [e[0].elapsed_time(e[1]) for e in evs]
+    rx_ms = [e[1].elapsed_time(e[2]) for e in evs]
+    return t1 - t0, float(np.mean(tx_ms)), float(np.mean(rx_ms)), verdict
+
+
+def pmc_traffic(kernel_key: str):
+    """HBM bytes per launch for the dominant kernel from the committed
+    rocprofv3 PMC summary (profiles/pmc_summary.json, written by
+    profiles/collect_pmc.py with the gfx950 FETCH_SIZE x2 correction)."""
+    p = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        d = json.load(open(p))
+        return d["kernels"][kernel_key]["hbm_bytes_per_launch"]
+    except Exception:
+        return None
+
+
+def cpu_baseline(tx, rx, stride, frame_len, budget_s, sample, torch):
+    """The reference's own software path (oracle/_ref: mTCP's TCPCalcChecksum +
+    ip_fast_csum, reference compile flags) on host cores over a bounded sample
+    of the SAME frames; the clean-room port if _ref was never built."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_lib import Oracle, RefHarness
+
+    m = min(sample, tx.numel() // stride)
+    tx_h = tx[: m * stride].cpu().numpy().copy()
+    rx_h = rx[: m * stride].cpu().numpy().copy()
+    kind = "reference" if RefHarness.available() else "port"
+    if kind == "reference":
+        R = RefHarness()
+        run = lambda buf, compute, thr: R.run_fixed(buf, stride, frame_len, m, compute, thr)  # noqa
+    else:
+        O = Oracle()
+
+        def run(buf, compute, thr):
+            if compute:
+                return O.compute_fixed(buf, stride, frame_len, m, threads=thr, want=False)
+            return O.verify_fixed(buf, stride, frame_len, m, threads=thr)
+
+    def measure(threads, budget):
+        rates = []
+        t_start = time.perf_counter()
+        while True:
+            t0 = time.perf_counter()
+            run(tx_h, True, threads)
+            run(rx_h, False, threads)
+            dt = time.perf_counter() - t0
+            rates.append(2 * m / dt)
+            if time.perf_counter() - t_start >= budget and len(rates) >= 3:
+                break
+        return float(np.median(rates)), len(rates)
+
+    r1, reps1 = measure(1, budget_s)
+    threads = max(1, min(16, (os.cpu_count() or 1)))
+    rmt, repsmt = measure(threads, max(1.0, budget_s / 4))
+    try:
+        cpu_model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo")
+                         if l.startswith("model name"))
+    except Exception:
+        cpu_model = "unknown"
+    return {
+        "value": r1 / 1e9, "unit": "Gpkt/s", "cores": 1, "kind": kind,
+        "sample": f"{m} TX + {m} RX frames of the bench batches ({frame_len} B, stride {stride}),"
+                  f" median of {reps1} passes, 1 pinned-free thread",
+        "gib_per_s": r1 * frame_len / 2**30,
+        "multi_core": {"value": rmt / 1e9, "unit": "Gpkt/s", "cores": threads,
+                       "gib_per_s": rmt * frame_len / 2**30, "passes": repsmt},
+        "cpu_model": cpu_model,
+    }
+
+
+def c1_small_frames(ctx, torch, steps=20):
+    """C1 side measurement: 1M x 64 B frames, IP+TCP verify, device-resident."""
+    from mtcp_amd import synth
+    n, L = 1 << 20, 64
+    buf, stride = synth.fixed_frames_device(n, L, seed=0x6401)
+    stream = torch.cuda.current_stream().cuda_stream
+    ctx.compute_fixed(buf, stride, L, n, stream=stream)
+    v = torch.empty(n, dtype=torch.uint8, device="cuda")
+    for _ in range(3):
+        ctx.verify_fixed(buf, stride, L, n, v, stream=stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(steps):
+        ctx.verify_fixed(buf, stride, L, n, v, stream=stream)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    assert int((v != 0).sum()) == 0
+    return {"workload": "C1: 1M x 64B verify, stride 64, back-to-back launches",
+            "ms_per_launch": ms, "gpkt_per_s": n / ms / 1e6,
+            "gib_per_s": n * L / (ms * 1e-3) / 2**30,
+            "hbm_gbs_algorithmic": n * (L + 1) / (ms * 1e-3) / 1e9}
+
+
+def pcie_inclusive(gcs, torch, frame_len=1500, n=1 << 18):
+    """Host-resident frames -> gcs_verify (pinned staging, H2D, kernel, D2H of
+    verdicts).  Reported beside the device-resident number, never as `value`."""
+    from mtcp_amd import synth
+    buf, stride = synth.fixed_frames(n, frame_len, seed=77)
+    off = np.arange(n, dtype=np.uint64) * stride
+    lens = np.full(n, frame_len, dtype=np.uint16)
+    with gcs.Context(torch.cuda.current_device(), max_frames=1 << 16, max_bytes=96 << 20) as c:
+        c.compute_host(buf, off, lens)
+        c.verify_host(buf, off, lens)
+        t0 = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            v = c.verify_host(buf, off, lens)
+        dt = (time.perf_counter() - t0) / reps
+    assert int((v != 0).sum()) == 0
+    return {"workload": f"{n} x {frame_len}B host frames, gcs_verify (gather->pinned->H2D->"
+                        "kernel->D2H verdicts)",
+            "gpkt_per_s": n / dt / 1e9, "gib_per_s": n * frame_len / dt / 2**30}
+
+
+def main():
+    args = parse()
+    import torch
+    from mtcp_amd import gpucsum
+
+    world, rank, local = dist_setup(args)
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    n = args.frames_per_gpu or ((1 << 20) if world == 1 else (1 << 22))
+    L = args.frame_len
+    ctx = gpucsum.Context(local)
+    tx, rx, stride, nbad = make_batches(ctx, n, L, 0x6D746370 ^ rank, torch)
+
+    elapsed, tx_ms, rx_ms, verdict = time_steps(ctx, tx, rx, stride, L, n, args.steps,
+                                                args.warmup, world, torch)
+    bad_seen = int((verdict != 0).sum())
+    if bad_seen != nbad:
+        raise SystemExit(f"rank {rank}: verify flagged {bad_seen} frames, {nbad} corrupted")
+    t = max_over_ranks(world, elapsed)
+
+    frames = 2 * n * world * args.steps          # TX fills + RX verifies, all ranks
+    value = frames / t / 1e9
+    gib = frames * L / t / 2**30
+    # dominant kernel's roofline (algorithmic bytes)
+    rx_bytes = n * (L + 1)
+    tx_bytes = n * (L + 4)
+    if rx_ms >= tx_ms:
+        kname, kms, kbytes = "verify", rx_ms, rx_bytes
+    else:
+        kname, kms, kbytes = "compute", tx_ms, tx_bytes
+    achieved = kbytes / (kms * 1e-3) / 1e9
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "Gpkt/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": t / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u16",
+        "data": "synthetic (seeded mTCP-shaped Eth/IPv4/TCP frames generated in HBM)",
+        "config": {
+            "workload": ("C2: 1M x 1500B frames, TX compute + RX verify per step" if world == 1
+                         and n == (1 << 20) and L == 1500 else
+                         f"C4 shard: {n} x {L}B frames per GPU, TX compute + RX verify per step"),
+            "frames_per_gpu": n, "frame_len": L, "stride": stride,
+            "parallelism": f"frame-shard x{world} (no collective)",
+        },
+        "gib_per_s": gib,
+        "roofline": {
+            "bound": "hbm", "kernel": f"k_fixed<32,3,{'true' if kname == 'compute' else 'false'},false> ({kname})",
+            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": pmc_traffic(f"{kname}_{L}"),
+            "bytes_per_launch_algorithmic": kbytes, "avg_launch_ms": kms,
+        },
+        "kernels_ms": {"compute": tx_ms, "verify": rx_ms},
+        "corrupted_frames_detected": bad_seen,
+    }
+    if rank == 0 and world == 1:
+        if args.cpu_seconds > 0:
+            line["cpu_baseline"] = cpu_baseline(tx, rx, stride, L, args.cpu_seconds,
+                                                args.cpu_sample, torch)
+        if not args.no_extras:
+            del tx, rx
+            torch.cuda.empty_cache()
+            line["c1_64B"] = c1_small_frames(ctx, torch)
+            line["pcie_inclusive"] = pcie_inclusive(gpucsum, torch)
+    ctx.close()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,167 @@
+/*
+ * mtcp_gpucsum.h -- C ABI of libmtcp_gpucsum.so: mTCP's software TCP/IP
+ * checksum path (the --disable-hwcsum branch) as batched MI355X (gfx950)
+ * HIP kernels.
+ *
+ * What each entry point replaces in the reference (/root/reference):
+ *
+ *   gcs_verify*        the per-frame RX checks of ProcessPacket / ProcessIPv4Packet /
+ *                      ProcessTCPPacket: eth_in.c:35, ip_in.c:21-59 (ip_fast_csum at
+ *                      :35) and tcp_in.c:1208-1241 (TCPCalcChecksum at :1231), one
+ *                      verdict byte per frame instead of one call per frame.
+ *   gcs_compute*       the TX folds of IPOutput / IPOutputStandalone (ip_out.c:153,172 /
+ *                      :82,100) and SendTCPPacket / SendTCPPacketStandalone
+ *                      (tcp_out.c:244,323-333 / :161,202-214), written in place.
+ *   gcs_tcp_checksum_dev  TCPCalcChecksum()   mtcp/src/tcp_util.c:244-277
+ *                         (declared mtcp/src/include/tcp_util.h:41-42), element-wise.
+ *   gcs_ip_checksum_dev   ip_fast_csum()      io_engine/include/ps.h:66-95, element-wise,
+ *                         x86 semantics incl. the ihl<=4 early exit (:72-73).
+ *
+ * The io_module_func plugin that sits on top of this ABI (the drop-in under
+ * mtcp/src, io_module.h:60-72) is declared in gpucsum_io_module.h.
+ *
+ * Conventions
+ *   - Plain C types only; every function returns GCS_OK (0) or a negative
+ *     GCS_E* code; no C++ exceptions cross the ABI.
+ *   - Byte order: frames are raw wire bytes.  Checksum values are returned
+ *     exactly as the reference returns them (uint16_t as stored by a
+ *     little-endian host, i.e. the value memcpy'd into iph->check).
+ *   - Batch layout in device memory ("HBM batch"): frame i at byte offset
+ *     off[i] of one buffer of frames_bytes bytes, length len[i].  off[i] must
+ *     be a multiple of 16 (the pslib packing uses 64, io_engine/lib/pslib.c:146);
+ *     a descriptor that is misaligned or reaches past frames_bytes yields
+ *     GCS_V_BAD_DESC / GCS_TX_BAD_DESC for that frame and is never read.
+ *   - Fixed-stride layout: frame i at i*stride (stride % 16 == 0), all of
+ *     length frame_len <= stride.
+ *   - *_dev functions take device pointers and are asynchronous on `stream`
+ *     (a hipStream_t; NULL = the context's own stream).  Host functions are
+ *     synchronous and stage through the context's pinned buffers.
+ *   - Threading: a context belongs to one host thread (mTCP: one per core,
+ *     core.c:1153-1245).  Different contexts may be used concurrently.
+ */
+#ifndef MTCP_GPUCSUM_H
+#define MTCP_GPUCSUM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GCS_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------- */
+#define GCS_OK        0
+#define GCS_EINVAL   (-1)   /* bad argument (NULL, n > capacity, stride < frame_len ...) */
+#define GCS_ENODEV   (-2)   /* no HIP device / device index out of range           */
+#define GCS_ENOMEM   (-3)   /* device or pinned host allocation failed             */
+#define GCS_EHIP     (-4)   /* a HIP runtime call failed (see gcs_last_hip_error)  */
+#define GCS_ERANGE   (-5)   /* batch larger than the context was created for       */
+
+/* ---- RX verdicts: one byte per frame ------------------------------------
+ * Same decision order as the reference (see csum order above).  "ERROR"
+ * verdicts are the ones mTCP returns ERROR for and counts in
+ * nstat.rx_errors (eth_in.c:49-53, core.c:796-799). */
+#define GCS_V_ACCEPT        0  /* IP + TCP checksums pass (tcp_in.c:1243 onward)        */
+#define GCS_V_NOT_IPV4      1  /* ethertype != 0x0800: ARP / release (eth_in.c:39-46)  */
+#define GCS_V_DROP_IPLEN    2  /* ERROR: tot_len < 20 (ip_in.c:25-26)                   */
+#define GCS_V_DROP_IPCSUM   3  /* ERROR: ip_fast_csum != 0 (ip_in.c:35-36)              */
+#define GCS_V_NOT_V4        4  /* version != 4: released (ip_in.c:47-50)                */
+#define GCS_V_NOT_TCP       5  /* IPv4, IP csum ok, protocol != TCP (ip_in.c:52-59)     */
+#define GCS_V_DROP_TCPLEN   6  /* ERROR: ip_len < (ihl+doff)*4 (tcp_in.c:1221-1222)      */
+#define GCS_V_DROP_TCPCSUM  7  /* ERROR: TCPCalcChecksum != 0 (tcp_in.c:1231-1239)      */
+#define GCS_V_DROP_TRUNC    8  /* ERROR: the reference would read past the frame (UB
+                                  there: tcp_in.c:1231 folds tot_len bytes regardless)  */
+#define GCS_V_BAD_DESC      9  /* ERROR: descriptor misaligned / outside the buffer     */
+#define GCS_V_IS_ERROR(v) ((v) == 2 || (v) == 3 || (v) >= 6)
+
+/* verify flags */
+#define GCS_VF_ZERO_BAD_TCP_CHECK 0x1u  /* reproduce tcp_in.c:1237: tcph->check = 0 on
+                                           a TCP checksum failure (writes the frame)   */
+
+/* ---- TX status: one byte per frame (optional output) ------------------- */
+#define GCS_TX_OK           0  /* iph->check and tcph->check written                   */
+#define GCS_TX_IP_ONLY      1  /* IPv4, not TCP: iph->check written (ip_out.c:90-92)   */
+#define GCS_TX_NOT_IPV4     2  /* untouched                                            */
+#define GCS_TX_BAD_HDR      3  /* ihl < 5 or IP header past the frame: untouched       */
+#define GCS_TX_BAD_TCPLEN   4  /* iph->check written; tot_len < ihl*4+20 or the segment
+                                  runs past the frame: TCP untouched                    */
+#define GCS_TX_BAD_DESC     9  /* descriptor misaligned / outside the buffer           */
+
+/* compute flags */
+#define GCS_CF_NO_INPLACE   0x1u  /* do not write the frames; only fill csums[]         */
+
+typedef struct gcs_ctx gcs_ctx;
+
+/* ---- library / context ------------------------------------------------- */
+int         gcs_abi_version(void);
+const char *gcs_strerror(int code);
+const char *gcs_last_hip_error(void);          /* thread-local, "" if none        */
+int         gcs_device_count(int *count);
+
+/* Create a context on HIP device `device` with its own non-blocking stream.
+ * max_frames / max_bytes size the staging used by the host-memory entry points
+ * (0 = no staging: only the *_dev functions may be used). */
+int gcs_ctx_create(gcs_ctx **out, int device, uint32_t max_frames, uint64_t max_bytes);
+int gcs_ctx_destroy(gcs_ctx *ctx);
+int gcs_ctx_device(const gcs_ctx *ctx, int *device);
+int gcs_ctx_stream(const gcs_ctx *ctx, void **stream);   /* hipStream_t */
+int gcs_sync(gcs_ctx *ctx);                               /* wait for ctx stream */
+
+/* Pinned host memory (hipHostMalloc) for zero-staging host batches. */
+int gcs_host_alloc(void **p, uint64_t bytes);
+int gcs_host_free(void *p);
+/* Device memory on the context's device. */
+int gcs_dev_alloc(gcs_ctx *ctx, void **p, uint64_t bytes);
+int gcs_dev_free(gcs_ctx *ctx, void *p);
+
+/* ---- device-resident batches (async on stream) ------------------------ */
+int gcs_verify_fixed_dev(gcs_ctx *ctx, uint8_t *d_frames, uint64_t stride,
+                         uint32_t frame_len, uint32_t n, uint8_t *d_verdict,
+                         uint32_t flags, void *stream);
+int gcs_compute_fixed_dev(gcs_ctx *ctx, uint8_t *d_frames, uint64_t stride,
+                          uint32_t frame_len, uint32_t n, uint8_t *d_status,
+                          uint32_t *d_csums, uint32_t flags, void *stream);
+int gcs_verify_dev(gcs_ctx *ctx, uint8_t *d_frames, uint64_t frames_bytes,
+                   const uint64_t *d_off, const uint16_t *d_len, uint32_t n,
+                   uint8_t *d_verdict, uint32_t flags, void *stream);
+int gcs_compute_dev(gcs_ctx *ctx, uint8_t *d_frames, uint64_t frames_bytes,
+                    const uint64_t *d_off, const uint16_t *d_len, uint32_t n,
+                    uint8_t *d_status, uint32_t *d_csums, uint32_t flags,
+                    void *stream);
+
+/* Element-wise reference functions.  Item i: buf + off[i] (off[i] even, the
+ * reference takes a uint16_t*), the bytes it reads must lie inside
+ * buf_bytes (else out[i] = 0 and the item is skipped).
+ *   tcp: out[i] = TCPCalcChecksum(buf+off[i], len[i], saddr[i], daddr[i])
+ *   ip : out[i] = ip_fast_csum(buf+off[i], ihl[i] & 15)                  */
+int gcs_tcp_checksum_dev(gcs_ctx *ctx, const uint8_t *d_buf, uint64_t buf_bytes,
+                         const uint64_t *d_off, const uint16_t *d_len,
+                         const uint32_t *d_saddr, const uint32_t *d_daddr,
+                         uint32_t n, uint16_t *d_out, void *stream);
+int gcs_ip_checksum_dev(gcs_ctx *ctx, const uint8_t *d_buf, uint64_t buf_bytes,
+                        const uint64_t *d_off, const uint8_t *d_ihl, uint32_t n,
+                        uint16_t *d_out, void *stream);
+
+/* ---- host-memory batches (synchronous) --------------------------------
+ * frames[off[i] .. off[i]+len[i]) in host memory (any alignment).  The
+ * context gathers them into pinned staging at 64 B-aligned slots, copies to
+ * HBM, runs the kernel and copies back only verdicts (RX) or the 4 bytes of
+ * check fields per frame (TX, scattered back into `frames` on the host). */
+int gcs_verify(gcs_ctx *ctx, uint8_t *frames, const uint64_t *off,
+               const uint16_t *len, uint32_t n, uint8_t *verdict, uint32_t flags);
+int gcs_compute(gcs_ctx *ctx, uint8_t *frames, const uint64_t *off,
+                const uint16_t *len, uint32_t n, uint8_t *status, uint32_t *csums);
+
+/* Pointer-vector variants (one pointer per frame, as an I/O module holds
+ * them: rte_mbuf data pointers, dpdk_module.c:517-548 / 399-436). */
+int gcs_verify_ptrs(gcs_ctx *ctx, uint8_t *const *pkts, const uint16_t *len,
+                    uint32_t n, uint8_t *verdict, uint32_t flags);
+int gcs_compute_ptrs(gcs_ctx *ctx, uint8_t *const *pkts, const uint16_t *len,
+                     uint32_t n, uint8_t *status, uint32_t *csums);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MTCP_GPUCSUM_H */

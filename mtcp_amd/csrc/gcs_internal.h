@@ -1,0 +1,27 @@
+// gcs_internal.h -- launchers shared between gcs_kernels.hip and gcs_api.cpp.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mtcp_gpucsum.h"
+
+namespace gcs {
+
+hipError_t launch_verify_fixed(uint8_t* frames, uint64_t stride, uint32_t frame_len, uint32_t n,
+                               uint8_t* verdict, uint32_t flags, hipStream_t s);
+hipError_t launch_compute_fixed(uint8_t* frames, uint64_t stride, uint32_t frame_len, uint32_t n,
+                                uint8_t* status, uint32_t* csums, uint32_t flags, hipStream_t s);
+hipError_t launch_verify_desc(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
+                              const uint16_t* len, uint32_t n, uint8_t* verdict, uint32_t flags,
+                              hipStream_t s);
+hipError_t launch_compute_desc(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
+                               const uint16_t* len, uint32_t n, uint8_t* status, uint32_t* csums,
+                               uint32_t flags, hipStream_t s);
+hipError_t launch_tcp_fn(const uint8_t* buf, uint64_t buf_bytes, const uint64_t* off,
+                         const uint16_t* len, const uint32_t* saddr, const uint32_t* daddr,
+                         uint32_t n, uint16_t* out, hipStream_t s);
+hipError_t launch_ip_fn(const uint8_t* buf, uint64_t buf_bytes, const uint64_t* off,
+                        const uint8_t* ihl, uint32_t n, uint16_t* out, hipStream_t s);
+
+}  // namespace gcs

@@ -142,3 +142,29 @@ def corrupt(buf: np.ndarray, off: np.ndarray, lengths: np.ndarray, frac_log2: in
         flip = int(rng.integers(1, 256))
         buf[int(off[i]) + pos] ^= flip
     return pick
+
+
+def fixed_frames_device(n: int, frame_len: int, stride: int | None = None,
+                        seed: int = DEFAULT_SEED, device: str = "cuda"):
+    """Same frame template as ``fixed_frames`` but generated directly in HBM
+    with torch (bench.py: 1.5-6 GB per GPU never touches the host).  Returns
+    (uint8 tensor of n*stride bytes, stride).  Check fields are 0."""
+    import torch
+
+    stride = stride or stride_for(frame_len)
+    assert stride >= frame_len and stride % 16 == 0 and frame_len >= 54
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    buf = torch.randint(0, 256, (n * stride,), dtype=torch.uint8, device=device, generator=g)
+    b = buf.view(n, stride)
+    tot = frame_len - ETH_LEN
+    doff = 5 if frame_len < 66 else 8
+    fixed = {12: 0x08, 13: 0x00, 14: 0x45, 15: 0, 16: tot >> 8, 17: tot & 0xFF, 20: 0x40,
+             21: 0, 22: 64, 23: 6, 24: 0, 25: 0, 46: doff << 4, 47: 0x10, 50: 0, 51: 0,
+             52: 0, 53: 0}
+    if doff == 8:
+        fixed.update({54: 1, 55: 1, 56: 8, 57: 10})
+    cols = torch.tensor(sorted(fixed), device=device)
+    vals = torch.tensor([fixed[k] for k in sorted(fixed)], dtype=torch.uint8, device=device)
+    b[:, cols] = vals
+    return buf, stride

@@ -129,7 +129,7 @@ int ref_rx_verdict(uint8_t *f, uint32_t len, uint32_t flags)
 	tcplen = tot_len - 4 * ihl;
 	if (ref_tcp_calc_checksum(tcph, (uint16_t)tcplen, ld32(iph + 12),
 	                          ld32(iph + 16)) != 0) {
-		if (flags & REF_VF_ZERO_BAD_TCP_CHECK) {
+		if ((flags & REF_VF_ZERO_BAD_TCP_CHECK) && ts + 18 <= len) {
 			tcph[16] = 0;
 			tcph[17] = 0;
 		}

@@ -1,0 +1,85 @@
+"""The C-ABI boundary without a GPU: the library loads, exports every entry
+point include/*.h declares, verdict/status numbering matches the oracle, and
+argument validation fails loudly (no compute call is made)."""
+import ctypes as C
+import glob
+import os
+import re
+import subprocess
+
+import pytest
+
+from mtcp_amd import gpucsum
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    names = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w \*]*?\b((?:gcs|gpucsum)_\w+)\s*\(", src, re.M):
+            names.add(m.group(1))
+        for m in re.finditer(r"^extern\s+[\w ]+\s+((?:gcs|gpucsum)_\w+)\s*;", src, re.M):
+            names.add(m.group(1))
+    return sorted(names)
+
+
+def exported_symbols(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True,
+                         check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
+def test_library_exports_every_declared_symbol():
+    names = declared_functions()
+    assert "gcs_verify_fixed_dev" in names and "gcs_tcp_checksum_dev" in names
+    syms = exported_symbols(gpucsum.LIB_PATH)
+    missing = [n for n in names if n not in syms]
+    assert not missing, missing
+    L = gpucsum.lib()
+    for n in names:
+        assert getattr(L, n) is not None
+
+
+def test_abi_version_and_strerror():
+    L = gpucsum.lib()
+    assert L.gcs_abi_version() == gpucsum.K["GCS_ABI_VERSION"] == 1
+    assert L.gcs_strerror(-1) == b"invalid argument"
+    assert L.gcs_strerror(0) == b"ok"
+
+
+def test_codes_match_oracle():
+    src = open(os.path.join(ROOT, "oracle", "csum_ref.h")).read()
+    ref = {m.group(1): int(m.group(2)) for m in re.finditer(r"REF_(V_\w+|TX_\w+)\s*=\s*(\d+)", src)}
+    K = gpucsum.K
+    for k, v in ref.items():
+        assert K["GCS_" + k] == v, k
+    assert K["GCS_VF_ZERO_BAD_TCP_CHECK"] == 1
+
+
+def test_argument_validation_without_gpu():
+    L = gpucsum.lib()
+    # NULL context / bad stride are rejected before any HIP call
+    assert L.gcs_verify_fixed_dev(None, None, 64, 64, 1, None, 0, None) == gpucsum.K["GCS_EINVAL"]
+    assert L.gcs_ctx_destroy(None) == gpucsum.K["GCS_EINVAL"]
+    p = C.c_void_p()
+    assert L.gcs_ctx_create(None, 0, 0, 0) == gpucsum.K["GCS_EINVAL"]
+    assert L.gcs_device_count(None) == gpucsum.K["GCS_EINVAL"]
+
+
+def test_no_device_here_is_reported_not_faked():
+    """Without a GPU, creating a context fails with an error code: there is
+    no CPU fallback behind the ABI."""
+    if gpucsum.device_count() > 0:
+        pytest.skip("a GPU is present")
+    with pytest.raises(gpucsum.GcsError):
+        gpucsum.Context(0)
+
+
+def test_product_does_not_link_oracle():
+    out = subprocess.run(["ldd", gpucsum.LIB_PATH], capture_output=True, text=True).stdout
+    assert "oracle" not in out and "ref_mtcp" not in out
+    syms = exported_symbols(gpucsum.LIB_PATH)
+    assert not any(s.startswith(("ref_", "refx_", "TCPCalcChecksum")) for s in syms)

@@ -1,0 +1,373 @@
+"""Parity of the HIP path (through the C ABI) with the oracle and with the
+reference's golden vectors.  Bit-exact: this is integer/byte work.
+
+Runs on a real MI355X (`-m gpu`).  The oracle (oracle/liboracle_csum.so) is
+the checker only; every result under test comes from libmtcp_gpucsum.so.
+"""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from mtcp_amd import gpucsum, synth
+from oracle_lib import Oracle
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+K = gpucsum.K
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need a GPU (no CPU fallback exists)")
+    return torch
+
+
+@pytest.fixture(scope="module")
+def ctx(torch_dev):
+    c = gpucsum.Context(0, max_frames=1 << 16, max_bytes=64 << 20)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def O():
+    return Oracle()
+
+
+def load(name):
+    with np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False) as d:
+        return {k: d[k] for k in d.files}
+
+
+def dev(torch, a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def host(t):
+    return t.cpu().numpy()
+
+
+# ---------------------------------------------------------------------------
+# golden vectors from the reference itself
+
+def test_golden_tcp_fn(torch_dev, ctx):
+    t = torch_dev
+    d = load("tcp_fn")
+    n = len(d["off"])
+    out = t.zeros(n, dtype=t.int16, device="cuda")
+    ctx.tcp_checksum(dev(t, d["buf"]), dev(t, d["off"].view(np.int64)), dev(t, d["len"].view(np.int16)),
+                     dev(t, d["saddr"].view(np.int32)), dev(t, d["daddr"].view(np.int32)), n, out)
+    ctx.sync()
+    np.testing.assert_array_equal(host(out).view(np.uint16), d["expect"])
+
+
+def test_golden_ip_fn(torch_dev, ctx):
+    t = torch_dev
+    d = load("ip_fn")
+    n = len(d["off"])
+    out = t.zeros(n, dtype=t.int16, device="cuda")
+    ctx.ip_checksum(dev(t, d["buf"]), dev(t, d["off"].view(np.int64)), dev(t, d["ihl"]), n, out)
+    ctx.sync()
+    np.testing.assert_array_equal(host(out).view(np.uint16), d["expect"])
+
+
+@pytest.mark.parametrize("flags", [0, 1])
+def test_golden_frames_rx(torch_dev, ctx, O, flags):
+    t = torch_dev
+    d = load("frames_rx")
+    n = len(d["off"])
+    buf = dev(t, d["buf"])
+    v = t.zeros(n, dtype=t.uint8, device="cuda")
+    ctx.verify(buf, dev(t, d["off"].view(np.int64)), dev(t, d["len"].view(np.int16)), n, v,
+               flags=flags)
+    ctx.sync()
+    np.testing.assert_array_equal(host(v), d["expect"])
+    # tcp_in.c:1237 side effect, exactly as the oracle applies it
+    ref = d["buf"].copy()
+    O.verify_batch(ref, d["off"], d["len"], flags=flags)
+    np.testing.assert_array_equal(host(buf), ref)
+
+
+def test_golden_frames_tx(torch_dev, ctx):
+    t = torch_dev
+    d = load("frames_tx")
+    n = len(d["off"])
+    buf = dev(t, d["buf"])
+    st = t.zeros(n, dtype=t.uint8, device="cuda")
+    cs = t.zeros(n, dtype=t.int32, device="cuda")
+    ctx.compute(buf, dev(t, d["off"].view(np.int64)), dev(t, d["len"].view(np.int16)), n, st, cs)
+    ctx.sync()
+    np.testing.assert_array_equal(host(st), d["status"])
+    np.testing.assert_array_equal(host(cs).view(np.uint32), d["csums"])
+    assert hashlib.sha256(host(buf).tobytes()).digest() == d["filled_sha256"].tobytes()
+
+
+# ---------------------------------------------------------------------------
+# fixed-stride kernels: every (G, U) dispatch class vs the oracle
+
+FIXED_LENS = [54, 60, 64, 100, 128, 200, 256, 400, 576, 900, 1024, 1500, 1514, 2000, 4000, 9000]
+
+
+@pytest.mark.parametrize("frame_len", FIXED_LENS)
+def test_fixed_compute_then_verify(torch_dev, ctx, O, frame_len):
+    t = torch_dev
+    n = 3000 if frame_len < 4000 else 600
+    buf, stride = synth.fixed_frames(n, frame_len, seed=frame_len)
+    ref = buf.copy()
+    rst, rcs = O.compute_fixed(ref, stride, frame_len, n)
+    d = dev(t, buf)
+    st = t.zeros(n, dtype=t.uint8, device="cuda")
+    cs = t.zeros(n, dtype=t.int32, device="cuda")
+    ctx.compute_fixed(d, stride, frame_len, n, st, cs)
+    ctx.sync()
+    np.testing.assert_array_equal(host(st), rst)
+    np.testing.assert_array_equal(host(cs).view(np.uint32), rcs)
+    np.testing.assert_array_equal(host(d), ref)
+    assert (rst == 0).all()
+    # corrupt ~1/8 of the frames, then verify both ways
+    bad = synth.corrupt(ref, np.arange(n, dtype=np.uint64) * stride, np.full(n, frame_len),
+                        frac_log2=3, seed=frame_len + 1)
+    d = dev(t, ref)
+    v = t.zeros(n, dtype=t.uint8, device="cuda")
+    ctx.verify_fixed(d, stride, frame_len, n, v)
+    ctx.sync()
+    rv = O.verify_fixed(ref, stride, frame_len, n)
+    np.testing.assert_array_equal(host(v), rv)
+    assert (rv[bad] != 0).all() and (np.delete(rv, bad) == 0).all()
+
+
+def test_fixed_no_inplace_and_null_outputs(torch_dev, ctx, O):
+    t = torch_dev
+    n, L = 2048, 1500
+    buf, stride = synth.fixed_frames(n, L, seed=5)
+    d = dev(t, buf)
+    cs = t.zeros(n, dtype=t.int32, device="cuda")
+    ctx.compute_fixed(d, stride, L, n, None, cs, flags=K["GCS_CF_NO_INPLACE"])
+    ctx.sync()
+    np.testing.assert_array_equal(host(d), buf)            # untouched
+    ref = buf.copy()
+    _, rcs = O.compute_fixed(ref, stride, L, n)
+    np.testing.assert_array_equal(host(cs).view(np.uint32), rcs)
+    ctx.compute_fixed(d, stride, L, n)                     # no status, no csums
+    ctx.sync()
+    np.testing.assert_array_equal(host(d), ref)
+
+
+# ---------------------------------------------------------------------------
+# descriptor kernels: IMIX and fuzzed frames
+
+def test_imix_packed(torch_dev, ctx, O):
+    t = torch_dev
+    n = 200_000
+    lens = synth.imix_lengths(n, seed=3)
+    buf, off, lens = synth.packed_frames(lens, seed=4)
+    ref = buf.copy()
+    rst, rcs = O.compute_batch(ref, off, lens)
+    d = dev(t, buf)
+    doff, dlen = dev(t, off.view(np.int64)), dev(t, lens.view(np.int16))
+    st = t.zeros(n, dtype=t.uint8, device="cuda")
+    cs = t.zeros(n, dtype=t.int32, device="cuda")
+    ctx.compute(d, doff, dlen, n, st, cs)
+    ctx.sync()
+    np.testing.assert_array_equal(host(st), rst)
+    np.testing.assert_array_equal(host(cs).view(np.uint32), rcs)
+    np.testing.assert_array_equal(host(d), ref)
+    bad = synth.corrupt(ref, off, lens, frac_log2=5, seed=9)
+    d = dev(t, ref)
+    v = t.zeros(n, dtype=t.uint8, device="cuda")
+    ctx.verify(d, doff, dlen, n, v)
+    ctx.sync()
+    rv = O.verify_batch(ref, off, lens)
+    np.testing.assert_array_equal(host(v), rv)
+    assert (rv[bad] != 0).all()
+
+
+def fuzz_frames(n, seed):
+    """Random headers: every field that steers the verdict is drawn from a
+    small set of interesting values, lengths are arbitrary (incl. odd)."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 1600, size=n).astype(np.uint16)
+    lens[rng.integers(0, n, n // 10)] = rng.integers(0, 80, n // 10)
+    off, total = synth.packed_offsets(lens, 16)
+    buf = rng.integers(0, 256, size=total + 64, dtype=np.uint8)
+    for i in range(n):
+        o, L = int(off[i]), int(lens[i])
+        f = buf[o:o + max(L, 64)]
+        if rng.random() < 0.9:
+            f[12], f[13] = 0x08, 0x00
+        ihl = int(rng.choice([5, 5, 5, 6, 15, 4, 0, int(rng.integers(0, 16))]))
+        ver = 4 if rng.random() < 0.9 else int(rng.integers(0, 16))
+        f[14] = (ver << 4) | ihl
+        tot = int(rng.choice([L - 14, L - 14, L - 13, L - 15, 19, 20, int(rng.integers(0, 2000))]))
+        tot = max(0, min(tot, 65535))
+        f[16], f[17] = tot >> 8, tot & 0xFF
+        f[23] = 6 if rng.random() < 0.9 else int(rng.integers(0, 256))
+        ts = 14 + 4 * ihl
+        if ts + 13 < len(f):
+            f[ts + 12] = int(rng.choice([5, 8, 15, 0, int(rng.integers(0, 16))])) << 4
+    return buf, off, lens
+
+
+def test_fuzz_desc_vs_oracle(torch_dev, ctx, O):
+    t = torch_dev
+    n = 20000
+    buf, off, lens = fuzz_frames(n, seed=17)
+    # make half of them internally consistent so TCP folds are exercised
+    tmp = buf.copy()
+    O.compute_batch(tmp, off, lens)
+    sel = np.random.default_rng(1).random(n) < 0.5
+    for i in np.nonzero(sel)[0]:
+        o, L = int(off[i]), int(lens[i])
+        buf[o:o + L] = tmp[o:o + L]
+    d = dev(t, buf)
+    doff, dlen = dev(t, off.view(np.int64)), dev(t, lens.view(np.int16))
+    v = t.zeros(n, dtype=t.uint8, device="cuda")
+    ctx.verify(d, doff, dlen, n, v, flags=1)
+    ctx.sync()
+    ref = buf.copy()
+    rv = O.verify_batch(ref, off, lens, flags=1)
+    np.testing.assert_array_equal(host(v), rv)
+    np.testing.assert_array_equal(host(d), ref)
+    assert len(np.unique(rv)) >= 8
+    # TX on the same fuzz
+    d = dev(t, buf)
+    st = t.zeros(n, dtype=t.uint8, device="cuda")
+    cs = t.zeros(n, dtype=t.int32, device="cuda")
+    ctx.compute(d, doff, dlen, n, st, cs)
+    ctx.sync()
+    ref = buf.copy()
+    rst, rcs = O.compute_batch(ref, off, lens)
+    np.testing.assert_array_equal(host(st), rst)
+    np.testing.assert_array_equal(host(cs).view(np.uint32), rcs)
+    np.testing.assert_array_equal(host(d), ref)
+
+
+def test_bad_descriptors(torch_dev, ctx):
+    t = torch_dev
+    buf = t.zeros(4096, dtype=t.uint8, device="cuda")
+    off = np.array([8, 4096, 4032, 0, 1 << 40], dtype=np.uint64)     # misaligned, at end, past end
+    lens = np.array([60, 1, 100, 0, 60], dtype=np.uint16)
+    v = t.full((5,), 255, dtype=t.uint8, device="cuda")
+    ctx.verify(buf, dev(t, off.view(np.int64)), dev(t, lens.view(np.int16)), 5, v)
+    st = t.full((5,), 255, dtype=t.uint8, device="cuda")
+    ctx.compute(buf, dev(t, off.view(np.int64)), dev(t, lens.view(np.int16)), 5, st)
+    ctx.sync()
+    assert host(v).tolist() == [9, 9, 9, 8, 9]
+    assert host(st).tolist() == [9, 9, 9, 2, 9]
+
+
+def test_descriptor_at_buffer_end_is_safe(torch_dev, ctx, O):
+    """A frame ending exactly at frames_bytes (not a multiple of 16) must be
+    read without touching bytes past the end (guarded partial chunk)."""
+    t = torch_dev
+    buf, stride = synth.fixed_frames(1, 1500, seed=2)
+    O.compute_fixed(buf, stride, 1500, 1)
+    raw = buf[:1500].copy()
+    d = dev(t, raw)
+    v = t.zeros(1, dtype=t.uint8, device="cuda")
+    ctx.verify(d, dev(t, np.zeros(1, np.int64)), dev(t, np.array([1500], np.int16)), 1, v,
+               frames_bytes=1500)
+    ctx.sync()
+    assert host(v)[0] == 0
+
+
+def test_zero_frames_and_invalid_args(torch_dev, ctx):
+    t = torch_dev
+    buf = t.zeros(64, dtype=t.uint8, device="cuda")
+    v = t.zeros(1, dtype=t.uint8, device="cuda")
+    ctx.verify_fixed(buf, 64, 64, 0, v)          # n = 0 is a no-op
+    with pytest.raises(gpucsum.GcsError):
+        ctx.verify_fixed(buf, 48, 64, 1, v)       # stride < frame_len
+    with pytest.raises(gpucsum.GcsError):
+        ctx.verify_fixed(buf, 72, 64, 1, v)       # stride % 16 != 0
+    with pytest.raises(gpucsum.GcsError):
+        ctx.verify_fixed(buf, 64, 64, 2, v)       # buffer too small (host check)
+    with pytest.raises(gpucsum.GcsError):
+        ctx.verify_fixed(np.zeros(64, np.uint8), 64, 64, 1, v)   # host buffer refused
+
+
+# ---------------------------------------------------------------------------
+# host-memory entry points (staged through pinned memory)
+
+def test_host_batches_chunked(torch_dev, O):
+    n = 5000
+    lens = synth.imix_lengths(n, seed=21)
+    buf, off, lens = synth.packed_frames(lens, seed=22)
+    with gpucsum.Context(0, max_frames=700, max_bytes=300_000) as c:   # forces many chunks
+        b1 = buf.copy()
+        st, cs = c.compute_host(b1, off, lens)
+        ref = buf.copy()
+        rst, rcs = O.compute_batch(ref, off, lens)
+        np.testing.assert_array_equal(st, rst)
+        np.testing.assert_array_equal(cs, rcs)
+        np.testing.assert_array_equal(b1, ref)
+        bad = synth.corrupt(ref, off, lens, frac_log2=4, seed=5)
+        b2 = ref.copy()
+        v = c.verify_host(b2, off, lens, flags=1)
+        rv = O.verify_batch(ref, off, lens, flags=1)
+        np.testing.assert_array_equal(v, rv)
+        np.testing.assert_array_equal(b2, ref)
+        assert (rv[bad] != 0).all()
+
+
+# ---------------------------------------------------------------------------
+# BASELINE sizes: size-independent properties
+
+@pytest.mark.parametrize("frame_len,n", [(64, 1 << 20), (1500, 1 << 20)])
+def test_full_size_properties(torch_dev, ctx, O, frame_len, n):
+    """C1/C2 sizes: TX fill then RX verify accepts everything; seeded
+    corruptions are exactly the drops; a fill is idempotent; a sample of
+    frames matches the oracle bit for bit."""
+    t = torch_dev
+    buf, stride = synth.fixed_frames(n, frame_len)
+    d = dev(t, buf)
+    ctx.compute_fixed(d, stride, frame_len, n)
+    v = t.zeros(n, dtype=t.uint8, device="cuda")
+    ctx.verify_fixed(d, stride, frame_len, n, v)
+    ctx.sync()
+    assert int((v != 0).sum()) == 0
+    filled = host(d)
+    cs1 = t.zeros(n, dtype=t.int32, device="cuda")
+    ctx.compute_fixed(d, stride, frame_len, n, None, cs1)     # idempotent
+    ctx.sync()
+    assert t.equal(d.cpu(), t.from_numpy(filled))
+    # sample vs oracle
+    idx = np.random.default_rng(0).choice(n, 4096, replace=False)
+    sample = np.concatenate([buf[i * stride:(i + 1) * stride] for i in idx])
+    _, rcs = O.compute_fixed(sample, stride, frame_len, len(idx))
+    np.testing.assert_array_equal(host(cs1).view(np.uint32)[idx], rcs)
+    # corruptions
+    bad = synth.corrupt(filled, np.arange(n, dtype=np.uint64) * stride, np.full(n, frame_len))
+    d = dev(t, filled)
+    ctx.verify_fixed(d, stride, frame_len, n, v)
+    ctx.sync()
+    got = np.nonzero(host(v))[0]
+    np.testing.assert_array_equal(got, np.sort(bad))
+
+
+def test_shards_equal_whole(torch_dev, ctx):
+    """Per-GPU sharding is exact: verdicts of contiguous frame
+    shards equal the verdicts of the whole batch."""
+    t = torch_dev
+    n, L = 100_003, 1500
+    buf, stride = synth.fixed_frames(n, L, seed=99)
+    d = dev(t, buf)
+    ctx.compute_fixed(d, stride, L, n)
+    ctx.sync()
+    filled = host(d)
+    filled[np.arange(0, n, 37, dtype=np.int64) * stride + 100] ^= 1
+    d = dev(t, filled)
+    whole = t.zeros(n, dtype=t.uint8, device="cuda")
+    ctx.verify_fixed(d, stride, L, n, whole)
+    parts = t.zeros(n, dtype=t.uint8, device="cuda")
+    for k in range(8):
+        lo, hi = n * k // 8, n * (k + 1) // 8
+        ctx.verify_fixed(d[lo * stride:hi * stride], stride, L, hi - lo, parts[lo:hi])
+    ctx.sync()
+    assert t.equal(whole, parts)
+    assert int((whole != 0).sum()) == len(range(0, n, 37))
