@@ -103,6 +103,7 @@ def make_batches(ctx, n, frame_len, seed, torch):
 
 def time_steps(ctx, tx, rx, stride, frame_len, n, steps, warmup, world, torch):
     stream = torch.cuda.current_stream().cuda_stream
+    assert stream, "kernels must run on the events' stream"
     verdict = torch.empty(n, dtype=torch.uint8, device="cuda")
 
     def step(ev=None):
@@ -254,6 +255,11 @@ def main():
     n = args.frames_per_gpu or ((1 << 20) if world == 1 else (1 << 22))
     L = args.frame_len
     ctx = gpucsum.Context(local)
+    # A dedicated torch stream: its handle is non-NULL, so the kernels run on
+    # exactly the stream the HIP events are recorded on (a NULL stream
+    # argument would select the context's own stream).
+    work = torch.cuda.Stream()
+    torch.cuda.set_stream(work)
     tx, rx, stride, nbad = make_batches(ctx, n, L, 0x6D746370 ^ rank, torch)
 
     elapsed, tx_ms, rx_ms, verdict = time_steps(ctx, tx, rx, stride, L, n, args.steps,
