@@ -46,6 +46,10 @@ def parse():
                    help="CPU-baseline time budget (rank 0, N=1 only); 0 disables")
     p.add_argument("--cpu-sample", type=int, default=1 << 18,
                    help="frames in the CPU-baseline sample")
+    p.add_argument("--settle-s", type=float, default=1.0,
+                   help="untimed seconds of the same kernels before the W warmup steps: "
+                        "the HBM/GPU clocks take ~10 ms of load to reach steady state "
+                        "(DESIGN.md §5); reported in the JSON line")
     p.add_argument("--no-extras", action="store_true",
                    help="skip the 64 B (C1) and PCIe-inclusive side measurements")
     return p.parse_args()
@@ -101,7 +105,7 @@ def make_batches(ctx, n, frame_len, seed, torch):
     return tx, rx, stride, int(pick.numel())
 
 
-def time_steps(ctx, tx, rx, stride, frame_len, n, steps, warmup, world, torch):
+def time_steps(ctx, tx, rx, stride, frame_len, n, steps, warmup, world, torch, settle_s=0.0):
     stream = torch.cuda.current_stream().cuda_stream
     assert stream, "kernels must run on the events' stream"
     verdict = torch.empty(n, dtype=torch.uint8, device="cuda")
@@ -116,6 +120,14 @@ def time_steps(ctx, tx, rx, stride, frame_len, n, steps, warmup, world, torch):
         if ev is not None:
             ev[2].record()
 
+    if settle_s > 0:
+        # bring HBM/GPU clocks to their loaded state: untimed
+        # passes of the same kernels, before and separate from the W warmups
+        t_end = time.perf_counter() + settle_s
+        while time.perf_counter() < t_end:
+            for _ in range(10):
+                step()
+            torch.cuda.synchronize()
     for _ in range(warmup):
         step()
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
@@ -129,7 +141,7 @@ def time_steps(ctx, tx, rx, stride, frame_len, n, steps, warmup, world, torch):
     barrier(world)
     tx_ms = [e[0].elapsed_time(e[1]) for e in evs]
     rx_ms = [e[1].elapsed_time(e[2]) for e in evs]
-    return t1 - t0, float(np.mean(tx_ms)), float(np.mean(rx_ms)), verdict
+    return t1 - t0, tx_ms, rx_ms, verdict
 
 
 def pmc_traffic(kernel_key: str):
@@ -262,8 +274,9 @@ def main():
     torch.cuda.set_stream(work)
     tx, rx, stride, nbad = make_batches(ctx, n, L, 0x6D746370 ^ rank, torch)
 
-    elapsed, tx_ms, rx_ms, verdict = time_steps(ctx, tx, rx, stride, L, n, args.steps,
-                                                args.warmup, world, torch)
+    elapsed, tx_list, rx_list, verdict = time_steps(ctx, tx, rx, stride, L, n, args.steps,
+                                                    args.warmup, world, torch, args.settle_s)
+    tx_ms, rx_ms = float(np.mean(tx_list)), float(np.mean(rx_list))
     bad_seen = int((verdict != 0).sum())
     if bad_seen != nbad:
         raise SystemExit(f"rank {rank}: verify flagged {bad_seen} frames, {nbad} corrupted")
@@ -302,13 +315,18 @@ def main():
         },
         "gib_per_s": gib,
         "roofline": {
-            "bound": "hbm", "kernel": f"k_fixed<32,3,{'true' if kname == 'compute' else 'false'},false> ({kname})",
+            "bound": "hbm",
+            "kernel": (f"gcs::k_fixed<32,3,{'true' if kname == 'compute' else 'false'},"
+                       f"false,true,2> ({kname})"),
             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": pmc_traffic(f"{kname}_{L}"),
             "bytes_per_launch_algorithmic": kbytes, "avg_launch_ms": kms,
         },
-        "kernels_ms": {"compute": tx_ms, "verify": rx_ms},
+        "kernels_ms": {"compute": tx_ms, "verify": rx_ms,
+                       "compute_first_last": [tx_list[0], tx_list[-1]],
+                       "verify_first_last": [rx_list[0], rx_list[-1]]},
+        "settle_s": args.settle_s,
         "corrupted_frames_detected": bad_seen,
     }
     if rank == 0 and world == 1:

@@ -1,0 +1,392 @@
+// gcs_device.h -- device-side building blocks of the gfx950 checksum kernels.
+//
+// Reference algorithm (derivation in DESIGN.md §3):
+//   TCPCalcChecksum  mtcp/src/tcp_util.c:244-277  -- u32 sum of LE16 words, odd tail
+//                    masked to its low byte (:262-263), + saddr/daddr halves,
+//                    htons(len), htons(6); two-step fold; ~.
+//   ip_fast_csum     io_engine/include/ps.h:66-95 -- x86 ADC chain over ihl dwords;
+//                    for ihl<=4 the raw low 16 bits of dword 0 (:72-73).
+//
+// Both folds are evaluated as EXACT integer sums of 16-bit words split across
+// lanes and added back together (no overflow: a 64 KiB segment sums to
+// < 2^31), then folded once, so results are bit-identical to the sequential
+// reference.  For ip_fast_csum with ihl>=5 the x86 ADC chain equals
+// ~fold16(sum of the header's 16-bit words): the end-around-carry sum R of the
+// dwords is congruent to that word sum mod 0xFFFF, is 0 only for an all-zero
+// header, and the final `adcl $0` can never carry out (state (0xFFFFFFFF, CF=1)
+// is unreachable from `addl`), so nothing is dropped.
+//
+// Layout: frames in HBM, each 16 B-aligned.  A frame is owned by a group of G
+// lanes (G | 64); lane `sub` loads the 16 B chunks c = j*G + sub (j < U) with
+// one global_load_dwordx4 each, so every load instruction of a group reads
+// G*16 contiguous bytes (whole 128 B lines).  Each lane keeps three partial
+// sums (IP header words; TCP segment words + pseudo header; one extra field),
+// the group all-reduces them on DPP, and the group applies the reference's
+// verdict order.  No LDS tiles, no MFMA: an HBM-bound integer reduction.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mtcp_gpucsum.h"
+
+namespace gcs {
+
+typedef uint32_t u32;
+typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+
+// TX check-field write-back modes (A/B'd in tools/kbench.hip)
+enum { WM_HALFWORD = 0,   // two 2-byte stores by the group leader
+       WM_CHUNK = 1,      // the 16 B chunk(s) holding a check field, rewritten whole
+       WM_SECTOR = 2,     // the 64 B sector(s) holding a check field, rewritten whole
+       WM_SECTOR_NT = 3,  // ... with non-temporal stores
+       WM_SECTOR_SC1 = 4  // ... with sc1 (write-through past the XCD L2) stores
+};
+
+// ---------------------------------------------------------------------------
+// scalar helpers
+
+__device__ __forceinline__ u32 hsum(u32 d) { return (d & 0xFFFFu) + (d >> 16); }
+
+__device__ __forceinline__ u32 hsum4(uint4 v)
+{
+    return hsum(v.x) + hsum(v.y) + hsum(v.z) + hsum(v.w);
+}
+
+// two-step fold of tcp_util.c:271-272 (also what ps.h's addw/adcl produces)
+__device__ __forceinline__ u32 fold16(u32 s)
+{
+    s = (s >> 16) + (s & 0xFFFFu);
+    s += s >> 16;
+    return s & 0xFFFFu;
+}
+
+__device__ __forceinline__ u32 csum16(u32 s) { return (~fold16(s)) & 0xFFFFu; }
+
+__device__ __forceinline__ u32 bswap16(u32 v) { return ((v >> 8) & 0xFFu) | ((v & 0xFFu) << 8); }
+
+// keep the low r bytes of d, r clamped to [0, 4]
+__device__ __forceinline__ u32 keep_low(u32 d, int r)
+{
+    r = r < 0 ? 0 : (r > 4 ? 4 : r);
+    return d & (u32)((1ull << (8 * r)) - 1ull);
+}
+
+// Sum of the 16-bit words of dword d (frame offset p, p % 4 == 0) that lie in
+// [a, b), a even.  A word straddling b (b odd) contributes its low byte only:
+// the reference's `*w & ntohs(0xFF00)` on a little-endian host.
+__device__ __forceinline__ u32 region_sum(u32 d, int p, int a, int b)
+{
+    u32 t = keep_low(d, b - p);
+    u32 lo = (p >= a) ? (t & 0xFFFFu) : 0u;
+    u32 hi = (p + 2 >= a) ? (t >> 16) : 0u;
+    return lo + hi;
+}
+
+__device__ __forceinline__ u32 pick(uint4 v, int k)
+{
+    return k == 0 ? v.x : (k == 1 ? v.y : (k == 2 ? v.z : v.w));
+}
+
+// Replace the high half of dword k of v by `hi16`.
+__device__ __forceinline__ uint4 patch_hi(uint4 v, int k, u32 hi16)
+{
+    const u32 m = 0x0000FFFFu, s = hi16 << 16;
+    v.x = k == 0 ? (v.x & m) | s : v.x;
+    v.y = k == 1 ? (v.y & m) | s : v.y;
+    v.z = k == 2 ? (v.z & m) | s : v.z;
+    v.w = k == 3 ? (v.w & m) | s : v.w;
+    return v;
+}
+
+// All-reduce (sum) inside aligned groups of G lanes.  Within a 16-lane row the
+// butterfly runs on DPP (VALU only): quad_perm [1,0,3,2] and [2,3,0,1],
+// row_half_mirror, row_mirror -- after the quad steps every lane of a quad
+// holds the quad sum, so a mirror adds exactly the partner's sum.  The 16 ->
+// 32 step is a ds_swizzle (xor 16, no LDS memory access), 32 -> 64 a bpermute.
+template <int G>
+__device__ __forceinline__ u32 group_sum(u32 x)
+{
+    if constexpr (G >= 2)
+        x += (u32)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
+    if constexpr (G >= 4)
+        x += (u32)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);
+    if constexpr (G >= 8)
+        x += (u32)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);
+    if constexpr (G >= 16)
+        x += (u32)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, false);
+    if constexpr (G >= 32)
+        x += (u32)__builtin_amdgcn_ds_swizzle((int)x, 0x401F);
+    if constexpr (G >= 64)
+        x += __shfl_xor(x, 32, 64);
+    return x;
+}
+
+// Value of lane SRC (0 or 1) of this lane's G-group.
+template <int G, int SRC>
+__device__ __forceinline__ u32 group_bcast(u32 x)
+{
+    if constexpr (G == 4) {
+        return (u32)__builtin_amdgcn_mov_dpp((int)x, SRC ? 0x55 : 0x00, 0xF, 0xF, false);
+    } else if constexpr (G <= 32) {
+        // ds_swizzle bit mode: src lane = (lane & and_mask) | or_mask in a 32-lane half
+        constexpr int and_mask = 0x1F & ~(G - 1);
+        return (u32)__builtin_amdgcn_ds_swizzle((int)x, and_mask | (SRC << 5));
+    } else {
+        return __shfl(x, SRC, 64);
+    }
+}
+
+// One global_load_dwordx4; NT adds the non-temporal (streaming) cache hint.
+template <bool NT>
+__device__ __forceinline__ uint4 ldg16(const uint8_t* p)
+{
+    const u32x4* q = reinterpret_cast<const u32x4*>(p);
+    u32x4 r = NT ? __builtin_nontemporal_load(q) : *q;
+    return make_uint4(r.x, r.y, r.z, r.w);
+}
+
+// One global_store_dwordx4 with the cache policy of write mode WM.
+template <int WM>
+__device__ __forceinline__ void stg16(uint8_t* p, uint4 v)
+{
+    u32x4 d = u32x4{v.x, v.y, v.z, v.w};
+    if constexpr (WM == WM_SECTOR_NT) {
+        __builtin_nontemporal_store(d, reinterpret_cast<u32x4*>(p));
+    } else if constexpr (WM == WM_SECTOR_SC1) {
+        // no result register: nothing to wait for before the kernel ends
+        asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(p), "v"(d) : "memory");
+    } else {
+        *reinterpret_cast<u32x4*>(p) = d;
+    }
+}
+
+// 16-byte chunk load; `avail` = readable bytes from p (only checked when SAFE)
+template <bool SAFE, bool NT>
+__device__ __forceinline__ uint4 load_chunk(const uint8_t* p, int64_t avail)
+{
+    if (!SAFE || avail >= 16)
+        return ldg16<NT>(p);
+    uint8_t b[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+        b[k] = (k < avail) ? p[k] : 0;
+    uint4 v;
+    v.x = b[0] | (b[1] << 8) | (b[2] << 16) | ((u32)b[3] << 24);
+    v.y = b[4] | (b[5] << 8) | (b[6] << 16) | ((u32)b[7] << 24);
+    v.z = b[8] | (b[9] << 8) | (b[10] << 16) | ((u32)b[11] << 24);
+    v.w = b[12] | (b[13] << 8) | (b[14] << 16) | ((u32)b[15] << 24);
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// per-frame work for one group of G lanes
+
+struct Hdr {
+    u32 d3, d4, d5;   // frame bytes 12..15, 16..19, 20..23
+};
+
+struct Acc {
+    u32 ip;    // IP header words [14, 14+4*ihl)          (COMPUTE: minus iph->check)
+    u32 tcp;   // TCP words [ts, te) + saddr/daddr halves (COMPUTE: minus tcph->check)
+    u32 x;     // VERIFY: the byte holding tcph->doff
+};
+
+// Accumulate the chunk at frame offset cb.  ts = 14 + 4*ihl, te = 14 + tot_len.
+template <bool COMPUTE>
+__device__ __forceinline__ void accum_chunk(uint4 v, int cb, int ts, int te, Acc& a)
+{
+    if (cb >= ts && cb + 16 <= te) {          // interior of the TCP segment
+        a.tcp += hsum4(v);
+    } else if (cb < ts || cb < te) {          // edge chunk: exact word masks
+        int p = cb;
+        a.ip += region_sum(v.x, p, 14, ts) + region_sum(v.y, p + 4, 14, ts) +
+                region_sum(v.z, p + 8, 14, ts) + region_sum(v.w, p + 12, 14, ts);
+        a.tcp += region_sum(v.x, p, ts, te) + region_sum(v.y, p + 4, ts, te) +
+                 region_sum(v.z, p + 8, ts, te) + region_sum(v.w, p + 12, ts, te);
+        if (cb == 16) {
+            // pseudo header: saddr halves at 26, 28; daddr low half at 30
+            a.tcp += (v.z >> 16) + hsum(v.w);
+            if (COMPUTE)
+                a.ip -= v.z & 0xFFFFu;        // iph->check is 0 when folded (ip_out.c:153)
+        } else if (cb == 32) {
+            a.tcp += v.x & 0xFFFFu;           // daddr high half at 32
+        }
+    }
+    // Fields at ihl-dependent offsets may sit in an interior chunk.
+    if (COMPUTE) {
+        int pc = ts + 14;                     // dword whose high half is tcph->check
+        if (pc >= cb && pc < cb + 16 && pc + 4 <= te)
+            a.tcp -= pick(v, (pc - cb) >> 2) >> 16;
+    } else {
+        int pd = ts + 10;                     // dword whose byte 2 is doff<<4 | res
+        if (pd >= cb && pd < cb + 16)
+            a.x += (pick(v, (pd - cb) >> 2) >> 16) & 0xFFu;
+    }
+}
+
+// Verdict for one frame, in the reference's order.
+__device__ __forceinline__ u32 rx_verdict(const Hdr& h, const Acc& a, u32 len, bool desc_ok)
+{
+    if (!desc_ok) return GCS_V_BAD_DESC;
+    if (len < 14) return GCS_V_DROP_TRUNC;
+    if ((h.d3 & 0xFFFFu) != 0x0008u) return GCS_V_NOT_IPV4;         // eth_in.c:35
+    if (len < 34) return GCS_V_DROP_TRUNC;
+    u32 vihl = (h.d3 >> 16) & 0xFFu;
+    u32 ihl = vihl & 15u, version = vihl >> 4;
+    u32 tot = bswap16(h.d4 & 0xFFFFu);
+    u32 proto = h.d5 >> 24;
+    if (tot < 20) return GCS_V_DROP_IPLEN;                          // ip_in.c:25
+    if (ihl >= 5 && 14 + 4 * ihl > len) return GCS_V_DROP_TRUNC;
+    u32 ipc = ihl <= 4 ? (h.d3 >> 16) : csum16(a.ip);               // ps.h:72-73 quirk
+    if (ipc != 0) return GCS_V_DROP_IPCSUM;                          // ip_in.c:35
+    if (version != 4) return GCS_V_NOT_V4;                           // ip_in.c:47
+    if (proto != 6) return GCS_V_NOT_TCP;                            // ip_in.c:52-59
+    u32 ts = 14 + 4 * ihl;
+    if (ts + 13 > len) return GCS_V_DROP_TRUNC;
+    u32 doff = a.x >> 4;
+    if (tot < 4 * (ihl + doff)) return GCS_V_DROP_TCPLEN;            // tcp_in.c:1221
+    if (14 + tot > len) return GCS_V_DROP_TRUNC;
+    u32 s = a.tcp + bswap16((tot - 4 * ihl) & 0xFFFFu) + 0x0600u;    // tcp_util.c:266-269
+    return csum16(s) != 0 ? GCS_V_DROP_TCPCSUM : GCS_V_ACCEPT;        // tcp_in.c:1231-1239
+}
+
+// Group reduction, then the verdict (RX) or the check-field fill (TX).
+// `v` holds this lane's chunks c = j*G + sub of the frame's FIRST U*G chunks
+// (the check fields always lie in chunks 1..5); `active` = false for padding
+// groups, which take part in the cross-lane steps but write nothing.
+template <int G, int U, bool COMPUTE, int WM>
+__device__ __forceinline__ void epilogue(const Hdr& h, Acc a, uint8_t* __restrict__ f, u32 len,
+                                         bool desc_ok, int sub, u32 flags,
+                                         uint8_t* __restrict__ out_code,
+                                         uint32_t* __restrict__ out_csum, bool active,
+                                         const uint4 (&v)[U])
+{
+    a.ip = group_sum<G>(a.ip);
+    a.tcp = group_sum<G>(a.tcp);
+    if (!COMPUTE)
+        a.x = group_sum<G>(a.x);
+    if (!active)
+        return;
+    const u32 ihl = (h.d3 >> 16) & 15u;
+    const u32 ts = 14 + 4 * ihl;
+
+    if (!COMPUTE) {
+        if (sub != 0)
+            return;
+        u32 vd = rx_verdict(h, a, len, desc_ok);
+        if (vd == GCS_V_DROP_TCPCSUM && (flags & GCS_VF_ZERO_BAD_TCP_CHECK) && ts + 18u <= len)
+            *reinterpret_cast<uint16_t*>(f + ts + 16) = 0;         // tcp_in.c:1237
+        out_code[0] = (uint8_t)vd;
+        return;
+    }
+    // TX fill: ip_out.c:143-173, tcp_out.c:244, 323-333.  Every lane of the
+    // group evaluates the (uniform) status so that WM_CHUNK / WM_SECTOR can
+    // rewrite whole chunks from the lanes that hold them.
+    u32 st, ipc = 0, tcpc = 0;
+    if (!desc_ok) {
+        st = GCS_TX_BAD_DESC;
+    } else if (len < 14 || (h.d3 & 0xFFFFu) != 0x0008u) {
+        st = GCS_TX_NOT_IPV4;
+    } else if (len < 34 || ihl < 5 || 14u + 4u * ihl > len) {
+        st = GCS_TX_BAD_HDR;
+    } else {
+        u32 tot = bswap16(h.d4 & 0xFFFFu);
+        ipc = csum16(a.ip);
+        if ((h.d5 >> 24) != 6) {
+            st = GCS_TX_IP_ONLY;
+        } else if (tot < 4u * ihl + 20u || 14u + tot > len) {
+            st = GCS_TX_BAD_TCPLEN;
+        } else {
+            tcpc = csum16(a.tcp + bswap16((tot - 4 * ihl) & 0xFFFFu) + 0x0600u);
+            st = GCS_TX_OK;
+        }
+    }
+    const bool wip = st == GCS_TX_OK || st == GCS_TX_IP_ONLY || st == GCS_TX_BAD_TCPLEN;
+    const bool wtcp = st == GCS_TX_OK;
+    if (!(flags & GCS_CF_NO_INPLACE) && wip) {
+        if constexpr (WM == WM_HALFWORD) {
+            if (sub == 0) {
+                *reinterpret_cast<uint16_t*>(f + 24) = (uint16_t)ipc;
+                if (wtcp)
+                    *reinterpret_cast<uint16_t*>(f + ts + 16) = (uint16_t)tcpc;
+            }
+        } else {
+            const int nchunks = (int)((len + 15) >> 4);
+            const int ctcp = (int)(ts + 16) >> 4;            // chunk holding tcph->check
+#pragma unroll
+            for (int j = 0; j < U; j++) {
+                const int c = j * G + sub;
+                if (j * G >= 8 || c >= nchunks || c >= 8)
+                    continue;
+                const bool has_ip = c == 1;
+                const bool has_tcp = wtcp && c == ctcp;
+                const bool take = WM == WM_CHUNK
+                                      ? (has_ip || has_tcp)
+                                      : ((c >> 2) == 0 || (wtcp && (c >> 2) == (ctcp >> 2)));
+                if (!take)
+                    continue;
+                uint4 w = v[j];
+                if (has_ip)
+                    w.z = (w.z & 0xFFFF0000u) | ipc;                 // bytes 24..25
+                if (has_tcp)
+                    w = patch_hi(w, (int)((ts + 14) >> 2) & 3, tcpc); // bytes ts+16..17
+                stg16<WM>(f + 16 * c, w);
+            }
+        }
+    }
+    if (sub == 0) {
+        if (out_code)
+            out_code[0] = (uint8_t)st;
+        if (out_csum)
+            out_csum[0] = ipc | (tcpc << 16);
+    }
+}
+
+// One frame per group: load, broadcast the header words, accumulate, epilogue.
+// LOOP: frames longer than G*U chunks are walked in further batches (the
+// first batch is kept for the TX write-back).
+template <int G, int U, bool COMPUTE, bool LOOP, bool SAFE, bool NT, int WM>
+__device__ __forceinline__ void do_frame(uint8_t* __restrict__ f, u32 len, int64_t avail,
+                                         bool desc_ok, int sub, u32 flags,
+                                         uint8_t* __restrict__ out_code,
+                                         uint32_t* __restrict__ out_csum)
+{
+    const int nchunks = desc_ok ? (int)((len + 15) >> 4) : 0;
+    uint4 v[U];
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+        int c = j * G + sub;
+        v[j] = c < nchunks ? load_chunk<SAFE, NT>(f + 16 * c, avail - 16 * c)
+                           : make_uint4(0, 0, 0, 0);
+    }
+    // header words: chunk 0 lives in group lane 0, chunk 1 in group lane 1 (j = 0)
+    Hdr h;
+    h.d3 = group_bcast<G, 0>(v[0].w);
+    h.d4 = group_bcast<G, 1>(v[0].x);
+    h.d5 = group_bcast<G, 1>(v[0].y);
+    const int ts = 14 + 4 * (int)((h.d3 >> 16) & 15u);
+    const int te = 14 + (int)bswap16(h.d4 & 0xFFFFu);
+
+    Acc a = {0u, 0u, 0u};
+#pragma unroll
+    for (int j = 0; j < U; j++)
+        accum_chunk<COMPUTE>(v[j], 16 * (j * G + sub), ts, te, a);
+    if (LOOP && nchunks > G * U) {
+        uint4 w[U];
+        for (int base = G * U; base < nchunks; base += G * U) {
+#pragma unroll
+            for (int j = 0; j < U; j++) {
+                int c = base + j * G + sub;
+                w[j] = c < nchunks ? load_chunk<SAFE, NT>(f + 16 * c, avail - 16 * c)
+                                   : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int j = 0; j < U; j++)
+                accum_chunk<COMPUTE>(w[j], 16 * (base + j * G + sub), ts, te, a);
+        }
+    }
+    epilogue<G, U, COMPUTE, WM>(h, a, f, len, desc_ok, sub, flags, out_code, out_csum, true, v);
+}
+
+}  // namespace gcs

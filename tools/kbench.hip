@@ -1,0 +1,210 @@
+// kbench.hip -- A/B timing of checksum kernel variants in ONE process
+// (cdna_hip_programming.md §5.4 rule 24: interleaved rounds, median), plus a
+// pure-read ceiling for the same bytes.  Not part of the product library.
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../include tools/kbench.hip -o tools/kbench
+//   tools/kbench [frame_len=1500] [n=1048576] [rounds=15]
+#include "../mtcp_amd/csrc/gcs_kernels.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#define CK(x)                                                                        \
+    do {                                                                             \
+        hipError_t e_ = (x);                                                         \
+        if (e_ != hipSuccess) {                                                      \
+            std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x,           \
+                         hipGetErrorString(e_));                                     \
+            std::exit(1);                                                            \
+        }                                                                            \
+    } while (0)
+
+using namespace gcs;
+
+__device__ inline uint32_t mix(uint64_t x)
+{
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull;
+    x ^= x >> 33;
+    return (uint32_t)x;
+}
+
+// random frame bytes with mTCP headers (checks zero), like mtcp_amd/synth.py
+__global__ void k_init(uint8_t* buf, uint64_t n, uint64_t stride, uint32_t len)
+{
+    uint64_t words = n * stride / 4;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        reinterpret_cast<uint32_t*>(buf)[i] = mix(i * 0x9E3779B97F4A7C15ull + 1);
+}
+
+__global__ void k_hdr(uint8_t* buf, uint64_t n, uint64_t stride, uint32_t len)
+{
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint8_t* f = buf + i * stride;
+    uint32_t tot = len - 14, doff = len < 66 ? 5 : 8;
+    f[12] = 8; f[13] = 0; f[14] = 0x45; f[15] = 0; f[16] = tot >> 8; f[17] = tot & 255;
+    f[20] = 0x40; f[21] = 0; f[22] = 64; f[23] = 6; f[24] = f[25] = 0;
+    f[46] = doff << 4; f[47] = 0x10; f[50] = f[51] = f[52] = f[53] = 0;
+    if (doff == 8) { f[54] = 1; f[55] = 1; f[56] = 8; f[57] = 10; }
+}
+
+template <bool NT>
+__global__ void __launch_bounds__(256) k_read(const uint4* __restrict__ p, uint64_t n16,
+                                              uint32_t* out)
+{
+    uint32_t acc = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        const uint8_t* b8 = reinterpret_cast<const uint8_t*>(p);
+        uint4 a = ldg16<NT>(b8 + 16 * i), b = ldg16<NT>(b8 + 16 * (i + stride)),
+              c = ldg16<NT>(b8 + 16 * (i + 2 * stride)), d = ldg16<NT>(b8 + 16 * (i + 3 * stride));
+        acc += a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^
+               d.y ^ d.z ^ d.w;
+    }
+    for (; i < n16; i += stride) acc += p[i].x;
+    if (acc == 0x9E3779B9u) out[0] = acc;
+}
+
+struct Variant {
+    std::string name;
+    double bytes;                       // algorithmic bytes per launch
+    std::function<void(hipStream_t)> run;
+    std::vector<float> ms;
+};
+
+int main(int argc, char** argv)
+{
+    uint32_t L = argc > 1 ? std::atoi(argv[1]) : 1500;
+    uint64_t n = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : (1u << 20);
+    int rounds = argc > 3 ? std::atoi(argv[3]) : 15;
+    uint64_t stride = L <= 64 ? 64 : (L + 127) / 128 * 128;
+    int dev = 0, cus = 0;
+    CK(hipGetDevice(&dev));
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    uint8_t *tx, *rx, *v1, *v2;
+    uint32_t *cs1, *cs2, *sink;
+    CK(hipMalloc(&tx, n * stride));
+    CK(hipMalloc(&rx, n * stride));
+    CK(hipMalloc(&v1, n));
+    CK(hipMalloc(&v2, n));
+    CK(hipMalloc(&cs1, 4 * n));
+    CK(hipMalloc(&cs2, 4 * n));
+    CK(hipMalloc(&sink, 4));
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    hipLaunchKernelGGL(k_init, dim3(4096), dim3(256), 0, s, tx, n, stride, L);
+    hipLaunchKernelGGL(k_hdr, dim3((n + 255) / 256), dim3(256), 0, s, tx, n, stride, L);
+    CK(hipMemcpyAsync(rx, tx, n * stride, hipMemcpyDeviceToDevice, s));
+    CK(launch_compute_fixed(rx, stride, L, n, nullptr, nullptr, 0, s));
+    CK(hipStreamSynchronize(s));
+    std::printf("frame_len %u stride %llu n %llu (%.2f GB per batch), CUs %d\n", L,
+                (unsigned long long)stride, (unsigned long long)n, n * stride / 1e9, cus);
+
+    const double vbytes = (double)n * (L + 1), cbytes = (double)n * (L + 4);
+    std::vector<Variant> vs;
+    constexpr int kG = 32, kU = 3;
+    const int FPB = 256 / kG;
+    if (L == 1500) {
+#define VFY(NT_)                                                                          \
+        vs.push_back({std::string("verify  k_fixed<32,3> NT=") + #NT_, vbytes,            \
+                      [&](hipStream_t st) {                                               \
+            hipLaunchKernelGGL((k_fixed<kG, kU, false, false, NT_, WM_HALFWORD>),          \
+                               dim3((n + FPB - 1) / FPB), dim3(256), 0, st, rx, stride, L, \
+                               (u32)n, v1, nullptr, 0u);                                  \
+        }});
+        VFY(false) VFY(true)
+#define CMP(NT_, WM_, FL_, TAG)                                                           \
+        vs.push_back({std::string("compute k_fixed<32,3> NT=") + #NT_ + " " + TAG, cbytes, \
+                      [&](hipStream_t st) {                                               \
+            hipLaunchKernelGGL((k_fixed<kG, kU, true, false, NT_, WM_>),                  \
+                               dim3((n + FPB - 1) / FPB), dim3(256), 0, st, tx, stride, L, \
+                               (u32)n, nullptr, cs1, FL_);                                \
+        }});
+        CMP(true, WM_HALFWORD, 0u, "2B stores")
+        CMP(true, WM_SECTOR, 0u, "64B sector stores")
+        CMP(true, WM_SECTOR_NT, 0u, "64B sector nt stores")
+        CMP(true, WM_SECTOR_SC1, 0u, "64B sector sc1 stores")
+        CMP(true, WM_SECTOR, (u32)GCS_CF_NO_INPLACE, "no in-place write")
+        // the bench step: TX compute over tx, then RX verify over rx (one sample)
+#define PAIR(WM_, FL_, TAG)                                                               \
+        vs.push_back({std::string("STEP compute(tx)+verify(rx) ") + TAG, cbytes + vbytes,  \
+                      [&](hipStream_t st) {                                               \
+            hipLaunchKernelGGL((k_fixed<kG, kU, true, false, true, WM_>),                 \
+                               dim3((n + FPB - 1) / FPB), dim3(256), 0, st, tx, stride, L, \
+                               (u32)n, nullptr, nullptr, FL_);                            \
+            hipLaunchKernelGGL((k_fixed<kG, kU, false, false, true, WM_>),                \
+                               dim3((n + FPB - 1) / FPB), dim3(256), 0, st, rx, stride, L, \
+                               (u32)n, v1, nullptr, 0u);                                  \
+        }});
+        PAIR(WM_HALFWORD, 0u, "2B stores")
+        PAIR(WM_SECTOR, 0u, "64B sector")
+        PAIR(WM_SECTOR_NT, 0u, "64B sector nt")
+        PAIR(WM_SECTOR_SC1, 0u, "64B sector sc1")
+        PAIR(WM_SECTOR, (u32)GCS_CF_NO_INPLACE, "no in-place write")
+    } else {
+        vs.push_back({"verify  dispatch_fixed", vbytes, [&](hipStream_t st) {
+            CK(launch_verify_fixed(rx, stride, L, (u32)n, v1, 0u, st));
+        }});
+        vs.push_back({"compute dispatch_fixed", cbytes, [&](hipStream_t st) {
+            CK(launch_compute_fixed(tx, stride, L, (u32)n, nullptr, cs1, 0u, st));
+        }});
+    }
+    vs.push_back({"read-ceiling uint4 (whole batch bytes)", (double)n * stride,
+                  [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_read<false>), dim3(cus * 8), dim3(256), 0, st,
+                           (const uint4*)rx, n * stride / 16, sink);
+    }});
+    vs.push_back({"read-ceiling uint4 NT (whole batch bytes)", (double)n * stride,
+                  [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_read<true>), dim3(cus * 8), dim3(256), 0, st,
+                           (const uint4*)rx, n * stride / 16, sink);
+    }});
+
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (auto& v : vs)
+        for (int w = 0; w < 3; w++) v.run(s);
+    CK(hipStreamSynchronize(s));
+    for (int r = 0; r < rounds; r++) {
+        for (auto& v : vs) {
+            CK(hipEventRecord(e0, s));
+            v.run(s);
+            CK(hipEventRecord(e1, s));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            v.ms.push_back(ms);
+        }
+    }
+    CK(hipGetLastError());
+    for (auto& v : vs) {
+        std::sort(v.ms.begin(), v.ms.end());
+        double med = v.ms[v.ms.size() / 2], mn = v.ms[0];
+        std::printf("%-44s median %8.1f us  min %8.1f us  %7.0f GB/s (%.1f%% of 8 TB/s)\n",
+                    v.name.c_str(), med * 1e3, mn * 1e3, v.bytes / (med * 1e-3) / 1e9,
+                    100.0 * v.bytes / (med * 1e-3) / 8e12);
+    }
+    // outputs of the variants must agree
+    std::vector<uint8_t> h1(n), h2(n);
+    std::vector<uint32_t> c1(n), c2(n);
+    CK(hipMemcpy(h1.data(), v1, n, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(c1.data(), cs1, 4 * n, hipMemcpyDeviceToHost));
+    // every variant rewrote tx with the same checks: tx must now verify clean
+    CK(launch_verify_fixed(tx, stride, L, (u32)n, v2, 0u, s));
+    CK(hipMemcpy(h2.data(), v2, n, hipMemcpyDeviceToHost));
+    size_t txbad = 0;
+    for (auto b : h2) txbad += b != 0;
+    std::printf("tx after all compute variants: %zu non-accept (expect 0)\n", txbad);
+    size_t bad = 0;
+    for (auto b : h1) bad += b != 0;
+    std::printf("non-accept verdicts: %zu (expect 0)\n", bad);
+    return 0;
+}
