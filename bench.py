@@ -55,35 +55,22 @@ def parse():
     return p.parse_args()
 
 
+from mtcp_amd.shard import aggregate_rate, barrier, env_world, max_over_ranks  # noqa: E402
+
+
 def dist_setup(args):
+    """One process per GPU; torch.distributed (RCCL) only for the timing
+    barrier and the max-over-ranks reduction -- no data-path collective."""
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = env_world()
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     return world, rank, local
-
-
-def barrier(world):
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
-
-
-def max_over_ranks(world, x: float) -> float:
-    if world == 1:
-        return x
-    import torch
-    import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
 
 
 def make_batches(ctx, n, frame_len, seed, torch):
@@ -282,9 +269,9 @@ def main():
         raise SystemExit(f"rank {rank}: verify flagged {bad_seen} frames, {nbad} corrupted")
     t = max_over_ranks(world, elapsed)
 
-    frames = 2 * n * world * args.steps          # TX fills + RX verifies, all ranks
-    value = frames / t / 1e9
-    gib = frames * L / t / 2**30
+    rate = aggregate_rate(2 * n, world, args.steps, t)   # TX fills + RX verifies, all ranks
+    value = rate / 1e9
+    gib = rate * L / 2**30
     # dominant kernel's roofline (algorithmic bytes)
     rx_bytes = n * (L + 1)
     tx_bytes = n * (L + 4)

@@ -1,0 +1,105 @@
+/*
+ * gpucsum_io_module.h -- mTCP I/O-module plugin that moves the software
+ * checksum path onto MI355X (exported by libmtcp_gpucsum.so).
+ *
+ * The plugin surface is mTCP's own (/root/reference/mtcp/src/include/io_module.h):
+ *   - struct io_module_func, 11 function pointers     io_module.h:60-72
+ *   - dev_ioctl command codes PKT_*_CSUM               io_module.h:84-91
+ *   - module selection by `io = <name>`               config.c:635-640, io_module.h:114-125
+ * It is restated below (same field order, types and alignment -- that is the
+ * ABI) only when io_module.h itself has not been included, so mTCP sources
+ * can include both headers.
+ *
+ * gpucsum_module_func is a DECORATOR around an inner NIC module (dpdk,
+ * netmap, psio, or any io_module_func):
+ *   recv_pkts   inner recv_pkts, then one batched RX verify of the burst on the
+ *               GPU (replaces ip_in.c:28-37 + tcp_in.c:1224-1241 per frame)
+ *   get_rptr    NULL for frames whose verdict mTCP would count as an ERROR --
+ *               exactly how dpdk_get_rptr surfaces bad HW checksums
+ *               (dpdk_module.c:536-542); core.c:794-799 counts rx_errors
+ *   get_wptr    inner get_wptr; the buffer is queued for the TX fill
+ *   send_pkts   one batched TX fill of the queued frames on the GPU (replaces
+ *               ip_out.c:155-173 + tcp_out.c:323-333), then inner send_pkts
+ *   dev_ioctl   0 ("done by the device") for PKT_TX_IP_CSUM, PKT_TX_TCPIP_CSUM,
+ *               PKT_RX_IP_CSUM, PKT_RX_TCP_CSUM, PKT_TX_TCPIP_CSUM_PEEK; -1
+ *               (software) for PKT_TX_TCP_CSUM; anything else is forwarded to
+ *               the inner module (DRV_NAME, PKT_RX_TCP_LROSEG)
+ *   others      forwarded unchanged
+ * Build mTCP WITHOUT -DDISABLE_HWCSUM so that ip_in.c / ip_out.c / tcp_in.c /
+ * tcp_out.c consult dev_ioctl (configure.ac:119-125, Makefile.in:63-65).
+ *
+ * Threading (core.c:1153-1245): load_module once on the main thread; every
+ * other call from the owning mTCP thread.  Per-thread state is keyed by the
+ * mtcp_thread_context pointer; mTCP thread k uses GPU k mod n_gpus (override:
+ * environment variable GPUCSUM_DEVICE).
+ */
+#ifndef GPUCSUM_IO_MODULE_H
+#define GPUCSUM_IO_MODULE_H
+
+#include <stdint.h>
+#include <limits.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#ifndef IO_MODULE_H   /* not already declared by mtcp/src/include/io_module.h */
+#ifndef __WORDSIZE
+#define __WORDSIZE 64
+#endif
+struct mtcp_thread_context;
+typedef struct io_module_func {
+	void      (*load_module)(void);
+	void      (*init_handle)(struct mtcp_thread_context *ctx);
+	int32_t   (*link_devices)(struct mtcp_thread_context *ctx);
+	void      (*release_pkt)(struct mtcp_thread_context *ctx, int ifidx,
+	                         unsigned char *pkt_data, int len);
+	uint8_t * (*get_wptr)(struct mtcp_thread_context *ctx, int ifidx, uint16_t len);
+	int32_t   (*send_pkts)(struct mtcp_thread_context *ctx, int nif);
+	uint8_t * (*get_rptr)(struct mtcp_thread_context *ctx, int ifidx, int index,
+	                      uint16_t *len);
+	int32_t   (*recv_pkts)(struct mtcp_thread_context *ctx, int ifidx);
+	int32_t   (*select)(struct mtcp_thread_context *ctx);
+	void      (*destroy_handle)(struct mtcp_thread_context *ctx);
+	int32_t   (*dev_ioctl)(struct mtcp_thread_context *ctx, int nif, int cmd, void *argp);
+} io_module_func __attribute__((aligned(__WORDSIZE)));
+
+#define PKT_TX_IP_CSUM          0x01
+#define PKT_TX_TCP_CSUM         0x02
+#define PKT_RX_TCP_LROSEG       0x03
+#define PKT_TX_TCPIP_CSUM       0x04
+#define PKT_RX_IP_CSUM          0x05
+#define PKT_RX_TCP_CSUM         0x06
+#define PKT_TX_TCPIP_CSUM_PEEK  0x07
+#define DRV_NAME                0x08
+#endif /* IO_MODULE_H */
+
+/* The decorator vtable (mTCP: `io = gpucsum` once AssignIOModule knows it). */
+extern io_module_func gpucsum_module_func;
+
+/* Set the inner module the decorator wraps.  Call before load_module(). */
+int gpucsum_set_inner(io_module_func *inner);
+
+#define GPUCSUM_MAX_IFS    16     /* MAX_DEVICES, io_engine/include/ps.h:4 */
+#define GPUCSUM_MAX_BURST  8192   /* frames per recv_pkts / per send_pkts queue */
+
+/* Per-thread counters of the calling context (0 = ok, GCS_E* otherwise). */
+struct gpucsum_stats {
+	uint64_t rx_frames;      /* frames seen in recv_pkts                         */
+	uint64_t rx_errors;      /* frames returned as NULL by get_rptr              */
+	uint64_t rx_batches;     /* GPU verify launches                              */
+	uint64_t tx_frames;      /* frames filled in send_pkts                       */
+	uint64_t tx_batches;     /* GPU fill launches                                */
+	uint64_t gpu_failures;   /* GPU calls that failed (frames then dropped/unsent)*/
+	int      device;         /* HIP device of this context                       */
+};
+int gpucsum_get_stats(struct mtcp_thread_context *ctx, struct gpucsum_stats *out);
+
+/* Verdict of frame `index` of the last recv_pkts burst on `ifidx`
+ * (GCS_V_* of mtcp_gpucsum.h), or -1. */
+int gpucsum_rx_verdict(struct mtcp_thread_context *ctx, int ifidx, int index);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPUCSUM_IO_MODULE_H */

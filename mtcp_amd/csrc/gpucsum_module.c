@@ -1,0 +1,355 @@
+/*
+ * gpucsum_module.c -- the io_module_func decorator of gpucsum_io_module.h.
+ *
+ * Semantics follow the reference's checksum-offload contract:
+ *   dev_ioctl answers      dpdk_module.c:805-928 (0 = device did it, -1 = software)
+ *   bad-checksum RX drop   dpdk_get_rptr returning NULL, dpdk_module.c:536-542,
+ *                          counted by core.c:794-799 as rx_errors
+ *   TX ownership           a get_wptr buffer is complete once the next get_wptr /
+ *                          send_pkts is called (mTCP writes each frame fully in
+ *                          SendTCPPacket before asking for the next, tcp_out.c:223-357)
+ *   RX ownership           get_rptr pointers live until the next recv_pkts on the
+ *                          same ifidx (dpdk_module.c:458-461)
+ * The checksum work itself is libmtcp_gpucsum's gcs_verify_ptrs /
+ * gcs_compute_ptrs (one GPU batch per burst).  There is no CPU fallback: a
+ * context that cannot reach its GPU exits at init_handle like the reference's
+ * modules do (dpdk_module.c:243-247), and a failing batch is reported on
+ * stderr and its frames are dropped.
+ */
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/mtcp_gpucsum.h"
+#include "../../include/gpucsum_io_module.h"
+
+#define GPUCSUM_MAX_THREADS 256
+#define GPUCSUM_STAGE_BYTES_PER_FRAME 2048   /* MAX_PKT_SIZE, mtcp.h:52 */
+
+struct rx_if {
+	int32_t n;
+	uint8_t *ptr[GPUCSUM_MAX_BURST];
+	uint16_t len[GPUCSUM_MAX_BURST];
+	uint8_t verdict[GPUCSUM_MAX_BURST];
+};
+
+struct tx_if {
+	uint32_t n;
+	uint8_t *ptr[GPUCSUM_MAX_BURST];
+	uint16_t len[GPUCSUM_MAX_BURST];
+	uint8_t status[GPUCSUM_MAX_BURST];
+};
+
+struct gthr {
+	struct mtcp_thread_context *ctx;
+	gcs_ctx *gcs;
+	struct rx_if *rx[GPUCSUM_MAX_IFS];
+	struct tx_if *tx[GPUCSUM_MAX_IFS];
+	struct gpucsum_stats st;
+};
+
+static io_module_func *g_inner;
+static struct gthr *g_table[GPUCSUM_MAX_THREADS];
+static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER;
+static int g_next_ordinal;
+static __thread struct gthr *t_cache;
+
+int gpucsum_set_inner(io_module_func *inner)
+{
+	if (!inner || inner == &gpucsum_module_func)
+		return GCS_EINVAL;
+	g_inner = inner;
+	return GCS_OK;
+}
+
+static struct gthr *lookup(struct mtcp_thread_context *ctx)
+{
+	struct gthr *g = t_cache;
+	int i;
+
+	if (g && g->ctx == ctx)
+		return g;
+	g = NULL;
+	pthread_mutex_lock(&g_lock);
+	for (i = 0; i < GPUCSUM_MAX_THREADS; i++)
+		if (g_table[i] && g_table[i]->ctx == ctx) {
+			g = g_table[i];
+			break;
+		}
+	pthread_mutex_unlock(&g_lock);
+	if (g)
+		t_cache = g;
+	return g;
+}
+
+static void die(const char *what, int rc)
+{
+	fprintf(stderr, "[gpucsum] %s failed: %s (%d) %s\n", what, gcs_strerror(rc), rc,
+	        gcs_last_hip_error());
+	exit(EXIT_FAILURE);
+}
+
+/* ---- vtable ------------------------------------------------------------ */
+
+static void gpucsum_load_module(void)
+{
+	int n = 0, rc;
+
+	if (!g_inner) {
+		fprintf(stderr, "[gpucsum] no inner I/O module: call gpucsum_set_inner() first\n");
+		exit(EXIT_FAILURE);
+	}
+	rc = gcs_device_count(&n);
+	if (rc || n <= 0)
+		die("gcs_device_count (no MI355X visible)", rc ? rc : GCS_ENODEV);
+	if (g_inner->load_module)
+		g_inner->load_module();
+}
+
+static void gpucsum_init_handle(struct mtcp_thread_context *ctx)
+{
+	struct gthr *g;
+	int ndev = 0, dev, ordinal, i, rc;
+	const char *env = getenv("GPUCSUM_DEVICE");
+
+	if (g_inner->init_handle)
+		g_inner->init_handle(ctx);
+	g = calloc(1, sizeof(*g));
+	if (!g)
+		die("calloc", GCS_ENOMEM);
+	g->ctx = ctx;
+	pthread_mutex_lock(&g_lock);
+	ordinal = g_next_ordinal++;
+	for (i = 0; i < GPUCSUM_MAX_THREADS && g_table[i]; i++)
+		;
+	if (i == GPUCSUM_MAX_THREADS) {
+		pthread_mutex_unlock(&g_lock);
+		die("thread table", GCS_ERANGE);
+	}
+	g_table[i] = g;
+	pthread_mutex_unlock(&g_lock);
+
+	rc = gcs_device_count(&ndev);
+	if (rc || ndev <= 0)
+		die("gcs_device_count", rc ? rc : GCS_ENODEV);
+	dev = env ? atoi(env) : ordinal % ndev;   /* mTCP thread k -> GPU k mod n */
+	rc = gcs_ctx_create(&g->gcs, dev, GPUCSUM_MAX_BURST,
+	                    (uint64_t)GPUCSUM_MAX_BURST * GPUCSUM_STAGE_BYTES_PER_FRAME);
+	if (rc)
+		die("gcs_ctx_create", rc);
+	g->st.device = dev;
+	t_cache = g;
+}
+
+static int32_t gpucsum_link_devices(struct mtcp_thread_context *ctx)
+{
+	return g_inner->link_devices ? g_inner->link_devices(ctx) : 0;
+}
+
+static void gpucsum_release_pkt(struct mtcp_thread_context *ctx, int ifidx,
+                                unsigned char *pkt_data, int len)
+{
+	if (g_inner->release_pkt)
+		g_inner->release_pkt(ctx, ifidx, pkt_data, len);
+}
+
+static struct tx_if *txq(struct gthr *g, int ifidx)
+{
+	if (ifidx < 0 || ifidx >= GPUCSUM_MAX_IFS)
+		return NULL;
+	if (!g->tx[ifidx])
+		g->tx[ifidx] = calloc(1, sizeof(struct tx_if));
+	return g->tx[ifidx];
+}
+
+/* TX fill of every queued frame of one interface (ip_out.c:155-173 and
+ * tcp_out.c:323-333, batched). */
+static void flush_tx(struct gthr *g, struct tx_if *q)
+{
+	int rc;
+
+	if (!q || q->n == 0)
+		return;
+	rc = gcs_compute_ptrs(g->gcs, q->ptr, q->len, q->n, q->status, NULL);
+	if (rc) {
+		g->st.gpu_failures++;
+		fprintf(stderr, "[gpucsum] TX fill of %u frames failed: %s %s\n", q->n,
+		        gcs_strerror(rc), gcs_last_hip_error());
+	} else {
+		g->st.tx_frames += q->n;
+		g->st.tx_batches++;
+	}
+	q->n = 0;
+}
+
+static uint8_t *gpucsum_get_wptr(struct mtcp_thread_context *ctx, int ifidx, uint16_t len)
+{
+	struct gthr *g = lookup(ctx);
+	struct tx_if *q;
+	uint8_t *p = g_inner->get_wptr(ctx, ifidx, len);
+
+	if (!p || !g)
+		return p;
+	q = txq(g, ifidx);
+	if (!q)
+		return p;
+	if (q->n == GPUCSUM_MAX_BURST)
+		flush_tx(g, q);        /* all queued frames are complete by now */
+	q->ptr[q->n] = p;
+	q->len[q->n] = len;
+	q->n++;
+	return p;
+}
+
+static int32_t gpucsum_send_pkts(struct mtcp_thread_context *ctx, int nif)
+{
+	struct gthr *g = lookup(ctx);
+
+	if (g && nif >= 0 && nif < GPUCSUM_MAX_IFS)
+		flush_tx(g, g->tx[nif]);
+	return g_inner->send_pkts(ctx, nif);
+}
+
+static int32_t gpucsum_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
+{
+	struct gthr *g = lookup(ctx);
+	struct rx_if *r;
+	int32_t n = g_inner->recv_pkts(ctx, ifidx), i;
+	int rc;
+
+	if (!g || ifidx < 0 || ifidx >= GPUCSUM_MAX_IFS)
+		return n;
+	if (!g->rx[ifidx])
+		g->rx[ifidx] = calloc(1, sizeof(struct rx_if));
+	r = g->rx[ifidx];
+	if (!r)
+		return n;
+	r->n = 0;
+	if (n <= 0)
+		return n;
+	if (n > GPUCSUM_MAX_BURST)
+		n = GPUCSUM_MAX_BURST;
+	for (i = 0; i < n; i++) {
+		r->len[i] = 0;
+		r->ptr[i] = g_inner->get_rptr(ctx, ifidx, i, &r->len[i]);
+		if (!r->ptr[i])
+			r->len[i] = 0;
+	}
+	rc = gcs_verify_ptrs(g->gcs, r->ptr, r->len, (uint32_t)n, r->verdict,
+	                     GCS_VF_ZERO_BAD_TCP_CHECK);
+	if (rc) {
+		g->st.gpu_failures++;
+		fprintf(stderr, "[gpucsum] RX verify of %d frames failed: %s %s\n", n,
+		        gcs_strerror(rc), gcs_last_hip_error());
+		memset(r->verdict, GCS_V_DROP_TRUNC, (size_t)n);
+	} else {
+		g->st.rx_batches++;
+	}
+	for (i = 0; i < n; i++)
+		if (!r->ptr[i])
+			r->verdict[i] = GCS_V_DROP_TRUNC;   /* the inner module's own drop */
+	g->st.rx_frames += (uint64_t)n;
+	r->n = n;
+	return n;
+}
+
+static uint8_t *gpucsum_get_rptr(struct mtcp_thread_context *ctx, int ifidx, int index,
+                                 uint16_t *len)
+{
+	struct gthr *g = lookup(ctx);
+	struct rx_if *r = (g && ifidx >= 0 && ifidx < GPUCSUM_MAX_IFS) ? g->rx[ifidx] : NULL;
+
+	if (!r || index < 0 || index >= r->n)
+		return g_inner->get_rptr(ctx, ifidx, index, len);
+	if (GCS_V_IS_ERROR(r->verdict[index])) {
+		g->st.rx_errors++;
+		return NULL;
+	}
+	*len = r->len[index];
+	return r->ptr[index];
+}
+
+static int32_t gpucsum_select(struct mtcp_thread_context *ctx)
+{
+	return g_inner->select ? g_inner->select(ctx) : 0;
+}
+
+static void gpucsum_destroy_handle(struct mtcp_thread_context *ctx)
+{
+	struct gthr *g = lookup(ctx);
+	int i;
+
+	if (g_inner->destroy_handle)
+		g_inner->destroy_handle(ctx);
+	if (!g)
+		return;
+	pthread_mutex_lock(&g_lock);
+	for (i = 0; i < GPUCSUM_MAX_THREADS; i++)
+		if (g_table[i] == g)
+			g_table[i] = NULL;
+	pthread_mutex_unlock(&g_lock);
+	if (t_cache == g)
+		t_cache = NULL;
+	if (g->gcs)
+		gcs_ctx_destroy(g->gcs);
+	for (i = 0; i < GPUCSUM_MAX_IFS; i++) {
+		free(g->rx[i]);
+		free(g->tx[i]);
+	}
+	free(g);
+}
+
+/* dpdk_dev_ioctl (dpdk_module.c:805-928) answers 0 when the NIC does the
+ * work; here the GPU does it, in recv_pkts (RX) and send_pkts (TX). */
+static int32_t gpucsum_dev_ioctl(struct mtcp_thread_context *ctx, int nif, int cmd, void *argp)
+{
+	switch (cmd) {
+	case PKT_TX_IP_CSUM:          /* ip_out.c:91, :163 (ICMP)          */
+	case PKT_TX_TCPIP_CSUM:       /* tcp_out.c:206, :326               */
+	case PKT_RX_IP_CSUM:          /* ip_in.c:30                        */
+	case PKT_RX_TCP_CSUM:         /* tcp_in.c:1227                     */
+	case PKT_TX_TCPIP_CSUM_PEEK:  /* ip_out.c:88, :160                 */
+		return 0;
+	case PKT_TX_TCP_CSUM:         /* NIC pseudo-header mode: not ours  */
+		return -1;
+	default:                      /* DRV_NAME, PKT_RX_TCP_LROSEG, ...  */
+		if (g_inner && g_inner->dev_ioctl)
+			return g_inner->dev_ioctl(ctx, nif, cmd, argp);
+		return -1;
+	}
+}
+
+io_module_func gpucsum_module_func = {
+	.load_module    = gpucsum_load_module,
+	.init_handle    = gpucsum_init_handle,
+	.link_devices   = gpucsum_link_devices,
+	.release_pkt    = gpucsum_release_pkt,
+	.get_wptr       = gpucsum_get_wptr,
+	.send_pkts      = gpucsum_send_pkts,
+	.get_rptr       = gpucsum_get_rptr,
+	.recv_pkts      = gpucsum_recv_pkts,
+	.select         = gpucsum_select,
+	.destroy_handle = gpucsum_destroy_handle,
+	.dev_ioctl      = gpucsum_dev_ioctl,
+};
+
+int gpucsum_get_stats(struct mtcp_thread_context *ctx, struct gpucsum_stats *out)
+{
+	struct gthr *g = lookup(ctx);
+
+	if (!g || !out)
+		return GCS_EINVAL;
+	*out = g->st;
+	return GCS_OK;
+}
+
+int gpucsum_rx_verdict(struct mtcp_thread_context *ctx, int ifidx, int index)
+{
+	struct gthr *g = lookup(ctx);
+	struct rx_if *r = (g && ifidx >= 0 && ifidx < GPUCSUM_MAX_IFS) ? g->rx[ifidx] : NULL;
+
+	if (!r || index < 0 || index >= r->n)
+		return -1;
+	return r->verdict[index];
+}
