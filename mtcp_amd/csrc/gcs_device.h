@@ -46,11 +46,24 @@ enum { WM_HALFWORD = 0,   // two 2-byte stores by the group leader
 // ---------------------------------------------------------------------------
 // scalar helpers
 
-__device__ __forceinline__ u32 hsum(u32 d) { return (d & 0xFFFFu) + (d >> 16); }
+// acc + lo16(d) + hi16(d) in ONE VALU op: v_sad_u16(d, 0, acc) =
+// |d.lo - 0| + |d.hi - 0| + acc.
+__device__ __forceinline__ u32 sad(u32 d, u32 acc) { return __builtin_amdgcn_sad_u16(d, 0u, acc); }
 
-__device__ __forceinline__ u32 hsum4(uint4 v)
+__device__ __forceinline__ u32 hsum(u32 d) { return sad(d, 0u); }
+
+__device__ __forceinline__ u32 sad4(uint4 v, u32 acc)
 {
-    return hsum(v.x) + hsum(v.y) + hsum(v.z) + hsum(v.w);
+    return sad(v.w, sad(v.z, sad(v.y, sad(v.x, acc))));
+}
+
+__device__ __forceinline__ u32 hsum4(uint4 v) { return sad4(v, 0u); }
+
+// byte mask keeping the low r bytes of a dword, r clamped to [0, 4]
+__device__ __forceinline__ u32 low_mask(int r)
+{
+    r = r < 0 ? 0 : (r > 4 ? 4 : r);
+    return (u32)((1ull << (8 * r)) - 1ull);
 }
 
 // two-step fold of tcp_util.c:271-272 (also what ps.h's addw/adcl produces)
@@ -65,22 +78,18 @@ __device__ __forceinline__ u32 csum16(u32 s) { return (~fold16(s)) & 0xFFFFu; }
 
 __device__ __forceinline__ u32 bswap16(u32 v) { return ((v >> 8) & 0xFFu) | ((v & 0xFFu) << 8); }
 
-// keep the low r bytes of d, r clamped to [0, 4]
-__device__ __forceinline__ u32 keep_low(u32 d, int r)
+// Mask of the 16-bit words of a dword at frame offset p (p % 4 == 0) that lie
+// in [a, b), a even.  A word straddling b (b odd) keeps its low byte only: the
+// reference's `*w & ntohs(0xFF00)` on a little-endian host.
+__device__ __forceinline__ u32 region_mask(int p, int a, int b)
 {
-    r = r < 0 ? 0 : (r > 4 ? 4 : r);
-    return d & (u32)((1ull << (8 * r)) - 1ull);
+    u32 start = p >= a ? 0xFFFFFFFFu : (p + 2 >= a ? 0xFFFF0000u : 0u);
+    return start & low_mask(b - p);
 }
 
-// Sum of the 16-bit words of dword d (frame offset p, p % 4 == 0) that lie in
-// [a, b), a even.  A word straddling b (b odd) contributes its low byte only:
-// the reference's `*w & ntohs(0xFF00)` on a little-endian host.
 __device__ __forceinline__ u32 region_sum(u32 d, int p, int a, int b)
 {
-    u32 t = keep_low(d, b - p);
-    u32 lo = (p >= a) ? (t & 0xFFFFu) : 0u;
-    u32 hi = (p + 2 >= a) ? (t >> 16) : 0u;
-    return lo + hi;
+    return hsum(d & region_mask(p, a, b));
 }
 
 __device__ __forceinline__ u32 pick(uint4 v, int k)
@@ -197,16 +206,20 @@ template <bool COMPUTE>
 __device__ __forceinline__ void accum_chunk(uint4 v, int cb, int ts, int te, Acc& a)
 {
     if (cb >= ts && cb + 16 <= te) {          // interior of the TCP segment
-        a.tcp += hsum4(v);
+        a.tcp = sad4(v, a.tcp);
     } else if (cb < ts || cb < te) {          // edge chunk: exact word masks
         int p = cb;
-        a.ip += region_sum(v.x, p, 14, ts) + region_sum(v.y, p + 4, 14, ts) +
-                region_sum(v.z, p + 8, 14, ts) + region_sum(v.w, p + 12, 14, ts);
-        a.tcp += region_sum(v.x, p, ts, te) + region_sum(v.y, p + 4, ts, te) +
-                 region_sum(v.z, p + 8, ts, te) + region_sum(v.w, p + 12, ts, te);
+        a.ip = sad(v.x & region_mask(p, 14, ts), a.ip);
+        a.ip = sad(v.y & region_mask(p + 4, 14, ts), a.ip);
+        a.ip = sad(v.z & region_mask(p + 8, 14, ts), a.ip);
+        a.ip = sad(v.w & region_mask(p + 12, 14, ts), a.ip);
+        a.tcp = sad(v.x & region_mask(p, ts, te), a.tcp);
+        a.tcp = sad(v.y & region_mask(p + 4, ts, te), a.tcp);
+        a.tcp = sad(v.z & region_mask(p + 8, ts, te), a.tcp);
+        a.tcp = sad(v.w & region_mask(p + 12, ts, te), a.tcp);
         if (cb == 16) {
             // pseudo header: saddr halves at 26, 28; daddr low half at 30
-            a.tcp += (v.z >> 16) + hsum(v.w);
+            a.tcp = sad(v.w, sad(v.z & 0xFFFF0000u, a.tcp));
             if (COMPUTE)
                 a.ip -= v.z & 0xFFFFu;        // iph->check is 0 when folded (ip_out.c:153)
         } else if (cb == 32) {
@@ -223,6 +236,60 @@ __device__ __forceinline__ void accum_chunk(uint4 v, int cb, int ts, int te, Acc
         if (pd >= cb && pd < cb + 16)
             a.x += (pick(v, (pd - cb) >> 2) >> 16) & 0xFFu;
     }
+}
+
+// ihl == 5 (ts = 34), the header mTCP always emits (ip_out.c:72, :143): the
+// word masks of chunks 0..3 are constants of the chunk index, so each lane
+// computes them once.  ip = words [14, 34); tcp = words [34, te) plus the
+// pseudo-header address halves at 26..33 (tcp_util.c:266-267); COMPUTE
+// leaves out iph->check (bytes 24-25) and tcph->check (bytes 50-51).
+struct Mask5 {
+    u32 ip[4];
+    u32 tcp[4];
+};
+
+template <bool COMPUTE>
+__device__ __forceinline__ Mask5 masks5(int c)
+{
+    const u32 F = 0xFFFFFFFFu, H = 0xFFFF0000u, Lo = 0x0000FFFFu;
+    Mask5 m;
+    m.ip[0] = c == 2 ? Lo : (c == 1 ? F : 0u);               // 32-33 | 16-19
+    m.ip[1] = c == 1 ? F : 0u;                                // 20-23
+    m.ip[2] = c == 1 ? (COMPUTE ? H : F) : 0u;                // 24-27
+    m.ip[3] = c == 1 ? F : (c == 0 ? H : 0u);                 // 28-31 | 14-15
+    m.tcp[0] = c >= 2 ? ((COMPUTE && c == 3) ? Lo : F) : 0u;  // 32-35 ... 48-51
+    m.tcp[1] = c >= 2 ? F : 0u;
+    m.tcp[2] = c >= 2 ? F : (c == 1 ? H : 0u);                // 26-27 (saddr lo)
+    m.tcp[3] = c >= 1 ? F : 0u;                               // 28-31 (saddr hi, daddr lo)
+    return m;
+}
+
+// HDR: the chunk may be one of chunks 0..3 (masks m); otherwise it is a
+// TCP-segment chunk (c >= 4) and only te limits it.
+template <bool COMPUTE, bool HDR>
+__device__ __forceinline__ void accum_fast5(uint4 v, int c, int te, const Mask5& m, Acc& a)
+{
+    const int cb = 16 * c;
+    u32 t0 = HDR ? m.tcp[0] : 0xFFFFFFFFu, t1 = HDR ? m.tcp[1] : 0xFFFFFFFFu;
+    u32 t2 = HDR ? m.tcp[2] : 0xFFFFFFFFu, t3 = HDR ? m.tcp[3] : 0xFFFFFFFFu;
+    if (HDR) {
+        a.ip = sad(v.x & m.ip[0], a.ip);
+        a.ip = sad(v.y & m.ip[1], a.ip);
+        a.ip = sad(v.z & m.ip[2], a.ip);
+        a.ip = sad(v.w & m.ip[3], a.ip);
+        if (!COMPUTE && c == 2)
+            a.x += (v.w >> 16) & 0xFFu;           // byte 46: doff << 4 | res
+    }
+    if (cb + 16 > te) {                           // the chunk holding the segment's end
+        t0 &= low_mask(te - cb);
+        t1 &= low_mask(te - cb - 4);
+        t2 &= low_mask(te - cb - 8);
+        t3 &= low_mask(te - cb - 12);
+    }
+    a.tcp = sad(v.x & t0, a.tcp);
+    a.tcp = sad(v.y & t1, a.tcp);
+    a.tcp = sad(v.z & t2, a.tcp);
+    a.tcp = sad(v.w & t3, a.tcp);
 }
 
 // Verdict for one frame, in the reference's order.
@@ -369,9 +436,17 @@ __device__ __forceinline__ void do_frame(uint8_t* __restrict__ f, u32 len, int64
     const int te = 14 + (int)bswap16(h.d4 & 0xFFFFu);
 
     Acc a = {0u, 0u, 0u};
+    if (__all(ts == 34)) {                    // wave-uniform: every frame has ihl == 5
+        const Mask5 m = masks5<COMPUTE>(sub);
+        accum_fast5<COMPUTE, true>(v[0], sub, te, m, a);
 #pragma unroll
-    for (int j = 0; j < U; j++)
-        accum_chunk<COMPUTE>(v[j], 16 * (j * G + sub), ts, te, a);
+        for (int j = 1; j < U; j++)
+            accum_fast5<COMPUTE, false>(v[j], j * G + sub, te, m, a);
+    } else {
+#pragma unroll
+        for (int j = 0; j < U; j++)
+            accum_chunk<COMPUTE>(v[j], 16 * (j * G + sub), ts, te, a);
+    }
     if (LOOP && nchunks > G * U) {
         uint4 w[U];
         for (int base = G * U; base < nchunks; base += G * U) {
