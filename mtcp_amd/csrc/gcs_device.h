@@ -163,8 +163,12 @@ __device__ __forceinline__ void stg16(uint8_t* p, uint4 v)
     if constexpr (WM == WM_SECTOR_NT) {
         __builtin_nontemporal_store(d, reinterpret_cast<u32x4*>(p));
     } else if constexpr (WM == WM_SECTOR_SC1) {
-        // no result register: nothing to wait for before the kernel ends
-        asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(p), "v"(d) : "memory");
+        // No result register, so nothing to wait for before the kernel ends; but
+        // the trailing s_nop 1 is required: hipcc does not pad an asm store, and
+        // its next instruction could overwrite the data VGPRs before the store
+        // has read them (cdna_hip_programming.md §5.7 item 1).
+        asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(d)
+                     : "memory");
     } else {
         *reinterpret_cast<u32x4*>(p) = d;
     }

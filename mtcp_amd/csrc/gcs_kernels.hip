@@ -15,25 +15,81 @@ constexpr int kBlock = 256;
 // 531 -> 515 us against 2-byte stores).
 constexpr bool kNT = true;
 constexpr int kWM = WM_SECTOR_SC1;
+// XCD-contiguous frame ranges (xcd_block below): TX+RX step 491 -> 485 us.
+constexpr bool kXCD = true;
 
 // Fixed stride: frame i at frames + i*stride, length frame_len,
 // 16*ceil(frame_len/16) <= stride.  One frame per G-lane group, 256/G frames
 // per workgroup, one workgroup per 256/G frames (no grid-stride loop: the
 // short-lived waves keep more bytes in flight than a persistent grid did).
-template <int G, int U, bool COMPUTE, bool LOOP, bool NT, int WM>
+// XCD-aware block order (cdna_hip_programming.md T1): workgroups are dealt
+// round-robin over the 8 XCDs, so block b runs on the XCD of b % 8.  Remap b
+// to a logical block such that every XCD owns ONE contiguous range of frames:
+// the per-frame outputs (verdict bytes, csums) of neighbouring frames are then
+// written through the same XCD L2 and leave it as whole sectors instead of
+// partial ones from eight L2s.  Bijective for any grid size; speed only.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb)
+{
+    const uint32_t q = nb / 8, r = nb % 8, x = b % 8, k = b / 8;
+    return x < r ? x * (q + 1) + k : r * (q + 1) + (x - r) * q + k;
+}
+
+template <int G, int U, bool COMPUTE, bool LOOP, bool NT, int WM, bool XCD = false>
 __global__ void __launch_bounds__(kBlock)
 k_fixed(uint8_t* __restrict__ frames, uint64_t stride, u32 frame_len, u32 n,
         uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags)
 {
     constexpr int FPB = kBlock / G;                    // frames per block
     const int sub = threadIdx.x & (G - 1);
-    const uint64_t i = (uint64_t)blockIdx.x * FPB + threadIdx.x / G;
+    const uint32_t blk = XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint64_t i = (uint64_t)blk * FPB + threadIdx.x / G;
     if (i >= n)
         return;                                        // whole group leaves together
     do_frame<G, U, COMPUTE, LOOP, false, NT, WM>(frames + i * stride, frame_len,
                                                  (int64_t)stride, true, sub, flags,
                                                  out_code ? out_code + i : nullptr,
                                                  out_csum ? out_csum + i : nullptr);
+}
+
+// Small frames (<= 64 B, C1): ONE LANE PER FRAME.  A lane loads its frame's
+// (up to) four 16 B chunks itself, so there is no cross-lane reduction, the
+// ihl == 5 word masks are compile-time constants per register, and the 64
+// verdict bytes of a wave are one coalesced 64 B store.  (The G-lane kernels
+// spend most of their instructions on reductions and a per-group epilogue at
+// this size: tools/kbench.hip)
+template <bool COMPUTE, bool NT, bool XCD>
+__global__ void __launch_bounds__(kBlock)
+k_small(uint8_t* __restrict__ frames, uint64_t stride, u32 frame_len, u32 n,
+        uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags)
+{
+    const uint32_t blk = XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint64_t i = (uint64_t)blk * kBlock + threadIdx.x;
+    if (i >= n)
+        return;
+    uint8_t* f = frames + i * stride;
+    const int nch = (int)((frame_len + 15) >> 4);      // <= 4, uniform
+    uint4 v[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+        v[c] = c < nch ? ldg16<NT>(f + 16 * c) : make_uint4(0, 0, 0, 0);
+    Hdr h = {v[0].w, v[1].x, v[1].y};
+    const int ts = 14 + 4 * (int)((h.d3 >> 16) & 15u);
+    const int te = 14 + (int)bswap16(h.d4 & 0xFFFFu);
+    Acc a = {0u, 0u, 0u};
+    if (ts == 34) {
+        // ihl == 5: constant masks (see masks5); only the chunk holding te is cut
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+            accum_fast5<COMPUTE, true>(v[c], c, te, masks5<COMPUTE>(c), a);
+    } else {
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+            accum_chunk<COMPUTE>(v[c], 16 * c, ts, te, a);
+    }
+    // one-lane "group": epilogue<1, 4> finishes the frame (no reduction steps)
+    epilogue<1, 4, COMPUTE, kWM>(h, a, f, frame_len, true, 0, flags,
+                                 out_code ? out_code + i : nullptr,
+                                 out_csum ? out_csum + i : nullptr, true, v);
 }
 
 // Descriptor batch: frame i at frames + off[i], length len[i].
@@ -136,8 +192,8 @@ static hipError_t launch_fixed(uint8_t* frames, uint64_t stride, u32 frame_len, 
 {
     constexpr int FPB = kBlock / G;
     dim3 grid((n + FPB - 1) / FPB);
-    hipLaunchKernelGGL((k_fixed<G, U, COMPUTE, LOOP, kNT, kWM>), grid, dim3(kBlock), 0, s,
-                       frames, stride, frame_len, n, code, csum, flags);
+    hipLaunchKernelGGL((k_fixed<G, U, COMPUTE, LOOP, kNT, kWM, kXCD>), grid, dim3(kBlock), 0,
+                       s, frames, stride, frame_len, n, code, csum, flags);
     return hipGetLastError();
 }
 
@@ -147,7 +203,18 @@ static hipError_t dispatch_fixed(uint8_t* frames, uint64_t stride, u32 frame_len
                                  uint8_t* code, uint32_t* csum, u32 flags, hipStream_t s)
 {
     const u32 chunks = (frame_len + 15) / 16;
-    if (chunks <= 4)   return launch_fixed<4, 1, COMPUTE, false>(frames, stride, frame_len, n, code, csum, flags, s);
+    if (chunks <= 4) {
+        // <= 64 B.  RX: one lane per frame (1M x 64 B: 16.7 us vs 19.8 us with 4 lanes
+        // per frame).  TX keeps 4 lanes per frame: their sector write-back is one
+        // coalesced 1 KiB store per wave, where one lane per frame scatters 64
+        // sectors per store instruction (74 us).
+        if (COMPUTE)
+            return launch_fixed<4, 1, COMPUTE, false>(frames, stride, frame_len, n, code, csum,
+                                                      flags, s);
+        hipLaunchKernelGGL((k_small<COMPUTE, kNT, kXCD>), dim3((n + kBlock - 1) / kBlock),
+                           dim3(kBlock), 0, s, frames, stride, frame_len, n, code, csum, flags);
+        return hipGetLastError();
+    }
     if (chunks <= 8)   return launch_fixed<8, 1, COMPUTE, false>(frames, stride, frame_len, n, code, csum, flags, s);
     if (chunks <= 16)  return launch_fixed<16, 1, COMPUTE, false>(frames, stride, frame_len, n, code, csum, flags, s);
     if (chunks <= 32)  return launch_fixed<32, 1, COMPUTE, false>(frames, stride, frame_len, n, code, csum, flags, s);

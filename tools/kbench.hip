@@ -132,6 +132,49 @@ int main(int argc, char** argv)
         CMP(true, WM_SECTOR_NT, 0u, "64B sector nt stores")
         CMP(true, WM_SECTOR_SC1, 0u, "64B sector sc1 stores")
         CMP(true, WM_SECTOR, (u32)GCS_CF_NO_INPLACE, "no in-place write")
+        vs.push_back({"compute NT no write, no csums (pure fold)", cbytes, [&](hipStream_t st) {
+            hipLaunchKernelGGL((k_fixed<kG, kU, true, false, true, WM_SECTOR_SC1>),
+                               dim3((n + FPB - 1) / FPB), dim3(256), 0, st, tx, stride, L,
+                               (u32)n, nullptr, nullptr, (u32)GCS_CF_NO_INPLACE);
+        }});
+        vs.push_back({"compute NT no write, no csums, over rx", cbytes, [&](hipStream_t st) {
+            hipLaunchKernelGGL((k_fixed<kG, kU, true, false, true, WM_SECTOR_SC1>),
+                               dim3((n + FPB - 1) / FPB), dim3(256), 0, st, rx, stride, L,
+                               (u32)n, nullptr, nullptr, (u32)GCS_CF_NO_INPLACE);
+        }});
+        vs.push_back({"verify NT XCD-mapped", vbytes, [&](hipStream_t st) {
+            hipLaunchKernelGGL((k_fixed<kG, kU, false, false, true, WM_SECTOR_SC1, true>),
+                               dim3((n + FPB - 1) / FPB), dim3(256), 0, st, rx, stride, L,
+                               (u32)n, v1, nullptr, 0u);
+        }});
+        vs.push_back({"compute NT sc1 + csums, XCD-mapped", cbytes, [&](hipStream_t st) {
+            hipLaunchKernelGGL((k_fixed<kG, kU, true, false, true, WM_SECTOR_SC1, true>),
+                               dim3((n + FPB - 1) / FPB), dim3(256), 0, st, tx, stride, L,
+                               (u32)n, nullptr, cs1, 0u);
+        }});
+        vs.push_back({"compute NT sc1 no csums, XCD-mapped", cbytes, [&](hipStream_t st) {
+            hipLaunchKernelGGL((k_fixed<kG, kU, true, false, true, WM_SECTOR_SC1, true>),
+                               dim3((n + FPB - 1) / FPB), dim3(256), 0, st, tx, stride, L,
+                               (u32)n, nullptr, nullptr, 0u);
+        }});
+        vs.push_back({"compute NT sc1 no csums", cbytes, [&](hipStream_t st) {
+            hipLaunchKernelGGL((k_fixed<kG, kU, true, false, true, WM_SECTOR_SC1>),
+                               dim3((n + FPB - 1) / FPB), dim3(256), 0, st, tx, stride, L,
+                               (u32)n, nullptr, nullptr, 0u);
+        }});
+        vs.push_back({"STEP XCD-mapped sc1", cbytes + vbytes, [&](hipStream_t st) {
+            hipLaunchKernelGGL((k_fixed<kG, kU, true, false, true, WM_SECTOR_SC1, true>),
+                               dim3((n + FPB - 1) / FPB), dim3(256), 0, st, tx, stride, L,
+                               (u32)n, nullptr, nullptr, 0u);
+            hipLaunchKernelGGL((k_fixed<kG, kU, false, false, true, WM_SECTOR_SC1, true>),
+                               dim3((n + FPB - 1) / FPB), dim3(256), 0, st, rx, stride, L,
+                               (u32)n, v1, nullptr, 0u);
+        }});
+        vs.push_back({"verify NT over tx", vbytes, [&](hipStream_t st) {
+            hipLaunchKernelGGL((k_fixed<kG, kU, false, false, true, WM_SECTOR_SC1>),
+                               dim3((n + FPB - 1) / FPB), dim3(256), 0, st, tx, stride, L,
+                               (u32)n, v2, nullptr, 0u);
+        }});
         // the bench step: TX compute over tx, then RX verify over rx (one sample)
 #define PAIR(WM_, FL_, TAG)                                                               \
         vs.push_back({std::string("STEP compute(tx)+verify(rx) ") + TAG, cbytes + vbytes,  \
@@ -148,6 +191,27 @@ int main(int argc, char** argv)
         PAIR(WM_SECTOR_NT, 0u, "64B sector nt")
         PAIR(WM_SECTOR_SC1, 0u, "64B sector sc1")
         PAIR(WM_SECTOR, (u32)GCS_CF_NO_INPLACE, "no in-place write")
+    } else if (L <= 64) {
+        vs.push_back({"verify  k_fixed<4,1> (4 lanes/frame)", vbytes, [&](hipStream_t st) {
+            hipLaunchKernelGGL((k_fixed<4, 1, false, false, true, WM_SECTOR_SC1, true>),
+                               dim3((n + 63) / 64), dim3(256), 0, st, rx, stride, L, (u32)n, v2,
+                               nullptr, 0u);
+        }});
+        vs.push_back({"compute k_fixed<4,1> (4 lanes/frame)", cbytes, [&](hipStream_t st) {
+            hipLaunchKernelGGL((k_fixed<4, 1, true, false, true, WM_SECTOR_SC1, true>),
+                               dim3((n + 63) / 64), dim3(256), 0, st, tx, stride, L, (u32)n,
+                               nullptr, nullptr, 0u);
+        }});
+        vs.push_back({"verify  k_small NT=false", vbytes, [&](hipStream_t st) {
+            hipLaunchKernelGGL((k_small<false, false, true>), dim3((n + 255) / 256), dim3(256), 0,
+                               st, rx, stride, L, (u32)n, v2, nullptr, 0u);
+        }});
+        vs.push_back({"verify  dispatch_fixed (k_small)", vbytes, [&](hipStream_t st) {
+            CK(launch_verify_fixed(rx, stride, L, (u32)n, v1, 0u, st));
+        }});
+        vs.push_back({"compute dispatch_fixed (k_small)", cbytes, [&](hipStream_t st) {
+            CK(launch_compute_fixed(tx, stride, L, (u32)n, nullptr, nullptr, 0u, st));
+        }});
     } else {
         vs.push_back({"verify  dispatch_fixed", vbytes, [&](hipStream_t st) {
             CK(launch_verify_fixed(rx, stride, L, (u32)n, v1, 0u, st));
