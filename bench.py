@@ -222,25 +222,38 @@ def c1_small_frames(ctx, torch, steps=20):
             "hbm_gbs_algorithmic": n * (L + 1) / (ms * 1e-3) / 1e9}
 
 
-def pcie_inclusive(gcs, torch, frame_len=1500, n=1 << 18):
-    """Host-resident frames -> gcs_verify (pinned staging, H2D, kernel, D2H of
-    verdicts).  Reported beside the device-resident number, never as `value`."""
+def pcie_inclusive(gcs, torch, frame_len=1500, n=1 << 20):
+    """Host-resident frames through the host entry points: gcs_verify (H2D of
+    the frames, kernel, D2H of 1 B verdicts) and gcs_compute (H2D, kernel, D2H
+    of 4 B checks, written back into the host frames).  Two host layouts:
+    pinned (gcs_host_alloc: one DMA per staging slot, no host copy) and
+    pageable (gathered into pinned staging by GCS_GATHER_THREADS threads).
+    Reported beside the device-resident number, never as `value`."""
     from mtcp_amd import synth
-    buf, stride = synth.fixed_frames(n, frame_len, seed=77)
+    src, stride = synth.fixed_frames(n, frame_len, seed=77)
     off = np.arange(n, dtype=np.uint64) * stride
     lens = np.full(n, frame_len, dtype=np.uint16)
+    pinned = gcs.PinnedBuffer(src.nbytes)
+    pinned.array[:] = src
+    out = {"workload": f"{n} x {frame_len}B frames in host memory, stride {stride}",
+           "pcie": "H2D frames + D2H results, 2 staging slots x 48 MiB"}
     with gcs.Context(torch.cuda.current_device(), max_frames=1 << 16, max_bytes=96 << 20) as c:
-        c.compute_host(buf, off, lens)
-        c.verify_host(buf, off, lens)
-        t0 = time.perf_counter()
-        reps = 3
-        for _ in range(reps):
-            v = c.verify_host(buf, off, lens)
-        dt = (time.perf_counter() - t0) / reps
-    assert int((v != 0).sum()) == 0
-    return {"workload": f"{n} x {frame_len}B host frames, gcs_verify (gather->pinned->H2D->"
-                        "kernel->D2H verdicts)",
-            "gpkt_per_s": n / dt / 1e9, "gib_per_s": n * frame_len / dt / 2**30}
+        for name, buf in (("pinned", pinned.array), ("pageable", src)):
+            c.compute_host(buf, off, lens)
+            for op in ("verify", "compute"):
+                fn = c.verify_host if op == "verify" else c.compute_host
+                fn(buf, off, lens)
+                reps, t0 = 3, time.perf_counter()
+                for _ in range(reps):
+                    r = fn(buf, off, lens)
+                dt = (time.perf_counter() - t0) / reps
+                codes = r if op == "verify" else r[0]
+                assert int((codes != 0).sum()) == 0
+                out[f"{op}_{name}"] = {"gpkt_per_s": n / dt / 1e9,
+                                       "gib_per_s": n * frame_len / dt / 2**30,
+                                       "gb_per_s_h2d": n * stride / dt / 1e9}
+    pinned.free()
+    return out
 
 
 def main():

@@ -109,9 +109,17 @@ int gcs_ctx_device(const gcs_ctx *ctx, int *device);
 int gcs_ctx_stream(const gcs_ctx *ctx, void **stream);   /* hipStream_t */
 int gcs_sync(gcs_ctx *ctx);                               /* wait for ctx stream */
 
-/* Pinned host memory (hipHostMalloc) for zero-staging host batches. */
+/* Pinned host memory for zero-copy host batches: when every frame of a
+ * gcs_verify / gcs_compute call lies in pinned memory (allocated here, or an
+ * existing buffer such as an mbuf pool registered with gcs_host_register) and
+ * the offsets are 16 B-aligned and increasing, the frames go to the GPU with
+ * one DMA per staging slot and no host copy.  Otherwise they are gathered
+ * into the context's pinned staging (environment GCS_GATHER_THREADS threads,
+ * default 8, for large batches). */
 int gcs_host_alloc(void **p, uint64_t bytes);
 int gcs_host_free(void *p);
+int gcs_host_register(void *p, uint64_t bytes);
+int gcs_host_unregister(void *p);
 /* Device memory on the context's device. */
 int gcs_dev_alloc(gcs_ctx *ctx, void **p, uint64_t bytes);
 int gcs_dev_free(gcs_ctx *ctx, void *p);

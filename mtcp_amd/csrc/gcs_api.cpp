@@ -8,9 +8,17 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <new>
+#include <thread>
+#include <vector>
 
 #include "gcs_internal.h"
 
@@ -57,12 +65,129 @@ struct Slot {
 
 }  // namespace
 
+namespace {
+
+// A few host threads that copy frames into pinned staging in parallel (one
+// memcpy stream cannot feed PCIe Gen5).  Parts are handed out by an atomic
+// counter; the calling thread works too and returns when every part is done.
+class GatherPool {
+  public:
+    ~GatherPool()
+    {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : workers_)
+            t.join();
+    }
+
+    void run(uint32_t total, uint32_t parts, const std::function<void(uint32_t, uint32_t)>& fn)
+    {
+        if (workers_.empty())
+            start();
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            job_ = &fn;
+            total_ = total;
+            parts_ = parts;
+            done_ = 0;
+            next_.store(0);
+            gen_++;
+        }
+        cv_.notify_all();
+        work();
+        std::unique_lock<std::mutex> lk(m_);
+        cv_done_.wait(lk, [&] { return done_ == parts_; });
+        job_ = nullptr;
+    }
+
+    static int threads()
+    {
+        const char* e = std::getenv("GCS_GATHER_THREADS");
+        int n = e ? std::atoi(e) : 8;
+        return n < 1 ? 1 : (n > 64 ? 64 : n);
+    }
+
+  private:
+    void start()
+    {
+        for (int i = 1; i < threads(); i++)
+            workers_.emplace_back([this] { loop(); });
+    }
+
+    void loop()
+    {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_)
+                    return;
+                seen = gen_;
+            }
+            work();
+        }
+    }
+
+    void work()
+    {
+        for (;;) {
+            const uint32_t p = next_.fetch_add(1);
+            const std::function<void(uint32_t, uint32_t)>* job;
+            uint32_t parts, total;
+            {
+                std::lock_guard<std::mutex> lk(m_);
+                job = job_;
+                parts = parts_;
+                total = total_;
+            }
+            if (!job || p >= parts)
+                return;
+            (*job)((uint32_t)((uint64_t)total * p / parts),
+                   (uint32_t)((uint64_t)total * (p + 1) / parts));
+            std::lock_guard<std::mutex> lk(m_);
+            if (++done_ == parts_)
+                cv_done_.notify_all();
+        }
+    }
+
+    std::vector<std::thread> workers_;
+    std::mutex m_;
+    std::condition_variable cv_, cv_done_;
+    const std::function<void(uint32_t, uint32_t)>* job_ = nullptr;
+    uint32_t total_ = 0, parts_ = 0, done_ = 0;
+    std::atomic<uint32_t> next_{0};
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+}  // namespace
+
 struct gcs_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     uint32_t max_frames = 0;   // per slot
     uint64_t max_bytes = 0;    // per slot
     Slot slot[kSlots];
+    std::unique_ptr<GatherPool> pool;
+
+    // Copy work for `count` frames / `bytes` bytes: inline when small, else
+    // spread over the gather pool.
+    void gather_run(uint32_t count, uint64_t bytes,
+                    const std::function<void(uint32_t, uint32_t)>& fn)
+    {
+        const int t = GatherPool::threads();
+        if (t <= 1 || bytes < (1u << 20) || count < 64) {
+            fn(0, count);
+            return;
+        }
+        if (!pool)
+            pool.reset(new GatherPool());
+        pool->run(count, (uint32_t)std::min<uint64_t>(4ull * t, count), fn);
+    }
 };
 
 namespace {
@@ -137,8 +262,36 @@ void scatter_tx(uint8_t* f, uint32_t len, uint8_t st, uint32_t cs)
     }
 }
 
+// Is [p, p + bytes) host memory the GPU can DMA from directly (hipHostMalloc'd
+// or hipHostRegister'ed)?
+bool is_pinned(const void* p, uint64_t bytes)
+{
+    if (!p || bytes == 0)
+        return false;
+    const uint8_t* q = static_cast<const uint8_t*>(p);
+    for (const uint8_t* a : {q, q + bytes - 1}) {
+        hipPointerAttribute_t at;
+        if (hipPointerGetAttributes(&at, a) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        if (at.type != hipMemoryTypeHost)
+            return false;
+    }
+    return true;
+}
+
 // Generic staged host batch.  Frames are addressed by base + off[i] or by
 // ptrs[i]; `compute` selects TX fill vs RX verify.
+//
+// Per slot (two slots alternate, so the host work of chunk k+1 overlaps the
+// H2D / kernel / D2H of chunk k):
+//   span mode    base is pinned and the chunk's offsets are 16 B-aligned and
+//                increasing: ONE hipMemcpyAsync of [off[first], end) straight
+//                from the caller's buffer (zero host copies);
+//   gather mode  otherwise: frames are copied into the slot's pinned staging at
+//                64 B-aligned slots (pslib.c:146), split over the context's
+//                gather threads when the chunk is large.
 int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* const* ptrs,
                    const uint16_t* len, uint32_t n, uint8_t* code, uint32_t* csums,
                    uint32_t flags, bool compute)
@@ -155,6 +308,15 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
 
     auto frame_ptr = [&](uint32_t i) -> uint8_t* { return ptrs ? ptrs[i] : base + off[i]; };
 
+    // span mode needs the whole referenced range pinned
+    bool pinned = false;
+    if (base) {
+        uint64_t end = 0;
+        for (uint32_t i = 0; i < n; i++)
+            end = std::max<uint64_t>(end, off[i] + len[i]);
+        pinned = is_pinned(base, end);
+    }
+
     // Drain one slot: wait for its stream and hand its results back.
     auto drain = [&](Slot& s) -> int {
         if (!s.busy)
@@ -165,15 +327,18 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
             std::memcpy(code + s.first, s.h_code, s.count);
             return GCS_OK;
         }
-        for (uint32_t k = 0; k < s.count; k++) {
-            uint32_t i = s.first + k;
-            uint8_t st = s.h_code[k];
-            uint32_t cs = s.h_csum[k];
-            if (code) code[i] = st;
-            if (csums) csums[i] = cs;
-            if (!(flags & GCS_CF_NO_INPLACE) && frame_ptr(i))
-                scatter_tx(frame_ptr(i), len[i], st, cs);
-        }
+        const uint32_t first = s.first;
+        ctx->gather_run(s.count, (uint64_t)s.count * 256, [&, first](uint32_t lo, uint32_t hi) {
+            for (uint32_t k = lo; k < hi; k++) {
+                uint32_t i = first + k;
+                uint8_t st = s.h_code[k];
+                uint32_t cs = s.h_csum[k];
+                if (code) code[i] = st;
+                if (csums) csums[i] = cs;
+                if (!(flags & GCS_CF_NO_INPLACE) && frame_ptr(i))
+                    scatter_tx(frame_ptr(i), len[i], st, cs);
+            }
+        });
         return GCS_OK;
     };
 
@@ -183,27 +348,52 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
         Slot& s = ctx->slot[k % kSlots];
         int rc = drain(s);
         if (rc) return rc;
-        // gather as many frames as fit this slot
         uint64_t used = 0;
         uint32_t cnt = 0;
-        while (next + cnt < n && cnt < ctx->max_frames) {
-            uint32_t i = next + cnt;
-            uint64_t need = (len[i] + kSlotAlign - 1) / kSlotAlign * kSlotAlign;
-            if (used + need > ctx->max_bytes)
-                break;
-            uint8_t* src = frame_ptr(i);
-            if (src)
-                std::memcpy(s.h_frames + used, src, len[i]);
-            s.h_off[cnt] = used;
-            s.h_len[cnt] = src ? len[i] : 0;
-            used += need;
-            cnt++;
+        const uint8_t* h2d_src = s.h_frames;
+        // span mode: frames in place in the caller's pinned buffer
+        if (pinned && (off[next] & 15) == 0) {
+            const uint64_t s0 = off[next];
+            uint64_t prev = s0;
+            while (next + cnt < n && cnt < ctx->max_frames) {
+                uint32_t i = next + cnt;
+                if ((off[i] & 15) || off[i] < prev || off[i] + len[i] - s0 > ctx->max_bytes)
+                    break;
+                s.h_off[cnt] = off[i] - s0;
+                s.h_len[cnt] = len[i];
+                used = std::max<uint64_t>(used, off[i] + len[i] - s0);
+                prev = off[i];
+                cnt++;
+            }
+            h2d_src = base + s0;
         }
-        if (cnt == 0)
-            return GCS_ERANGE;   // a single frame larger than the staging
+        // gather mode
+        if (cnt == 0) {
+            h2d_src = s.h_frames;
+            while (next + cnt < n && cnt < ctx->max_frames) {
+                uint32_t i = next + cnt;
+                uint64_t need = (len[i] + kSlotAlign - 1) / kSlotAlign * kSlotAlign;
+                if (used + need > ctx->max_bytes)
+                    break;
+                s.h_off[cnt] = used;
+                s.h_len[cnt] = frame_ptr(i) ? len[i] : 0;
+                used += need;
+                cnt++;
+            }
+            if (cnt == 0)
+                return GCS_ERANGE;   // a single frame larger than the staging
+            const uint32_t first = next;
+            ctx->gather_run(cnt, used, [&, first](uint32_t lo, uint32_t hi) {
+                for (uint32_t k = lo; k < hi; k++) {
+                    const uint8_t* src = frame_ptr(first + k);
+                    if (src)
+                        std::memcpy(s.h_frames + s.h_off[k], src, s.h_len[k]);
+                }
+            });
+        }
         s.first = next;
         s.count = cnt;
-        HIP_TRY(hipMemcpyAsync(s.d_frames, s.h_frames, used, hipMemcpyHostToDevice, s.stream));
+        HIP_TRY(hipMemcpyAsync(s.d_frames, h2d_src, used, hipMemcpyHostToDevice, s.stream));
         HIP_TRY(hipMemcpyAsync(s.d_off, s.h_off, cnt * sizeof(uint64_t), hipMemcpyHostToDevice,
                                s.stream));
         HIP_TRY(hipMemcpyAsync(s.d_len, s.h_len, cnt * sizeof(uint16_t), hipMemcpyHostToDevice,
@@ -369,6 +559,22 @@ int gcs_host_alloc(void** p, uint64_t bytes)
 int gcs_host_free(void* p)
 {
     HIP_TRY(hipHostFree(p));
+    return GCS_OK;
+}
+
+int gcs_host_register(void* p, uint64_t bytes)
+{
+    if (!p || bytes == 0)
+        return GCS_EINVAL;
+    HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterDefault));
+    return GCS_OK;
+}
+
+int gcs_host_unregister(void* p)
+{
+    if (!p)
+        return GCS_EINVAL;
+    HIP_TRY(hipHostUnregister(p));
     return GCS_OK;
 }
 

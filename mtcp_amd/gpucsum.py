@@ -62,6 +62,8 @@ def lib() -> C.CDLL:
             "gcs_sync": (i, [vp]),
             "gcs_host_alloc": (i, [C.POINTER(vp), u64]),
             "gcs_host_free": (i, [vp]),
+            "gcs_host_register": (i, [vp, u64]),
+            "gcs_host_unregister": (i, [vp]),
             "gcs_dev_alloc": (i, [vp, C.POINTER(vp), u64]),
             "gcs_dev_free": (i, [vp, vp]),
             "gcs_verify_fixed_dev": (i, [vp, vp, u64, u32, u32, vp, u32, vp]),

@@ -315,6 +315,42 @@ def test_host_batches_chunked(torch_dev, O):
         assert (rv[bad] != 0).all()
 
 
+@pytest.mark.parametrize("mode", ["pinned", "registered"])
+def test_host_batches_zero_copy(torch_dev, O, mode):
+    """Pinned / registered host frames take the span (zero host copy) path."""
+    import ctypes as C
+    n = 20000
+    lens = synth.imix_lengths(n, seed=31)
+    buf, off, lens = synth.packed_frames(lens, seed=32)
+    if mode == "pinned":
+        pb = gpucsum.PinnedBuffer(buf.nbytes)
+        host = pb.array
+        host[:] = buf
+    else:
+        host = buf.copy()
+        gpucsum.check(gpucsum.lib().gcs_host_register(host.ctypes.data, host.nbytes))
+    try:
+        with gpucsum.Context(0, max_frames=3000, max_bytes=1 << 20) as c:
+            st, cs = c.compute_host(host, off, lens)
+            ref = buf.copy()
+            rst, rcs = O.compute_batch(ref, off, lens)
+            np.testing.assert_array_equal(st, rst)
+            np.testing.assert_array_equal(cs, rcs)
+            np.testing.assert_array_equal(host, ref)
+            bad = synth.corrupt(ref, off, lens, frac_log2=4, seed=6)
+            host[:] = ref
+            v = c.verify_host(host, off, lens, flags=1)
+            rv = O.verify_batch(ref, off, lens, flags=1)
+            np.testing.assert_array_equal(v, rv)
+            np.testing.assert_array_equal(host, ref)
+            assert (rv[bad] != 0).all()
+    finally:
+        if mode == "pinned":
+            pb.free()
+        else:
+            gpucsum.check(gpucsum.lib().gcs_host_unregister(host.ctypes.data))
+
+
 # ---------------------------------------------------------------------------
 # BASELINE sizes: size-independent properties
 
