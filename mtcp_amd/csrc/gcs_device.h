@@ -416,14 +416,16 @@ __device__ __forceinline__ void epilogue(const Hdr& h, Acc a, uint8_t* __restric
 
 // One frame per group: load, broadcast the header words, accumulate, epilogue.
 // LOOP: frames longer than G*U chunks are walked in further batches (the
-// first batch is kept for the TX write-back).
+// first batch is kept for the TX write-back).  `active` = false: a padding
+// group of a block-uniform loop -- it loads nothing and writes nothing but
+// still takes part in the wave's cross-lane steps.
 template <int G, int U, bool COMPUTE, bool LOOP, bool SAFE, bool NT, int WM>
 __device__ __forceinline__ void do_frame(uint8_t* __restrict__ f, u32 len, int64_t avail,
                                          bool desc_ok, int sub, u32 flags,
                                          uint8_t* __restrict__ out_code,
-                                         uint32_t* __restrict__ out_csum)
+                                         uint32_t* __restrict__ out_csum, bool active = true)
 {
-    const int nchunks = desc_ok ? (int)((len + 15) >> 4) : 0;
+    const int nchunks = (desc_ok && active) ? (int)((len + 15) >> 4) : 0;
     uint4 v[U];
 #pragma unroll
     for (int j = 0; j < U; j++) {
@@ -440,7 +442,7 @@ __device__ __forceinline__ void do_frame(uint8_t* __restrict__ f, u32 len, int64
     const int te = 14 + (int)bswap16(h.d4 & 0xFFFFu);
 
     Acc a = {0u, 0u, 0u};
-    if (__all(ts == 34)) {                    // wave-uniform: every frame has ihl == 5
+    if (__all(ts == 34 || !active)) {         // wave-uniform: every frame has ihl == 5
         const Mask5 m = masks5<COMPUTE>(sub);
         accum_fast5<COMPUTE, true>(v[0], sub, te, m, a);
 #pragma unroll
@@ -465,7 +467,8 @@ __device__ __forceinline__ void do_frame(uint8_t* __restrict__ f, u32 len, int64
                 accum_chunk<COMPUTE>(w[j], 16 * (base + j * G + sub), ts, te, a);
         }
     }
-    epilogue<G, U, COMPUTE, WM>(h, a, f, len, desc_ok, sub, flags, out_code, out_csum, true, v);
+    epilogue<G, U, COMPUTE, WM>(h, a, f, len, desc_ok, sub, flags, out_code, out_csum, active,
+                                v);
 }
 
 }  // namespace gcs

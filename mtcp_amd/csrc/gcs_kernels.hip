@@ -17,6 +17,10 @@ constexpr bool kNT = true;
 constexpr int kWM = WM_SECTOR_SC1;
 // XCD-contiguous frame ranges (xcd_block below): TX+RX step 491 -> 485 us.
 constexpr bool kXCD = true;
+// k_desc_mixed register budget: 6 waves per SIMD (<= 80 VGPRs, no spills).
+// 4M IMIX frames: verify 349 -> 316 us against the unbounded 89-94 VGPRs (5
+// waves); 8 waves spills and takes 385 us.
+constexpr int kDescOcc = 6;
 
 // Fixed stride: frame i at frames + i*stride, length frame_len,
 // 16*ceil(frame_len/16) <= stride.  One frame per G-lane group, 256/G frames
@@ -112,6 +116,80 @@ k_desc(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __re
                                                 ok, sub, flags,
                                                 out_code ? out_code + i : nullptr,
                                                 out_csum ? out_csum + i : nullptr);
+}
+
+// Mixed-size descriptor batch (IMIX, plugin bursts): a block takes 256
+// consecutive frames, sorts them into three LDS lists by size, and runs each
+// list on a group size that fits it: <= 64 B on 4 lanes (1 chunk per lane),
+// <= 768 B on 16 lanes (3 chunks per lane), larger on 32 lanes (3 chunks per
+// lane, then further batches).  Each list is walked by a block-uniform loop
+// so every cross-lane step sees its whole group.  Verdicts / statuses / checks
+// are staged in LDS and leave as one coalesced store per block.
+template <int G, int U, bool COMPUTE, bool LOOP>
+__device__ __forceinline__ void desc_class(uint8_t* __restrict__ frames, uint64_t frames_bytes,
+                                           const uint64_t* __restrict__ off,
+                                           const uint16_t* __restrict__ lens, uint64_t f0,
+                                           const uint16_t* list, int count, u32 flags,
+                                           uint8_t* codes, uint32_t* csums)
+{
+    constexpr int GPB = kBlock / G;                    // groups per block
+    const int g = threadIdx.x / G, sub = threadIdx.x & (G - 1);
+    for (int base = 0; base < count; base += GPB) {    // block-uniform trip count
+        const int k = base + g;
+        const bool active = k < count;
+        const int t = active ? list[k] : list[0];      // list[0] exists: count > 0
+        const uint64_t o = off[f0 + t];
+        const u32 len = lens[f0 + t];
+        uint8_t* f = frames + o;                       // descriptor validated in phase 0
+        do_frame<G, U, COMPUTE, LOOP, true, kNT, kWM>(f, len, (int64_t)(frames_bytes - o), true,
+                                                      sub, flags, codes + t,
+                                                      COMPUTE ? csums + t : nullptr, active);
+    }
+}
+
+template <bool COMPUTE, bool XCD, int OCC = 1>
+__global__ void __launch_bounds__(kBlock, OCC)
+k_desc_mixed(uint8_t* __restrict__ frames, uint64_t frames_bytes,
+             const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens, u32 n,
+             uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags)
+{
+    __shared__ uint16_t list[3][kBlock];
+    __shared__ int cnt[3];
+    __shared__ uint8_t codes[kBlock];
+    __shared__ uint32_t csums[COMPUTE ? kBlock : 1];
+    const uint32_t blk = XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint64_t f0 = (uint64_t)blk * kBlock;
+    const int t = threadIdx.x;
+    if (t < 3)
+        cnt[t] = 0;
+    __syncthreads();
+    // phase 0: validate and classify
+    const uint64_t i = f0 + t;
+    if (i < n) {
+        const uint64_t o = off[i];
+        const u32 len = lens[i];
+        const bool ok = (o & 15) == 0 && o <= frames_bytes && len <= frames_bytes - o;
+        if (!ok) {
+            codes[t] = COMPUTE ? GCS_TX_BAD_DESC : GCS_V_BAD_DESC;
+            if (COMPUTE)
+                csums[t] = 0;
+        } else {
+            const int c = len <= 64 ? 0 : (len <= 768 ? 1 : 2);
+            list[c][atomicAdd(&cnt[c], 1)] = (uint16_t)t;
+        }
+    }
+    __syncthreads();
+    const int n0 = cnt[0], n1 = cnt[1], n2 = cnt[2];
+    if (n0) desc_class<4, 1, COMPUTE, false>(frames, frames_bytes, off, lens, f0, list[0], n0, flags, codes, csums);
+    if (n1) desc_class<16, 3, COMPUTE, false>(frames, frames_bytes, off, lens, f0, list[1], n1, flags, codes, csums);
+    if (n2) desc_class<32, 3, COMPUTE, true>(frames, frames_bytes, off, lens, f0, list[2], n2, flags, codes, csums);
+    __syncthreads();
+    if (i < n) {
+        if (out_code)
+            out_code[i] = codes[t];
+        if (COMPUTE && out_csum)
+            out_csum[i] = csums[t];
+    }
 }
 
 // TCPCalcChecksum(buf + off[i], len[i], saddr[i], daddr[i]), G lanes per item.
@@ -236,14 +314,12 @@ hipError_t launch_compute_fixed(uint8_t* frames, uint64_t stride, u32 frame_len,
     return dispatch_fixed<true>(frames, stride, frame_len, n, status, csums, flags, s);
 }
 
-constexpr int kDescG = 16, kDescU = 2;
 
 hipError_t launch_verify_desc(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
                               const uint16_t* len, u32 n, uint8_t* verdict, u32 flags,
                               hipStream_t s)
 {
-    constexpr int FPB = kBlock / kDescG;
-    hipLaunchKernelGGL((k_desc<kDescG, kDescU, false, kNT, kWM>), dim3((n + FPB - 1) / FPB),
+    hipLaunchKernelGGL((k_desc_mixed<false, kXCD, kDescOcc>), dim3((n + kBlock - 1) / kBlock),
                        dim3(kBlock), 0, s, frames, frames_bytes, off, len, n, verdict,
                        (uint32_t*)nullptr, flags);
     return hipGetLastError();
@@ -253,8 +329,7 @@ hipError_t launch_compute_desc(uint8_t* frames, uint64_t frames_bytes, const uin
                                const uint16_t* len, u32 n, uint8_t* status, uint32_t* csums,
                                u32 flags, hipStream_t s)
 {
-    constexpr int FPB = kBlock / kDescG;
-    hipLaunchKernelGGL((k_desc<kDescG, kDescU, true, kNT, kWM>), dim3((n + FPB - 1) / FPB),
+    hipLaunchKernelGGL((k_desc_mixed<true, kXCD, kDescOcc>), dim3((n + kBlock - 1) / kBlock),
                        dim3(kBlock), 0, s, frames, frames_bytes, off, len, n, status, csums,
                        flags);
     return hipGetLastError();

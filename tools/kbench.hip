@@ -79,8 +79,130 @@ struct Variant {
     std::vector<float> ms;
 };
 
+__global__ void k_hdr_desc(uint8_t* buf, const uint64_t* off, const uint16_t* lens, uint64_t n)
+{
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint8_t* f = buf + off[i];
+    uint32_t len = lens[i], tot = len - 14, doff = len < 66 ? 5 : 8;
+    f[12] = 8; f[13] = 0; f[14] = 0x45; f[15] = 0; f[16] = tot >> 8; f[17] = tot & 255;
+    f[20] = 0x40; f[21] = 0; f[22] = 64; f[23] = 6; f[24] = f[25] = 0;
+    f[46] = doff << 4; f[47] = 0x10; f[50] = f[51] = f[52] = f[53] = 0;
+    if (doff == 8) { f[54] = 1; f[55] = 1; f[56] = 8; f[57] = 10; }
+}
+
+void run_variants(std::vector<Variant>& vs, hipStream_t s, int rounds);
+
+// C3: IMIX 64/576/1500 at 7:4:1, pslib 64 B packing, descriptor kernels.
+int imix_main(uint64_t n, int rounds)
+{
+    std::vector<uint64_t> off(n);
+    std::vector<uint16_t> len(n);
+    uint64_t x = 0x6d746370, total = 0, bytes = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+        uint32_t u = (uint32_t)(x % 12);
+        len[i] = u < 7 ? 64 : (u < 11 ? 576 : 1500);
+        off[i] = total;
+        total += (len[i] + 63) / 64 * 64;
+        bytes += len[i];
+    }
+    uint8_t *tx, *rx, *v1;
+    uint64_t* doff;
+    uint16_t* dlen;
+    uint32_t* sink;
+    CK(hipMalloc(&tx, total));
+    CK(hipMalloc(&rx, total));
+    CK(hipMalloc(&v1, n));
+    CK(hipMalloc(&doff, 8 * n));
+    CK(hipMalloc(&dlen, 2 * n));
+    CK(hipMalloc(&sink, 4));
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    CK(hipMemcpy(doff, off.data(), 8 * n, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dlen, len.data(), 2 * n, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_init, dim3(4096), dim3(256), 0, s, tx, total / 64, (uint64_t)64, 64u);
+    hipLaunchKernelGGL(k_hdr_desc, dim3((n + 255) / 256), dim3(256), 0, s, tx, doff, dlen, n);
+    CK(hipMemcpyAsync(rx, tx, total, hipMemcpyDeviceToDevice, s));
+    CK(launch_compute_desc(rx, total, doff, dlen, (u32)n, nullptr, nullptr, 0, s));
+    CK(hipStreamSynchronize(s));
+    int dev = 0, cus = 0;
+    CK(hipGetDevice(&dev));
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    std::printf("IMIX n %llu, %.3f GB packed, mean frame %.1f B\n", (unsigned long long)n,
+                total / 1e9, (double)bytes / n);
+    const double vb = bytes + n * (1.0 + 10.0), cb = bytes + n * (4.0 + 10.0);
+    std::vector<Variant> vs;
+    vs.push_back({"verify  k_desc<16,2> (one group size)", vb, [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_desc<16, 2, false, true, WM_SECTOR_SC1>), dim3((n + 15) / 16),
+                           dim3(256), 0, st, rx, total, doff, dlen, (u32)n, v1, nullptr, 0u);
+    }});
+    vs.push_back({"compute k_desc<16,2> (one group size)", cb, [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_desc<16, 2, true, true, WM_SECTOR_SC1>), dim3((n + 15) / 16),
+                           dim3(256), 0, st, tx, total, doff, dlen, (u32)n, nullptr, nullptr, 0u);
+    }});
+#define MIXED(C_, OCC_, TAG)                                                               \
+    vs.push_back({std::string(C_ ? "compute" : "verify ") + " k_desc_mixed occ " + TAG,     \
+                  C_ ? cb : vb, [&](hipStream_t st) {                                      \
+        hipLaunchKernelGGL((k_desc_mixed<C_, true, OCC_>), dim3((n + 255) / 256), dim3(256), \
+                           0, st, C_ ? tx : rx, total, doff, dlen, (u32)n,                  \
+                           C_ ? nullptr : v1, nullptr, 0u);                                 \
+    }});
+    MIXED(false, 6, "6") MIXED(false, 8, "8") MIXED(true, 6, "6") MIXED(true, 8, "8")
+    vs.push_back({"verify  desc (launch_verify_desc)", vb, [&](hipStream_t st) {
+        CK(launch_verify_desc(rx, total, doff, dlen, (u32)n, v1, 0u, st));
+    }});
+    vs.push_back({"compute desc (launch_compute_desc)", cb, [&](hipStream_t st) {
+        CK(launch_compute_desc(tx, total, doff, dlen, (u32)n, nullptr, nullptr, 0u, st));
+    }});
+    vs.push_back({"read-ceiling uint4 NT (whole packed buffer)", (double)total,
+                  [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_read<true>), dim3(cus * 8), dim3(256), 0, st, (const uint4*)rx,
+                           total / 16, sink);
+    }});
+    run_variants(vs, s, rounds);
+    std::vector<uint8_t> h(n);
+    CK(hipMemcpy(h.data(), v1, n, hipMemcpyDeviceToHost));
+    size_t bad = 0;
+    for (auto b : h) bad += b != 0;
+    std::printf("non-accept verdicts: %zu (expect 0)\n", bad);
+    return 0;
+}
+
+void run_variants(std::vector<Variant>& vs, hipStream_t s, int rounds)
+{
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (auto& v : vs)
+        for (int w = 0; w < 3; w++) v.run(s);
+    CK(hipStreamSynchronize(s));
+    for (int r = 0; r < rounds; r++) {
+        for (auto& v : vs) {
+            CK(hipEventRecord(e0, s));
+            v.run(s);
+            CK(hipEventRecord(e1, s));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            v.ms.push_back(ms);
+        }
+    }
+    CK(hipGetLastError());
+    for (auto& v : vs) {
+        std::sort(v.ms.begin(), v.ms.end());
+        double med = v.ms[v.ms.size() / 2], mn = v.ms[0];
+        std::printf("%-44s median %8.1f us  min %8.1f us  %7.0f GB/s (%.1f%% of 8 TB/s)\n",
+                    v.name.c_str(), med * 1e3, mn * 1e3, v.bytes / (med * 1e-3) / 1e9,
+                    100.0 * v.bytes / (med * 1e-3) / 8e12);
+    }
+}
+
 int main(int argc, char** argv)
 {
+    if (argc > 1 && std::string(argv[1]) == "imix")
+        return imix_main(argc > 2 ? std::strtoull(argv[2], nullptr, 10) : (4u << 20),
+                         argc > 3 ? std::atoi(argv[3]) : 10);
     uint32_t L = argc > 1 ? std::atoi(argv[1]) : 1500;
     uint64_t n = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : (1u << 20);
     int rounds = argc > 3 ? std::atoi(argv[3]) : 15;
