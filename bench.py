@@ -317,7 +317,8 @@ def main():
         "roofline": {
             "bound": "hbm",
             "kernel": (f"gcs::k_fixed<32,3,{'true' if kname == 'compute' else 'false'},"
-                       f"false,true,2> ({kname})"),
+                       f"false,true,4,true> ({kname}: G=32 lanes x U=3 chunks, NT loads, "
+                       f"sc1 sector write-back, XCD block map)"),
             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": pmc_traffic(f"{kname}_{L}"),
