@@ -40,8 +40,16 @@ enum { WM_HALFWORD = 0,   // two 2-byte stores by the group leader
        WM_CHUNK = 1,      // the 16 B chunk(s) holding a check field, rewritten whole
        WM_SECTOR = 2,     // the 64 B sector(s) holding a check field, rewritten whole
        WM_SECTOR_NT = 3,  // ... with non-temporal stores
-       WM_SECTOR_SC1 = 4  // ... with sc1 (write-through past the XCD L2) stores
+       WM_SECTOR_SC1 = 4, // ... with sc1 (write-through past the XCD L2) stores
+       WM_LINE_SC1 = 5,   // the 128 B line(s) holding a check field, sc1 stores
+       WM_CHUNK_SC1 = 6,  // WM_CHUNK with sc1 stores
+       WM_SECTOR_SC01 = 7 // WM_SECTOR with sc0 sc1 (system scope) stores
 };
+
+__host__ __device__ constexpr bool wm_sc1(int wm)
+{
+    return wm == WM_SECTOR_SC1 || wm == WM_LINE_SC1 || wm == WM_CHUNK_SC1;
+}
 
 // ---------------------------------------------------------------------------
 // scalar helpers
@@ -162,12 +170,15 @@ __device__ __forceinline__ void stg16(uint8_t* p, uint4 v)
     u32x4 d = u32x4{v.x, v.y, v.z, v.w};
     if constexpr (WM == WM_SECTOR_NT) {
         __builtin_nontemporal_store(d, reinterpret_cast<u32x4*>(p));
-    } else if constexpr (WM == WM_SECTOR_SC1) {
+    } else if constexpr (wm_sc1(WM)) {
         // No result register, so nothing to wait for before the kernel ends; but
         // the trailing s_nop 1 is required: hipcc does not pad an asm store, and
         // its next instruction could overwrite the data VGPRs before the store
         // has read them (cdna_hip_programming.md §5.7 item 1).
         asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(d)
+                     : "memory");
+    } else if constexpr (WM == WM_SECTOR_SC01) {
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" : : "v"(p), "v"(d)
                      : "memory");
     } else {
         *reinterpret_cast<u32x4*>(p) = d;
@@ -392,8 +403,10 @@ __device__ __forceinline__ void epilogue(const Hdr& h, Acc a, uint8_t* __restric
                     continue;
                 const bool has_ip = c == 1;
                 const bool has_tcp = wtcp && c == ctcp;
-                const bool take = WM == WM_CHUNK
+                const bool take = (WM == WM_CHUNK || WM == WM_CHUNK_SC1)
                                       ? (has_ip || has_tcp)
+                                      : WM == WM_LINE_SC1
+                                      ? true                       // c < 8: line 0 holds both
                                       : ((c >> 2) == 0 || (wtcp && (c >> 2) == (ctcp >> 2)));
                 if (!take)
                     continue;
@@ -419,20 +432,28 @@ __device__ __forceinline__ void epilogue(const Hdr& h, Acc a, uint8_t* __restric
 // first batch is kept for the TX write-back).  `active` = false: a padding
 // group of a block-uniform loop -- it loads nothing and writes nothing but
 // still takes part in the wave's cross-lane steps.
-template <int G, int U, bool COMPUTE, bool LOOP, bool SAFE, bool NT, int WM>
-__device__ __forceinline__ void do_frame(uint8_t* __restrict__ f, u32 len, int64_t avail,
-                                         bool desc_ok, int sub, u32 flags,
-                                         uint8_t* __restrict__ out_code,
-                                         uint32_t* __restrict__ out_csum, bool active = true)
+template <int G, int U, bool SAFE, bool NT>
+__device__ __forceinline__ void load_first(const uint8_t* __restrict__ f, int nchunks,
+                                           int64_t avail, int sub, uint4 (&v)[U])
 {
-    const int nchunks = (desc_ok && active) ? (int)((len + 15) >> 4) : 0;
-    uint4 v[U];
 #pragma unroll
     for (int j = 0; j < U; j++) {
         int c = j * G + sub;
         v[j] = c < nchunks ? load_chunk<SAFE, NT>(f + 16 * c, avail - 16 * c)
                            : make_uint4(0, 0, 0, 0);
     }
+}
+
+// The frame's first U*G chunks are already in v (load_first); `wf` is where
+// the TX write-back goes (normally f).
+template <int G, int U, bool COMPUTE, bool LOOP, bool SAFE, bool NT, int WM>
+__device__ __forceinline__ void frame_body(const uint4 (&v)[U], uint8_t* __restrict__ f,
+                                           uint8_t* __restrict__ wf, u32 len, int64_t avail,
+                                           bool desc_ok, int sub, u32 flags,
+                                           uint8_t* __restrict__ out_code,
+                                           uint32_t* __restrict__ out_csum, bool active)
+{
+    const int nchunks = (desc_ok && active) ? (int)((len + 15) >> 4) : 0;
     // header words: chunk 0 lives in group lane 0, chunk 1 in group lane 1 (j = 0)
     Hdr h;
     h.d3 = group_bcast<G, 0>(v[0].w);
@@ -467,8 +488,21 @@ __device__ __forceinline__ void do_frame(uint8_t* __restrict__ f, u32 len, int64
                 accum_chunk<COMPUTE>(w[j], 16 * (base + j * G + sub), ts, te, a);
         }
     }
-    epilogue<G, U, COMPUTE, WM>(h, a, f, len, desc_ok, sub, flags, out_code, out_csum, active,
+    epilogue<G, U, COMPUTE, WM>(h, a, wf, len, desc_ok, sub, flags, out_code, out_csum, active,
                                 v);
+}
+
+template <int G, int U, bool COMPUTE, bool LOOP, bool SAFE, bool NT, int WM>
+__device__ __forceinline__ void do_frame(uint8_t* __restrict__ f, u32 len, int64_t avail,
+                                         bool desc_ok, int sub, u32 flags,
+                                         uint8_t* __restrict__ out_code,
+                                         uint32_t* __restrict__ out_csum, bool active = true)
+{
+    const int nchunks = (desc_ok && active) ? (int)((len + 15) >> 4) : 0;
+    uint4 v[U];
+    load_first<G, U, SAFE, NT>(f, nchunks, avail, sub, v);
+    frame_body<G, U, COMPUTE, LOOP, SAFE, NT, WM>(v, f, f, len, avail, desc_ok, sub, flags,
+                                                  out_code, out_csum, active);
 }
 
 }  // namespace gcs

@@ -169,6 +169,119 @@ int imix_main(uint64_t n, int rounds)
     return 0;
 }
 
+// K frames per group, software-pipelined: the loads of frame k+1 are issued
+// before frame k is reduced and written back, so a wave's store tail overlaps
+// its next loads.  OOP: the 64 B write-back goes to scratch + 64*i (a
+// contiguous stream) instead of the frame, to separate the cost of scattered
+// DRAM writes from the cost of the store tail.
+template <int G, int U, int K, bool COMPUTE, int WM, bool OOP>
+__global__ void __launch_bounds__(256)
+k_multi(uint8_t* __restrict__ frames, uint64_t stride, u32 len, u32 n,
+        uint8_t* __restrict__ out_code, uint8_t* __restrict__ scratch)
+{
+    constexpr int FPB = 256 / G;
+    const int sub = threadIdx.x & (G - 1);
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);
+    const uint64_t i0 = (uint64_t)blk * FPB * K + threadIdx.x / G;
+    const int nch = (int)((len + 15) >> 4);
+    uint4 v[U], w[U];
+    if (i0 >= n)
+        return;
+    load_first<G, U, false, true>(frames + i0 * stride, nch, 1 << 30, sub, v);
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint64_t i = i0 + (uint64_t)k * FPB;
+        if (i >= n)
+            break;                                     // group-uniform
+        const bool more = k + 1 < K && i + FPB < n;
+        if (more)
+            load_first<G, U, false, true>(frames + (i + FPB) * stride, nch, 1 << 30, sub, w);
+        uint8_t* f = frames + i * stride;
+        frame_body<G, U, COMPUTE, false, false, true, WM>(
+            v, f, OOP ? scratch + 64 * i : f, len, 1 << 30, true, sub, 0u,
+            COMPUTE ? nullptr : out_code + i, nullptr, true);
+        if (more) {
+#pragma unroll
+            for (int j = 0; j < U; j++)
+                v[j] = w[j];
+        }
+    }
+}
+
+// C2 TX fill: group shapes and write-back policies (1M x 1500 B, XCD-mapped).
+int tx_main(uint64_t n, int rounds)
+{
+    const uint32_t L = 1500;
+    const uint64_t stride = 1536;
+    uint8_t *tx, *rx, *v1;
+    uint32_t* sink;
+    CK(hipMalloc(&tx, n * stride));
+    CK(hipMalloc(&rx, n * stride));
+    CK(hipMalloc(&v1, n));
+    CK(hipMalloc(&sink, 4));
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    hipLaunchKernelGGL(k_init, dim3(4096), dim3(256), 0, s, tx, n, stride, L);
+    hipLaunchKernelGGL(k_hdr, dim3((n + 255) / 256), dim3(256), 0, s, tx, n, stride, L);
+    CK(hipMemcpyAsync(rx, tx, n * stride, hipMemcpyDeviceToDevice, s));
+    CK(launch_compute_fixed(rx, stride, L, n, nullptr, nullptr, 0, s));
+    CK(hipStreamSynchronize(s));
+    int dev = 0, cus = 0;
+    CK(hipGetDevice(&dev));
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    std::printf("TX variants: frame_len %u stride %llu n %llu\n", L, (unsigned long long)stride,
+                (unsigned long long)n);
+    const double vbytes = (double)n * (L + 1), cbytes = (double)n * (L + 4);
+    std::vector<Variant> vs;
+#define TXV(G_, U_, C_, WM_, FL_, TAG)                                                        \
+    vs.push_back({std::string(C_ ? "compute" : "verify ") + " <" #G_ "," #U_ "> " + TAG,      \
+                  C_ ? cbytes : vbytes, [&](hipStream_t st) {                                 \
+        hipLaunchKernelGGL((k_fixed<G_, U_, C_, false, true, WM_, true>),                     \
+                           dim3((n + 256 / G_ - 1) / (256 / G_)), dim3(256), 0, st,           \
+                           C_ ? tx : rx, stride, L, (u32)n, C_ ? nullptr : v1, nullptr, FL_); \
+    }});
+    TXV(32, 3, false, WM_SECTOR_SC1, 0u, "")
+    TXV(16, 6, false, WM_SECTOR_SC1, 0u, "")
+    TXV(64, 2, false, WM_SECTOR_SC1, 0u, "")
+    TXV(8, 12, false, WM_SECTOR_SC1, 0u, "")
+    TXV(32, 3, true, WM_SECTOR_SC1, (u32)GCS_CF_NO_INPLACE, "pure fold (no write-back)")
+    TXV(32, 3, true, WM_SECTOR_SC1, 0u, "64B sector sc1 (shipped)")
+    TXV(32, 3, true, WM_LINE_SC1, 0u, "128B line sc1")
+    TXV(32, 3, true, WM_CHUNK_SC1, 0u, "16B chunks sc1")
+    TXV(32, 3, true, WM_SECTOR_SC01, 0u, "64B sector sc0 sc1")
+    TXV(16, 6, true, WM_SECTOR_SC1, 0u, "64B sector sc1")
+    TXV(64, 2, true, WM_SECTOR_SC1, 0u, "64B sector sc1")
+    TXV(8, 12, true, WM_SECTOR_SC1, 0u, "64B sector sc1")
+    uint8_t* scratch;
+    CK(hipMalloc(&scratch, 64 * n));
+#define MULTI(K_, C_, WM_, OOP_, TAG)                                                         \
+    vs.push_back({std::string(C_ ? "compute" : "verify ") + " <32,3> K=" #K_ " " + TAG,       \
+                  C_ ? cbytes : vbytes, [&](hipStream_t st) {                                 \
+        hipLaunchKernelGGL((k_multi<32, 3, K_, C_, WM_, OOP_>),                               \
+                           dim3((n + 8 * K_ - 1) / (8 * K_)), dim3(256), 0, st,               \
+                           C_ ? tx : rx, stride, L, (u32)n, v1, scratch);                     \
+    }});
+    MULTI(1, true, WM_SECTOR_SC1, true, "64B sector sc1 to a contiguous scratch")
+    MULTI(1, true, WM_SECTOR, true, "64B sector plain to a contiguous scratch")
+    MULTI(2, true, WM_SECTOR_SC1, false, "64B sector sc1, pipelined")
+    MULTI(4, true, WM_SECTOR_SC1, false, "64B sector sc1, pipelined")
+    MULTI(2, false, WM_SECTOR_SC1, false, "pipelined")
+    MULTI(4, false, WM_SECTOR_SC1, false, "pipelined")
+    vs.push_back({"read-ceiling uint4 NT (whole batch bytes)", (double)n * stride,
+                  [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_read<true>), dim3(cus * 8), dim3(256), 0, st, (const uint4*)rx,
+                           n * stride / 16, sink);
+    }});
+    run_variants(vs, s, rounds);
+    std::vector<uint8_t> h(n);
+    CK(launch_verify_fixed(tx, stride, L, (u32)n, v1, 0u, s));
+    CK(hipMemcpy(h.data(), v1, n, hipMemcpyDeviceToHost));
+    size_t bad = 0;
+    for (auto b : h) bad += b != 0;
+    std::printf("tx after all compute variants: %zu non-accept (expect 0)\n", bad);
+    return 0;
+}
+
 void run_variants(std::vector<Variant>& vs, hipStream_t s, int rounds)
 {
     hipEvent_t e0, e1;
@@ -203,6 +316,9 @@ int main(int argc, char** argv)
     if (argc > 1 && std::string(argv[1]) == "imix")
         return imix_main(argc > 2 ? std::strtoull(argv[2], nullptr, 10) : (4u << 20),
                          argc > 3 ? std::atoi(argv[3]) : 10);
+    if (argc > 1 && std::string(argv[1]) == "tx")
+        return tx_main(argc > 2 ? std::strtoull(argv[2], nullptr, 10) : (1u << 20),
+                       argc > 3 ? std::atoi(argv[3]) : 15);
     uint32_t L = argc > 1 ? std::atoi(argv[1]) : 1500;
     uint64_t n = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : (1u << 20);
     int rounds = argc > 3 ? std::atoi(argv[3]) : 15;
