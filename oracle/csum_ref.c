@@ -80,6 +80,86 @@ uint16_t ref_ip_fast_csum(const uint8_t *iph, unsigned int ihl)
 	return (uint16_t)~sum;
 }
 
+/* icmp.c:18-42.  Same word loop as TCPCalcChecksum without a pseudo header;
+ * the odd final byte is the low byte of a word whose high byte the C leaves
+ * uninitialised -- zero here, as in the reference's gcc -O3 object (movzbl),
+ * pinned by tests/golden/icmp_fn.npz. */
+uint16_t ref_icmp_checksum(const uint8_t *buf, int len)
+{
+	uint32_t sum = 0;
+	const uint8_t *w = buf;
+
+	while (len > 1) {
+		sum += ld16(w);
+		w += 2;
+		len -= 2;
+	}
+	if (len == 1)
+		sum += w[0];
+	sum = (sum >> 16) + (sum & 0xFFFFu);
+	sum += (sum >> 16);
+	return (uint16_t)~sum;
+}
+
+/* rss.c:19-25: the key mTCP's RSS address selection assumes. */
+const uint8_t REF_RSS_DEFAULT_KEY[40] = {
+	5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5,
+	5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5};
+
+/* rss.c:13-41: cache[i] = the 32 key bits starting at bit i (MSB-first). */
+void ref_rss_key_cache(const uint8_t *key, uint32_t cache[96])
+{
+	int i;
+	if (!key)
+		key = REF_RSS_DEFAULT_KEY;
+	for (i = 0; i < 96; i++) {
+		uint32_t v = 0;
+		int b;
+		for (b = 0; b < 32; b++) {
+			int bit = i + b;
+			v = (v << 1) | ((key[bit >> 3] >> (7 - (bit & 7))) & 1u);
+		}
+		cache[i] = v;
+	}
+}
+
+/* rss.c:44-86: Toeplitz hash, input bits MSB-first: sip, dip, sp, dp. */
+uint32_t ref_rss_hash(const uint8_t *key, uint32_t sip, uint32_t dip, uint16_t sp,
+                      uint16_t dp)
+{
+	uint32_t cache[96], h = 0;
+	int i;
+	ref_rss_key_cache(key, cache);
+	for (i = 0; i < 32; i++)
+		if ((sip >> (31 - i)) & 1u)
+			h ^= cache[i];
+	for (i = 0; i < 32; i++)
+		if ((dip >> (31 - i)) & 1u)
+			h ^= cache[32 + i];
+	for (i = 0; i < 16; i++)
+		if ((sp >> (15 - i)) & 1u)
+			h ^= cache[64 + i];
+	for (i = 0; i < 16; i++)
+		if ((dp >> (15 - i)) & 1u)
+			h ^= cache[80 + i];
+	return h;
+}
+
+/* rss.c:97-115 */
+int ref_rss_core(const uint8_t *key, uint32_t sip, uint32_t dip, uint16_t sp, uint16_t dp,
+                 int num_queues, int endian_check)
+{
+	static const uint32_t adj[4] = {3u, 1u, 0xFFFFFFFFu, 0xFFFFFFFDu};
+	uint32_t m;
+	if (endian_check) {
+		m = ref_rss_hash(key, sip, dip, sp, dp) & 0x1FFu;
+		m += adj[m & 3u];
+	} else {
+		m = ref_rss_hash(key, sip, dip, sp, dp) & 0x7Fu;
+	}
+	return (int)(m % (uint32_t)num_queues);
+}
+
 /* RX verdict in the reference's order:
  *   eth_in.c:35  ethertype == ETH_P_IP, else ARP/release (not checked)
  *   ip_in.c:21-26  ip_len = ntohs(tot_len); ip_len < 20 -> ERROR
@@ -115,6 +195,17 @@ int ref_rx_verdict(uint8_t *f, uint32_t len, uint32_t flags)
 		return REF_V_DROP_IPCSUM;
 	if (version != 4)
 		return REF_V_NOT_V4;
+	if (proto == 1 && (flags & REF_VF_ICMP)) {
+		/* ProcessICMPPacket (ip_in.c:56) -> ICMPChecksum(icmph, ip_len - ihl*4)
+		 * (icmp.c:89); a negative length sums nothing (0xFFFF: bad). */
+		if (tot_len < 4 * ihl)
+			return REF_V_ICMP_BADCSUM;
+		if (14 + tot_len > len)
+			return REF_V_DROP_TRUNC;
+		return ref_icmp_checksum(iph + 4 * ihl, (int)(tot_len - 4 * ihl)) != 0
+		           ? REF_V_ICMP_BADCSUM
+		           : REF_V_ICMP_OK;
+	}
 	if (proto != 6)
 		return REF_V_NOT_TCP;
 	ts = 14 + 4 * ihl;
@@ -145,6 +236,11 @@ int ref_rx_verdict(uint8_t *f, uint32_t len, uint32_t flags)
  * Non-TCP IPv4 frames get only the IP check (ICMP: ip_out.c:90-92,100). */
 int ref_tx_fill(uint8_t *f, uint32_t len, uint32_t *csums)
 {
+	return ref_tx_fill_f(f, len, csums, 0);
+}
+
+int ref_tx_fill_f(uint8_t *f, uint32_t len, uint32_t *csums, uint32_t flags)
+{
 	uint32_t ihl, proto, tot_len, ts;
 	uint16_t ipc, tcpc;
 	uint8_t *iph, *tcph;
@@ -168,6 +264,21 @@ int ref_tx_fill(uint8_t *f, uint32_t len, uint32_t *csums)
 	memcpy(iph + 10, &ipc, 2);
 	if (csums)
 		*csums = ipc;
+	if (proto == 1 && (flags & REF_CF_ICMP)) {
+		/* ICMPOutput (icmp.c:44-77): icmp_checksum = 0, then ICMPChecksum over
+		 * sizeof(struct icmphdr) + len = tot_len - ihl*4 bytes. */
+		uint8_t *icmph = iph + 4 * ihl;
+		uint16_t icc;
+		if (tot_len < 4 * ihl + 8 || 14 + tot_len > len)
+			return REF_TX_BAD_ICMPLEN;
+		icmph[2] = 0;
+		icmph[3] = 0;
+		icc = ref_icmp_checksum(icmph, (int)(tot_len - 4 * ihl));
+		memcpy(icmph + 2, &icc, 2);
+		if (csums)
+			*csums = (uint32_t)ipc | ((uint32_t)icc << 16);
+		return REF_TX_ICMP_OK;
+	}
 	if (proto != 6)
 		return REF_TX_IP_ONLY;
 	ts = 4 * ihl;
@@ -204,6 +315,62 @@ void ref_compute_batch(uint8_t *buf, uint64_t buf_bytes, const uint64_t *off,
                        const uint16_t *len, uint32_t n, uint8_t *status,
                        uint32_t *csums)
 {
+	ref_compute_batch_f(buf, buf_bytes, off, len, n, status, csums, 0);
+}
+
+/* Steering of one verdict (ref_classify_*): ACCEPT frames only. */
+static void classify_one(const uint8_t *f, int vd, uint32_t *hash, uint16_t *queue,
+                         const uint8_t *key, int num_queues, int endian_check)
+{
+	uint32_t ts, sip, dip;
+	uint16_t sp, dp;
+	if (vd != REF_V_ACCEPT) {
+		if (hash)
+			*hash = 0;
+		if (queue)
+			*queue = 0xFFFF;
+		return;
+	}
+	ts = 14 + 4 * (f[14] & 0x0Fu);
+	sip = ((uint32_t)f[26] << 24) | ((uint32_t)f[27] << 16) | ((uint32_t)f[28] << 8) | f[29];
+	dip = ((uint32_t)f[30] << 24) | ((uint32_t)f[31] << 16) | ((uint32_t)f[32] << 8) | f[33];
+	sp = (uint16_t)((f[ts] << 8) | f[ts + 1]);
+	dp = (uint16_t)((f[ts + 2] << 8) | f[ts + 3]);
+	if (hash)
+		*hash = ref_rss_hash(key, sip, dip, sp, dp);
+	if (queue)
+		*queue = (uint16_t)ref_rss_core(key, sip, dip, sp, dp, num_queues, endian_check);
+}
+
+void ref_classify_batch(uint8_t *buf, uint64_t buf_bytes, const uint64_t *off,
+                        const uint16_t *len, uint32_t n, uint8_t *verdict,
+                        uint32_t *hash, uint16_t *queue, uint32_t flags,
+                        const uint8_t *key, int num_queues, int endian_check)
+{
+	uint32_t i;
+	ref_verify_batch(buf, buf_bytes, off, len, n, verdict, flags);
+	for (i = 0; i < n; i++)
+		classify_one(verdict[i] == REF_V_BAD_DESC ? NULL : buf + off[i], verdict[i],
+		             hash ? hash + i : NULL, queue ? queue + i : NULL, key, num_queues,
+		             endian_check);
+}
+
+void ref_classify_fixed(uint8_t *buf, uint64_t stride, uint32_t frame_len, uint32_t n,
+                        uint8_t *verdict, uint32_t *hash, uint16_t *queue,
+                        uint32_t flags, const uint8_t *key, int num_queues,
+                        int endian_check)
+{
+	uint32_t i;
+	ref_verify_fixed(buf, stride, frame_len, n, verdict, flags);
+	for (i = 0; i < n; i++)
+		classify_one(buf + (uint64_t)i * stride, verdict[i], hash ? hash + i : NULL,
+		             queue ? queue + i : NULL, key, num_queues, endian_check);
+}
+
+void ref_compute_batch_f(uint8_t *buf, uint64_t buf_bytes, const uint64_t *off,
+                         const uint16_t *len, uint32_t n, uint8_t *status,
+                         uint32_t *csums, uint32_t flags)
+{
 	uint32_t i;
 	for (i = 0; i < n; i++) {
 		int s;
@@ -212,7 +379,7 @@ void ref_compute_batch(uint8_t *buf, uint64_t buf_bytes, const uint64_t *off,
 			if (csums)
 				csums[i] = 0;
 		} else {
-			s = ref_tx_fill(buf + off[i], len[i], csums ? &csums[i] : NULL);
+			s = ref_tx_fill_f(buf + off[i], len[i], csums ? &csums[i] : NULL, flags);
 		}
 		if (status)
 			status[i] = (uint8_t)s;
@@ -322,4 +489,12 @@ void ref_ip_checksum_batch(const uint8_t *buf, const uint64_t *off,
 	uint32_t i;
 	for (i = 0; i < n; i++)
 		out[i] = ref_ip_fast_csum(buf + off[i], ihl[i]);
+}
+
+void ref_icmp_checksum_batch(const uint8_t *buf, const uint64_t *off,
+                             const uint16_t *len, uint32_t n, uint16_t *out)
+{
+	uint32_t i;
+	for (i = 0; i < n; i++)
+		out[i] = ref_icmp_checksum(buf + off[i], len[i]);
 }

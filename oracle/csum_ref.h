@@ -16,6 +16,9 @@
  *                          tcp_in.c:1208-1241            (RX verify order)
  *   ref_tx_fill            mtcp/src/ip_out.c:143-173, tcp_out.c:244,323-333
  *                          (TX: check fields zero when folded, then stored)
+ *   ref_icmp_checksum      mtcp/src/icmp.c:18-42         (ICMPChecksum, static)
+ *   ref_rss_hash/_core     mtcp/src/rss.c:13-41,44-86,97-115 (BuildKeyCache,
+ *                          GetRSSHash, GetRSSCPUCore)
  *
  * Parity is pinned: tests/golden/ holds vectors produced by the reference's
  * own compiled objects (oracle/_ref, built from /root/reference sources by
@@ -45,7 +48,10 @@ enum {
 	REF_V_DROP_TCPCSUM = 7, /* TCPCalcChecksum != 0 (tcp_in.c:1231-1239)      */
 	REF_V_DROP_TRUNC = 8,   /* the reference would read past the frame (UB);
 	                           defined here as a drop                          */
-	REF_V_BAD_DESC = 9      /* descriptor misuse (offset/len outside buffer)  */
+	REF_V_BAD_DESC = 9,     /* descriptor misuse (offset/len outside buffer)  */
+	REF_V_ICMP_OK = 10,     /* REF_VF_ICMP: ICMPChecksum == 0 (icmp.c:89-90)  */
+	REF_V_ICMP_BADCSUM = 11 /* REF_VF_ICMP: ICMPChecksum != 0: no echo reply
+	                           (icmp.c:89-91); not an error for mTCP          */
 };
 
 /* TX fill status (same numbering as GCS_TX_*). */
@@ -55,10 +61,14 @@ enum {
 	REF_TX_NOT_IPV4 = 2,    /* untouched                                      */
 	REF_TX_BAD_HDR = 3,     /* ihl < 5 or header beyond frame: untouched      */
 	REF_TX_BAD_TCPLEN = 4,  /* IP written; TCP segment too short / truncated  */
+	REF_TX_ICMP_OK = 5,     /* REF_CF_ICMP: IP and ICMP check written         */
+	REF_TX_BAD_ICMPLEN = 6, /* REF_CF_ICMP: IP written; ICMP < 8 B / truncated */
 	REF_TX_BAD_DESC = 9
 };
 
 #define REF_VF_ZERO_BAD_TCP_CHECK 0x1u  /* tcp_in.c:1237 side effect */
+#define REF_VF_ICMP 0x2u                /* classify ICMP frames by ICMPChecksum */
+#define REF_CF_ICMP 0x2u                /* TX: also fill ICMP checks (icmp.c:67-69) */
 
 /* TCPCalcChecksum(buf, len, saddr, daddr): buf must be readable for
  * len (+1 if odd: the reference reads the whole last halfword, tcp_util.c:262) */
@@ -73,8 +83,43 @@ uint16_t ref_ip_fast_csum(const uint8_t *iph, unsigned int ihl);
 int ref_rx_verdict(uint8_t *frame, uint32_t len, uint32_t flags);
 
 /* One TX frame: fills iph->check / tcph->check in place; returns REF_TX_*.
- * If csums != NULL it receives ip | tcp << 16 of what was written. */
+ * If csums != NULL it receives ip | tcp << 16 of what was written.
+ * ref_tx_fill_f with REF_CF_ICMP also fills the ICMP check of ICMP frames
+ * (ICMPOutput, icmp.c:44-77: checksum = 0, then ICMPChecksum over the whole
+ * ICMP message, tot_len - ihl*4 bytes); csums then holds ip | icmp << 16. */
 int ref_tx_fill(uint8_t *frame, uint32_t len, uint32_t *csums);
+int ref_tx_fill_f(uint8_t *frame, uint32_t len, uint32_t *csums, uint32_t flags);
+
+/* ICMPChecksum(buf, len): LE 16-bit words, an odd final byte added as the
+ * low byte of a zero-high-byte word, two-step fold, ~.  The C leaves the high
+ * byte of `odd_byte` uninitialised (icmp.c:24,33-34); gcc -O3 compiles it
+ * to a zero-extending byte load (movzbl), which tests/golden pins.  len <= 0
+ * sums nothing: 0xFFFF. */
+uint16_t ref_icmp_checksum(const uint8_t *buf, int len);
+
+/* RSS (rss.c).  key: >= 16 bytes (only the first 16 reach the 96 cached
+ * windows, :27-40); NULL = the reference's built-in key (:19-25).  Arguments
+ * are host-order integers, as addr_pool.c:168,251 pass them for an incoming
+ * packet (source = remote).  ref_rss_core = GetRSSCPUCore: endian_check != 0
+ * is the i40e mapping (9 LSBs + {3,1,-1,-3}[h & 3]), else ixgbe/mlx (7 LSBs),
+ * then % num_queues. */
+extern const uint8_t REF_RSS_DEFAULT_KEY[40];
+void     ref_rss_key_cache(const uint8_t *key, uint32_t cache[96]);
+uint32_t ref_rss_hash(const uint8_t *key, uint32_t sip, uint32_t dip, uint16_t sp,
+                      uint16_t dp);
+int      ref_rss_core(const uint8_t *key, uint32_t sip, uint32_t dip, uint16_t sp,
+                      uint16_t dp, int num_queues, int endian_check);
+
+/* RX verdict + RSS steering of ACCEPT frames: hash/queue of the frame's
+ * (saddr, daddr, source, dest); 0 / 0xFFFF for any other verdict. */
+void ref_classify_batch(uint8_t *buf, uint64_t buf_bytes, const uint64_t *off,
+                        const uint16_t *len, uint32_t n, uint8_t *verdict,
+                        uint32_t *hash, uint16_t *queue, uint32_t flags,
+                        const uint8_t *key, int num_queues, int endian_check);
+void ref_classify_fixed(uint8_t *buf, uint64_t stride, uint32_t frame_len, uint32_t n,
+                        uint8_t *verdict, uint32_t *hash, uint16_t *queue,
+                        uint32_t flags, const uint8_t *key, int num_queues,
+                        int endian_check);
 
 /* Batches over a buffer with per-frame byte offsets and lengths. */
 void ref_verify_batch(uint8_t *buf, uint64_t buf_bytes, const uint64_t *off,
@@ -83,6 +128,9 @@ void ref_verify_batch(uint8_t *buf, uint64_t buf_bytes, const uint64_t *off,
 void ref_compute_batch(uint8_t *buf, uint64_t buf_bytes, const uint64_t *off,
                        const uint16_t *len, uint32_t n, uint8_t *status,
                        uint32_t *csums);
+void ref_compute_batch_f(uint8_t *buf, uint64_t buf_bytes, const uint64_t *off,
+                         const uint16_t *len, uint32_t n, uint8_t *status,
+                         uint32_t *csums, uint32_t flags);
 
 /* Fixed-stride batches (frame i at buf + i*stride, length frame_len). */
 void ref_verify_fixed(uint8_t *buf, uint64_t stride, uint32_t frame_len,
@@ -105,6 +153,8 @@ void ref_tcp_checksum_batch(const uint8_t *buf, const uint64_t *off,
                             const uint32_t *daddr, uint32_t n, uint16_t *out);
 void ref_ip_checksum_batch(const uint8_t *buf, const uint64_t *off,
                            const uint8_t *ihl, uint32_t n, uint16_t *out);
+void ref_icmp_checksum_batch(const uint8_t *buf, const uint64_t *off,
+                             const uint16_t *len, uint32_t n, uint16_t *out);
 
 #ifdef __cplusplus
 }

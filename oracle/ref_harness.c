@@ -7,6 +7,10 @@
  *     place with the reference's flags, mtcp/src/Makefile.in:44,50,63-65), and
  *   - ip_fast_csum, the static inline x86 asm from
  *     /root/reference/io_engine/include/ps.h:66-95 (included, not copied).
+ * Also ICMPChecksum (mtcp/src/icmp.c:18-42) and GetRSSHash (mtcp/src/rss.c:44-86),
+ * both `static` there: oracle/Makefile compiles icmp.c / rss.c in place with
+ * -fkeep-static-functions and makes just those two symbols global with
+ * objcopy (no source is changed or copied), plus GetRSSCPUCore (rss.c:97-115).
  * The RX/TX drivers below follow ip_in.c:21-59 / tcp_in.c:1208-1241 and
  * ip_out.c:143-173 / tcp_out.c:244,323-333, using the same <netinet/*.h>
  * structs the reference uses, so field parsing is checked independently of
@@ -19,6 +23,7 @@
 #include <arpa/inet.h>
 #include <netinet/ip.h>
 #include <netinet/tcp.h>
+#include <netinet/ip_icmp.h>
 #include <linux/if_ether.h>
 
 #include "ps.h"   /* reference: io_engine/include/ps.h (ip_fast_csum) */
@@ -37,8 +42,31 @@ uint16_t refx_ip_fast_csum(const uint8_t *iph, unsigned int ihl)
 	return (uint16_t)ip_fast_csum(iph, ihl);
 }
 
-/* Verdict codes: identical numbering to oracle/csum_ref.h REF_V_*. */
-int refx_rx_verdict(uint8_t *pkt, uint32_t len)
+/* reference: mtcp/src/icmp.c:18-19, rss.c:44-45 (static, globalized), rss.h:7-9 */
+uint16_t ICMPChecksum(uint16_t *icmph, int len);
+uint32_t GetRSSHash(in_addr_t sip, in_addr_t dip, in_port_t sp, in_port_t dp);
+int GetRSSCPUCore(in_addr_t sip, in_addr_t dip, in_port_t sp, in_port_t dp, int num_queues,
+                  uint8_t endian_check);
+
+uint16_t refx_icmp_checksum(const uint8_t *buf, int len)
+{
+	return ICMPChecksum((uint16_t *)buf, len);
+}
+
+uint32_t refx_rss_hash(uint32_t sip, uint32_t dip, uint16_t sp, uint16_t dp)
+{
+	return GetRSSHash(sip, dip, sp, dp);
+}
+
+int refx_rss_core(uint32_t sip, uint32_t dip, uint16_t sp, uint16_t dp, int num_queues,
+                  int endian_check)
+{
+	return GetRSSCPUCore(sip, dip, sp, dp, num_queues, (uint8_t)endian_check);
+}
+
+/* Verdict codes: identical numbering to oracle/csum_ref.h REF_V_*.
+ * flags & 0x2 (REF_VF_ICMP): ICMP frames are classified by ICMPChecksum. */
+int refx_rx_verdict_f(uint8_t *pkt, uint32_t len, uint32_t flags)
 {
 	struct ethhdr *ethh = (struct ethhdr *)pkt;
 	struct iphdr *iph;
@@ -61,6 +89,13 @@ int refx_rx_verdict(uint8_t *pkt, uint32_t len)
 		return 3;
 	if (iph->version != 0x4)                               /* ip_in.c:47 */
 		return 4;
+	if (iph->protocol == IPPROTO_ICMP && (flags & 0x2u)) { /* ip_in.c:56 */
+		int icmp_len = ip_len - (iph->ihl << 2);         /* icmp.c:89 */
+		if (icmp_len >= 0 && 14u + (uint32_t)ip_len > len)
+			return 8;
+		return ICMPChecksum((uint16_t *)((uint8_t *)iph + (iph->ihl << 2)), icmp_len)
+		           ? 11 : 10;
+	}
 	if (iph->protocol != IPPROTO_TCP)                      /* ip_in.c:52-59 */
 		return 5;
 	if (14u + (iph->ihl << 2) + 13u > len)
@@ -77,8 +112,14 @@ int refx_rx_verdict(uint8_t *pkt, uint32_t len)
 	return 0;
 }
 
-/* TX fill (status numbering = REF_TX_*). */
-int refx_tx_fill(uint8_t *pkt, uint32_t len, uint32_t *csums)
+int refx_rx_verdict(uint8_t *pkt, uint32_t len)
+{
+	return refx_rx_verdict_f(pkt, len, 0);
+}
+
+/* TX fill (status numbering = REF_TX_*).  flags & 0x2 (REF_CF_ICMP): ICMP
+ * frames also get the ICMP check, in ICMPOutput's order (icmp.c:57-69). */
+int refx_tx_fill_f(uint8_t *pkt, uint32_t len, uint32_t *csums, uint32_t flags)
 {
 	struct ethhdr *ethh = (struct ethhdr *)pkt;
 	struct iphdr *iph;
@@ -99,6 +140,17 @@ int refx_tx_fill(uint8_t *pkt, uint32_t len, uint32_t *csums)
 	iph->check = ip_fast_csum(iph, iph->ihl);              /* ip_out.c:172 */
 	if (csums)
 		*csums = iph->check;
+	if (iph->protocol == IPPROTO_ICMP && (flags & 0x2u)) {
+		struct icmphdr *icmph = (struct icmphdr *)((uint8_t *)iph + (iph->ihl << 2));
+		if (ip_len < (int)(iph->ihl << 2) + 8 || 14u + (uint32_t)ip_len > len)
+			return 6;
+		icmph->checksum = 0;                               /* icmp.c:60 */
+		icmph->checksum = ICMPChecksum((uint16_t *)icmph,
+		                               ip_len - (iph->ihl << 2)); /* icmp.c:68-69 */
+		if (csums)
+			*csums = (uint32_t)iph->check | ((uint32_t)icmph->checksum << 16);
+		return 5;
+	}
 	if (iph->protocol != IPPROTO_TCP)
 		return 1;
 	if (ip_len < (int)(iph->ihl << 2) + 20 || 14u + (uint32_t)ip_len > len)
@@ -110,6 +162,11 @@ int refx_tx_fill(uint8_t *pkt, uint32_t len, uint32_t *csums)
 	if (csums)
 		*csums = (uint32_t)iph->check | ((uint32_t)tcph->check << 16);
 	return 0;
+}
+
+int refx_tx_fill(uint8_t *pkt, uint32_t len, uint32_t *csums)
+{
+	return refx_tx_fill_f(pkt, len, csums, 0);
 }
 
 void refx_verify_fixed(uint8_t *buf, uint64_t stride, uint32_t frame_len,

@@ -17,6 +17,15 @@ plain data (.npz without pickles, .json):
 * ip_fn.npz       element-wise ip_fast_csum vectors (ihl 0..15, carry edges)
 * frames_rx.npz   packed frames -> RX verdicts (every verdict path)
 * frames_tx.npz   packed frames (garbage checks) -> TX status + check values
+* icmp_fn.npz     element-wise ICMPChecksum vectors (mtcp/src/icmp.c:18-42),
+                  odd lengths with junk after the last byte
+* rss.npz         GetRSSHash / GetRSSCPUCore (mtcp/src/rss.c:44-115) over
+                  random and edge 4-tuples, 13 queue counts x both mappings
+* frames_l4.npz   ICMP + TCP frames -> RX verdicts with the ICMP flag, TX
+                  fill with the ICMP flag, RSS hash/core of ACCEPT frames
+
+``python tests/golden/gen_golden.py [name ...]`` regenerates only the named
+files (default: all).
 """
 from __future__ import annotations
 
@@ -255,15 +264,187 @@ def gen_frames_tx(R: RefHarness):
                                             dtype=np.uint8))
 
 
+def gen_icmp_fn(R: RefHarness):
+    rng = np.random.default_rng(SEED + 5)
+    lens = list(range(0, 600)) + list(range(600, 1481, 11)) + [1472, 1473, 1480, 4095, 65535]
+    n = len(lens)
+    lens = np.array(lens, dtype=np.uint32)
+    starts = rng.integers(0, 8, size=n) * 2
+    slots = (starts + lens + 2 + 15) // 16 * 16 + 16
+    off = np.zeros(n, dtype=np.uint64)
+    np.cumsum(slots[:-1], out=off[1:])
+    buf = rng.integers(0, 256, size=int(off[-1] + slots[-1]) + 64, dtype=np.uint8)
+    for i in np.nonzero(lens >= 4095)[0]:
+        buf[int(off[i]) + int(starts[i]): int(off[i]) + int(starts[i]) + int(lens[i])] = 0xFF
+    item_off = off + starts.astype(np.uint64)
+    expect = np.array([R.icmp_checksum_at(buf, int(item_off[i]), int(lens[i])) for i in range(n)],
+                      dtype=np.uint16)
+    return dict(buf=buf, off=item_off, len=lens.astype(np.uint16), expect=expect)
+
+
+RSS_NQ = np.array([1, 2, 3, 4, 5, 6, 7, 8, 12, 16, 32, 64, 100], dtype=np.int32)
+
+
+def gen_rss(R: RefHarness):
+    rng = np.random.default_rng(SEED + 6)
+    n = 1024
+    sip = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+    dip = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+    sp = rng.integers(0, 1 << 16, size=n).astype(np.uint16)
+    dp = rng.integers(0, 1 << 16, size=n).astype(np.uint16)
+    # edges: all-zero, all-ones, and each single input bit
+    sip[0], dip[0], sp[0], dp[0] = 0, 0, 0, 0
+    sip[1], dip[1], sp[1], dp[1] = 0xFFFFFFFF, 0xFFFFFFFF, 0xFFFF, 0xFFFF
+    for b in range(96):
+        k = 2 + b
+        sip[k] = dip[k] = sp[k] = dp[k] = 0
+        if b < 32:
+            sip[k] = 1 << (31 - b)
+        elif b < 64:
+            dip[k] = 1 << (63 - b)
+        elif b < 80:
+            sp[k] = 1 << (79 - b)
+        else:
+            dp[k] = 1 << (95 - b)
+    h = np.array([R.rss_hash(int(sip[i]), int(dip[i]), int(sp[i]), int(dp[i])) for i in range(n)],
+                 dtype=np.uint32)
+    core = np.zeros((len(RSS_NQ), 2, n), dtype=np.int32)
+    for a, nq in enumerate(RSS_NQ):
+        for e in (0, 1):
+            core[a, e] = [R.rss_core(int(sip[i]), int(dip[i]), int(sp[i]), int(dp[i]), int(nq), e)
+                          for i in range(n)]
+    return dict(sip=sip, dip=dip, sp=sp, dp=dp, hash=h, nq=RSS_NQ, core=core)
+
+
+def _l4_frame_set(R: RefHarness, rng: np.random.Generator):
+    frames = []
+
+    def icmp_frame(payload, ihl=5, typ=8, fill=True):
+        L = 14 + 4 * ihl + 8 + payload
+        f = rng.integers(0, 256, size=L + 4, dtype=np.uint8)
+        f[12], f[13] = 0x08, 0x00
+        f[14] = 0x40 | ihl
+        tot = L - 14
+        f[16], f[17] = tot >> 8, tot & 0xFF
+        f[20], f[21], f[22], f[23] = 0x40, 0, 64, 1
+        ts = 14 + 4 * ihl
+        f[ts], f[ts + 1] = typ, 0
+        if fill:
+            st, _ = R.tx_fill_f_at(f, 0, L, 0x2)
+            assert st == 5, st
+        return f, L
+
+    def tcp_frame(payload, ihl=5, doff=8):
+        L = 14 + 4 * ihl + 4 * doff + payload
+        f = rng.integers(0, 256, size=L + 4, dtype=np.uint8)
+        f[12], f[13] = 0x08, 0x00
+        f[14] = 0x40 | ihl
+        tot = L - 14
+        f[16], f[17] = tot >> 8, tot & 0xFF
+        f[20], f[21], f[22], f[23] = 0x40, 0, 64, 6
+        ts = 14 + 4 * ihl
+        f[ts + 12] = doff << 4
+        st, _ = R.tx_fill_f_at(f, 0, L, 0)
+        assert st == 0
+        return f, L
+
+    def refill_ip(g, ihl=5):
+        g[24] = g[25] = 0
+        c = R.ip_fast_csum_at(g, 14, ihl)
+        g[24], g[25] = c & 0xFF, c >> 8
+
+    for p in list(range(0, 130)) + list(range(130, 1473, 41)) + [1472]:
+        frames.append(icmp_frame(p, typ=(8, 0, 3, 11)[p % 4]))
+    for ihl in range(6, 16):
+        for p in (0, 1, 7, 64, 301):
+            frames.append(icmp_frame(p, ihl=ihl))
+    for p in range(0, 260, 3):                           # TCP: RSS over ACCEPT frames
+        frames.append(tcp_frame(p, ihl=5 + (p % 7 == 0) * (p % 11), doff=5 + (p % 4)))
+    base_valid = len(frames)
+    for k in range(160):                                 # single-byte corruptions
+        f, L = frames[int(rng.integers(0, base_valid))]
+        g = f.copy()
+        pos = int(rng.integers(14, L))
+        g[pos] ^= int(rng.integers(1, 256))
+        frames.append((g, L))
+    f, L = icmp_frame(40)
+    for tot in (20, 23, 24, 27, 28, 29, 35):              # short ICMP messages, valid IP csum
+        for ihl in (5, 6):
+            g = f.copy(); g[14] = 0x40 | ihl
+            g[16], g[17] = tot >> 8, tot & 0xFF
+            refill_ip(g, ihl); frames.append((g, L))
+    for tot in (L - 14 + 1, L - 14 + 64, 65535):          # ICMP message past the frame
+        g = f.copy(); g[16], g[17] = tot >> 8, tot & 0xFF; refill_ip(g); frames.append((g, L))
+    for short in (34, 35, 38, 41):                        # frames cut inside the ICMP header
+        g = f.copy(); tot = short - 14
+        g[16], g[17] = tot >> 8, tot & 0xFF; refill_ip(g); frames.append((g, short))
+    for k in range(20):                                   # checksums landing on 0x0000/0xFFFF
+        frames.append(icmp_frame(int(rng.integers(0, 200))))
+    return frames
+
+
+def gen_frames_l4(R: RefHarness):
+    rng = np.random.default_rng(SEED + 7)
+    frames = _l4_frame_set(R, rng)
+    buf, off, lens = _pack(frames)
+    rx = np.array([R.rx_verdict_f_at(buf, int(o), int(L), 0x2) for o, L in zip(off, lens)],
+                  dtype=np.uint8)
+    rx_noflag = np.array([R.rx_verdict_f_at(buf, int(o), int(L), 0) for o, L in zip(off, lens)],
+                         dtype=np.uint8)
+    # RSS of ACCEPT frames: (saddr, daddr, source, dest) in host order
+    rss_hash = np.zeros(len(off), dtype=np.uint32)
+    rss_core = np.full((2, len(off)), 0xFFFF, dtype=np.int32)
+    for i, (o, L) in enumerate(zip(off, lens)):
+        if rx[i] != 0:
+            continue
+        f = buf[int(o):]
+        ts = 14 + 4 * (int(f[14]) & 15)
+        sip = int.from_bytes(bytes(f[26:30]), "big")
+        dip = int.from_bytes(bytes(f[30:34]), "big")
+        sp = int.from_bytes(bytes(f[ts:ts + 2]), "big")
+        dp = int.from_bytes(bytes(f[ts + 2:ts + 4]), "big")
+        rss_hash[i] = R.rss_hash(sip, dip, sp, dp)
+        rss_core[0, i] = R.rss_core(sip, dip, sp, dp, 16, 0)
+        rss_core[1, i] = R.rss_core(sip, dip, sp, dp, 6, 1)
+    # TX with the ICMP flag over garbage check fields
+    tx = buf.copy()
+    for o, L in zip(off, lens):
+        o = int(o)
+        if L >= 26:
+            tx[o + 24], tx[o + 25] = rng.integers(0, 256, 2)
+        ts = 14 + 4 * (int(tx[o + 14]) & 15) if L > 14 else 0
+        if L >= ts + 4 and ts:
+            tx[o + ts + 2], tx[o + ts + 3] = rng.integers(0, 256, 2)
+    filled = tx.copy()
+    status = np.zeros(len(off), dtype=np.uint8)
+    csums = np.zeros(len(off), dtype=np.uint32)
+    for i, (o, L) in enumerate(zip(off, lens)):
+        status[i], csums[i] = R.tx_fill_f_at(filled, int(o), int(L), 0x2)
+    return dict(buf=buf, off=off, len=lens, rx=rx, rx_noflag=rx_noflag, rss_hash=rss_hash,
+                rss_core=rss_core, rss_nq=np.array([16, 6], dtype=np.int32),
+                rss_endian=np.array([0, 1], dtype=np.int32), tx=tx, tx_status=status,
+                tx_csums=csums,
+                tx_filled_sha256=np.frombuffer(hashlib.sha256(filled.tobytes()).digest(),
+                                               dtype=np.uint8))
+
+
+GENERATORS = (("tcp_fn", gen_tcp_fn), ("ip_fn", gen_ip_fn), ("frames_rx", gen_frames_rx),
+              ("frames_tx", gen_frames_tx), ("icmp_fn", gen_icmp_fn), ("rss", gen_rss),
+              ("frames_l4", gen_frames_l4))
+
+
 def main() -> None:
     if not RefHarness.available():
         sys.exit("oracle/_ref/libref_mtcp_csum.so missing: run `make -C oracle ref` "
                  "in a container that has /root/reference")
     R = RefHarness()
-    with open(os.path.join(HERE, "kat.json"), "w") as fh:
-        json.dump(gen_kat(R), fh, indent=1, sort_keys=True)
-    for name, fn in (("tcp_fn", gen_tcp_fn), ("ip_fn", gen_ip_fn),
-                     ("frames_rx", gen_frames_rx), ("frames_tx", gen_frames_tx)):
+    only = set(sys.argv[1:])
+    if not only or "kat" in only:
+        with open(os.path.join(HERE, "kat.json"), "w") as fh:
+            json.dump(gen_kat(R), fh, indent=1, sort_keys=True)
+    for name, fn in GENERATORS:
+        if only and name not in only:
+            continue
         d = fn(R)
         np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)
         print(name, {k: (v.shape, str(v.dtype)) for k, v in d.items()})

@@ -65,6 +65,25 @@ class Oracle:
                                              C.c_void_p, C.c_uint32, C.c_void_p]
         L.ref_ip_checksum_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                             C.c_void_p]
+        L.ref_icmp_checksum.restype = C.c_uint16
+        L.ref_icmp_checksum.argtypes = [C.c_void_p, C.c_int]
+        L.ref_icmp_checksum_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                              C.c_void_p]
+        L.ref_tx_fill_f.restype = C.c_int
+        L.ref_tx_fill_f.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]
+        L.ref_compute_batch_f.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
+                                          C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint32]
+        L.ref_rss_hash.restype = C.c_uint32
+        L.ref_rss_hash.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint16, C.c_uint16]
+        L.ref_rss_core.restype = C.c_int
+        L.ref_rss_core.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint16, C.c_uint16,
+                                   C.c_int, C.c_int]
+        L.ref_classify_batch.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
+                                         C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.c_uint32, C.c_void_p, C.c_int, C.c_int]
+        L.ref_classify_fixed.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32,
+                                         C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                         C.c_void_p, C.c_int, C.c_int]
         self.L = L
 
     # -- element functions -------------------------------------------------
@@ -76,7 +95,55 @@ class Oracle:
         b = np.frombuffer(bytes(hdr) + b"\0" * 64, dtype=np.uint8).copy()
         return self.L.ref_ip_fast_csum(_p(b), ihl)
 
+    def icmp_checksum(self, buf: bytes, length: int) -> int:
+        b = np.frombuffer(bytes(buf) + b"\0\0", dtype=np.uint8).copy()
+        return self.L.ref_icmp_checksum(_p(b), length)
+
+    @staticmethod
+    def _key(key):
+        if key is None:
+            return None
+        k = np.frombuffer(bytes(key), dtype=np.uint8).copy()
+        assert k.size >= 16
+        return k
+
+    def rss_hash(self, sip, dip, sp, dp, key=None) -> int:
+        k = self._key(key)
+        return self.L.ref_rss_hash(_p(k), sip, dip, sp, dp)
+
+    def rss_core(self, sip, dip, sp, dp, num_queues, endian_check, key=None) -> int:
+        k = self._key(key)
+        return self.L.ref_rss_core(_p(k), sip, dip, sp, dp, num_queues, endian_check)
+
     # -- batches ----------------------------------------------------------
+    def classify_batch(self, buf, off, lens, num_queues, endian_check, key=None, flags=0):
+        n = len(off)
+        vd = np.zeros(n, dtype=np.uint8)
+        h = np.zeros(n, dtype=np.uint32)
+        q = np.zeros(n, dtype=np.uint16)
+        k = self._key(key)
+        self.L.ref_classify_batch(_p(buf), buf.nbytes, _p(np.ascontiguousarray(off, np.uint64)),
+                                  _p(np.ascontiguousarray(lens, np.uint16)), n, _p(vd), _p(h),
+                                  _p(q), flags, _p(k), num_queues, endian_check)
+        return vd, h, q
+
+    def classify_fixed(self, buf, stride, frame_len, n, num_queues, endian_check, key=None,
+                       flags=0):
+        vd = np.zeros(n, dtype=np.uint8)
+        h = np.zeros(n, dtype=np.uint32)
+        q = np.zeros(n, dtype=np.uint16)
+        k = self._key(key)
+        self.L.ref_classify_fixed(_p(buf), stride, frame_len, n, _p(vd), _p(h), _p(q), flags,
+                                  _p(k), num_queues, endian_check)
+        return vd, h, q
+
+    def icmp_checksum_batch(self, buf, off, lens):
+        n = len(off)
+        out = np.zeros(n, dtype=np.uint16)
+        self.L.ref_icmp_checksum_batch(_p(buf), _p(np.ascontiguousarray(off, np.uint64)),
+                                       _p(np.ascontiguousarray(lens, np.uint16)), n, _p(out))
+        return out
+
     def verify_batch(self, buf, off, lens, flags=0):
         n = len(off)
         out = np.zeros(n, dtype=np.uint8)
@@ -84,12 +151,14 @@ class Oracle:
                                 _p(np.ascontiguousarray(lens, np.uint16)), n, _p(out), flags)
         return out
 
-    def compute_batch(self, buf, off, lens):
+    def compute_batch(self, buf, off, lens, flags=0):
         n = len(off)
         st = np.zeros(n, dtype=np.uint8)
         cs = np.zeros(n, dtype=np.uint32)
-        self.L.ref_compute_batch(_p(buf), buf.nbytes, _p(np.ascontiguousarray(off, np.uint64)),
-                                 _p(np.ascontiguousarray(lens, np.uint16)), n, _p(st), _p(cs))
+        self.L.ref_compute_batch_f(_p(buf), buf.nbytes,
+                                   _p(np.ascontiguousarray(off, np.uint64)),
+                                   _p(np.ascontiguousarray(lens, np.uint16)), n, _p(st), _p(cs),
+                                   flags)
         return st, cs
 
     def verify_fixed(self, buf, stride, frame_len, n, flags=0, threads=1):
@@ -150,7 +219,37 @@ class RefHarness:
                                          C.c_void_p]
         L.refx_run_fixed_mt.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32,
                                         C.c_void_p, C.c_int, C.c_int]
+        L.refx_icmp_checksum.restype = C.c_uint16
+        L.refx_icmp_checksum.argtypes = [C.c_void_p, C.c_int]
+        L.refx_rss_hash.restype = C.c_uint32
+        L.refx_rss_hash.argtypes = [C.c_uint32, C.c_uint32, C.c_uint16, C.c_uint16]
+        L.refx_rss_core.restype = C.c_int
+        L.refx_rss_core.argtypes = [C.c_uint32, C.c_uint32, C.c_uint16, C.c_uint16, C.c_int,
+                                    C.c_int]
+        L.refx_rx_verdict_f.restype = C.c_int
+        L.refx_rx_verdict_f.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+        L.refx_tx_fill_f.restype = C.c_int
+        L.refx_tx_fill_f.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]
         self.L = L
+
+    def icmp_checksum_at(self, buf: np.ndarray, pos: int, length: int) -> int:
+        return self.L.refx_icmp_checksum(C.c_void_p(buf.ctypes.data + pos), length)
+
+    def rss_hash(self, sip: int, dip: int, sp: int, dp: int) -> int:
+        return self.L.refx_rss_hash(sip, dip, sp, dp)
+
+    def rss_core(self, sip: int, dip: int, sp: int, dp: int, num_queues: int,
+                 endian_check: int) -> int:
+        return self.L.refx_rss_core(sip, dip, sp, dp, num_queues, endian_check)
+
+    def rx_verdict_f_at(self, buf: np.ndarray, pos: int, length: int, flags: int) -> int:
+        return self.L.refx_rx_verdict_f(C.c_void_p(buf.ctypes.data + pos), length, flags)
+
+    def tx_fill_f_at(self, buf: np.ndarray, pos: int, length: int,
+                     flags: int) -> tuple[int, int]:
+        cs = C.c_uint32(0)
+        st = self.L.refx_tx_fill_f(C.c_void_p(buf.ctypes.data + pos), length, C.byref(cs), flags)
+        return st, cs.value
 
     def tcp_calc_checksum_at(self, buf: np.ndarray, pos: int, length: int, saddr: int,
                              daddr: int) -> int:

@@ -94,3 +94,58 @@ def test_tx_then_rx_accepts(O):
     v = O.verify_batch(buf, d["off"], d["len"])
     assert not np.isin(v[st == 0], [3, 7]).any()
     assert (v[st == 0] == 0).mean() > 0.95
+
+
+# ---- ICMPChecksum and RSS --------------------------------
+
+def test_icmp_fn_golden(O):
+    """icmp.c:18-42, incl. odd lengths (the reference object zero-extends the
+    uninitialised high byte of odd_byte) and junk after the last byte."""
+    d = load("icmp_fn")
+    got = O.icmp_checksum_batch(d["buf"], d["off"], d["len"])
+    np.testing.assert_array_equal(got, d["expect"])
+    assert (d["len"] % 2 == 1).sum() > 300
+
+
+def test_rss_golden(O):
+    """rss.c:44-115 with the reference's built-in key: hash and core mapping."""
+    d = load("rss")
+    n = len(d["sip"])
+    got = np.array([O.rss_hash(int(d["sip"][i]), int(d["dip"][i]), int(d["sp"][i]),
+                               int(d["dp"][i])) for i in range(n)], dtype=np.uint32)
+    np.testing.assert_array_equal(got, d["hash"])
+    for a, nq in enumerate(d["nq"]):
+        for e in (0, 1):
+            core = [O.rss_core(int(d["sip"][i]), int(d["dip"][i]), int(d["sp"][i]),
+                               int(d["dp"][i]), int(nq), e) for i in range(0, n, 3)]
+            np.testing.assert_array_equal(core, d["core"][a, e, ::3])
+
+
+def test_rss_default_key_is_the_reference_key(O):
+    key = bytes([5] * 40)
+    assert O.rss_hash(0x0A000001, 0x0A000002, 1234, 80, key=key) == \
+        O.rss_hash(0x0A000001, 0x0A000002, 1234, 80)
+
+
+def test_frames_l4_golden(O):
+    d = load("frames_l4")
+    got = O.verify_batch(d["buf"].copy(), d["off"], d["len"], flags=0x2)
+    np.testing.assert_array_equal(got, d["rx"])
+    got = O.verify_batch(d["buf"].copy(), d["off"], d["len"], flags=0)
+    np.testing.assert_array_equal(got, d["rx_noflag"])
+    for k in range(2):
+        vd, h, q = O.classify_batch(d["buf"].copy(), d["off"], d["len"], int(d["rss_nq"][k]),
+                                    int(d["rss_endian"][k]), flags=0x2)
+        np.testing.assert_array_equal(vd, d["rx"])
+        acc = vd == 0
+        np.testing.assert_array_equal(h[acc], d["rss_hash"][acc])
+        np.testing.assert_array_equal(q[acc], d["rss_core"][k][acc])
+        assert (q[~acc] == 0xFFFF).all() and (h[~acc] == 0).all()
+    tx = d["tx"].copy()
+    st, cs = O.compute_batch(tx, d["off"], d["len"], flags=0x2)
+    np.testing.assert_array_equal(st, d["tx_status"])
+    np.testing.assert_array_equal(cs, d["tx_csums"])
+    assert hashlib.sha256(tx.tobytes()).digest() == bytes(d["tx_filled_sha256"])
+    # every verdict / status the ICMP path defines is covered
+    assert {10, 11, 0, 3, 8} <= set(d["rx"].tolist())
+    assert {0, 5, 6} <= set(d["tx_status"].tolist())

@@ -66,3 +66,61 @@ def test_fixed_frames_rx_tx(both, frame_len):
     v2 = R.run_fixed(b1, stride, frame_len, n, compute=False)
     np.testing.assert_array_equal(v1, v2)
     assert (v1[bad] != 0).all() and (np.delete(v1, bad) == 0).all()
+
+
+def test_icmp_checksum_random(both):
+    O, R = both
+    rng = np.random.default_rng(9)
+    n = 3000
+    lens = rng.integers(0, 3000, size=n).astype(np.uint16)
+    off = np.zeros(n, dtype=np.uint64)
+    np.cumsum((lens[:-1].astype(np.uint64) + 18) // 16 * 16, out=off[1:])
+    off += 2 * rng.integers(0, 4, size=n).astype(np.uint64)
+    buf = rng.integers(0, 256, size=int(off[-1]) + 4096, dtype=np.uint8)
+    got = O.icmp_checksum_batch(buf, off, lens)
+    exp = np.array([R.icmp_checksum_at(buf, int(off[i]), int(lens[i])) for i in range(n)],
+                   dtype=np.uint16)
+    np.testing.assert_array_equal(got, exp)
+    # non-positive lengths (ICMPChecksum takes an int)
+    for ln in (-7, -1, 0):
+        assert O.L.ref_icmp_checksum(buf.ctypes.data, ln) == R.icmp_checksum_at(buf, 0, ln)
+
+
+def test_rss_random(both):
+    O, R = both
+    rng = np.random.default_rng(10)
+    for _ in range(3000):
+        sip, dip = (int(x) for x in rng.integers(0, 1 << 32, 2, dtype=np.uint64))
+        sp, dp = (int(x) for x in rng.integers(0, 1 << 16, 2))
+        assert O.rss_hash(sip, dip, sp, dp) == R.rss_hash(sip, dip, sp, dp)
+        nq = int(rng.integers(1, 129))
+        e = int(rng.integers(0, 2))
+        assert O.rss_core(sip, dip, sp, dp, nq, e) == R.rss_core(sip, dip, sp, dp, nq, e)
+
+
+@pytest.mark.parametrize("payload", [0, 1, 2, 57, 1471])
+def test_icmp_frames_rx_tx(both, payload):
+    """ICMP echo frames through both RX/TX drivers with the ICMP flag, before
+    and after seeded corruption."""
+    O, R = both
+    rng = np.random.default_rng(100 + payload)
+    L = 14 + 20 + 8 + payload
+    n = 256
+    stride = (L + 63) // 64 * 64 + 64
+    buf = rng.integers(0, 256, size=n * stride, dtype=np.uint8)
+    for i in range(n):
+        f = buf[i * stride:]
+        f[12], f[13], f[14] = 8, 0, 0x45
+        f[16], f[17] = (L - 14) >> 8, (L - 14) & 0xFF
+        f[23] = 1
+    b1, b2 = buf.copy(), buf.copy()
+    for i in range(n):
+        s1 = O.L.ref_tx_fill_f(b1.ctypes.data + i * stride, L, None, 2)
+        s2, _ = R.tx_fill_f_at(b2, i * stride, L, 2)
+        assert s1 == s2 == 5
+    np.testing.assert_array_equal(b1, b2)
+    for i in range(0, n, 2):
+        b1[i * stride + int(rng.integers(14, L))] ^= int(rng.integers(1, 256))
+    for i in range(n):
+        assert O.L.ref_rx_verdict(b1.ctypes.data + i * stride, L, 2) == \
+            R.rx_verdict_f_at(b1, i * stride, L, 2)
