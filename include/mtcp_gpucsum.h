@@ -16,6 +16,11 @@
  *                         (declared mtcp/src/include/tcp_util.h:41-42), element-wise.
  *   gcs_ip_checksum_dev   ip_fast_csum()      io_engine/include/ps.h:66-95, element-wise,
  *                         x86 semantics incl. the ihl<=4 early exit (:72-73).
+ *   gcs_icmp_checksum_dev ICMPChecksum()      mtcp/src/icmp.c:18-42 (static there), element-wise.
+ *   GCS_VF_ICMP / GCS_CF_ICMP  the ICMP fold of ProcessICMPECHORequest (icmp.c:89) and
+ *                         ICMPOutput (icmp.c:57-69) inside the batched verify / fill.
+ *   gcs_classify*, gcs_rss_dev  RSS steering: GetRSSHash / GetRSSCPUCore
+ *                         (mtcp/src/rss.c:44-115), fused into the RX verify.
  *
  * The io_module_func plugin that sits on top of this ABI (the drop-in under
  * mtcp/src, io_module.h:60-72) is declared in gpucsum_io_module.h.
@@ -49,7 +54,7 @@
 extern "C" {
 #endif
 
-#define GCS_ABI_VERSION 1
+#define GCS_ABI_VERSION 2
 
 /* ---- status codes ---------------------------------------------------- */
 #define GCS_OK        0
@@ -74,11 +79,20 @@ extern "C" {
 #define GCS_V_DROP_TRUNC    8  /* ERROR: the reference would read past the frame (UB
                                   there: tcp_in.c:1231 folds tot_len bytes regardless)  */
 #define GCS_V_BAD_DESC      9  /* ERROR: descriptor misaligned / outside the buffer     */
-#define GCS_V_IS_ERROR(v) ((v) == 2 || (v) == 3 || (v) >= 6)
+#define GCS_V_ICMP_OK      10  /* GCS_VF_ICMP: IPv4 ICMP, ICMPChecksum == 0 (icmp.c:89)  */
+#define GCS_V_ICMP_BADCSUM 11  /* GCS_VF_ICMP: ICMPChecksum != 0 -- mTCP sends no echo
+                                  reply (icmp.c:89-91) but does NOT count an error
+                                  (ProcessICMPPacket returns TRUE, icmp.c:140)          */
+#define GCS_V_IS_ERROR(v) ((v) == 2 || (v) == 3 || ((v) >= 6 && (v) <= 9))
 
 /* verify flags */
 #define GCS_VF_ZERO_BAD_TCP_CHECK 0x1u  /* reproduce tcp_in.c:1237: tcph->check = 0 on
                                            a TCP checksum failure (writes the frame)   */
+#define GCS_VF_ICMP               0x2u  /* give IPv4 ICMP frames (otherwise NOT_TCP) the
+                                           verdict of ICMPChecksum over tot_len - ihl*4
+                                           bytes; a message past the frame is TRUNC;
+                                           tot_len < ihl*4 is BADCSUM (the reference
+                                           folds nothing and gets 0xFFFF)              */
 
 /* ---- TX status: one byte per frame (optional output) ------------------- */
 #define GCS_TX_OK           0  /* iph->check and tcph->check written                   */
@@ -87,10 +101,17 @@ extern "C" {
 #define GCS_TX_BAD_HDR      3  /* ihl < 5 or IP header past the frame: untouched       */
 #define GCS_TX_BAD_TCPLEN   4  /* iph->check written; tot_len < ihl*4+20 or the segment
                                   runs past the frame: TCP untouched                    */
+#define GCS_TX_ICMP_OK      5  /* GCS_CF_ICMP: iph->check and icmph->checksum written   */
+#define GCS_TX_BAD_ICMPLEN  6  /* GCS_CF_ICMP: iph->check written; tot_len < ihl*4+8 or
+                                  the message runs past the frame: ICMP untouched       */
 #define GCS_TX_BAD_DESC     9  /* descriptor misaligned / outside the buffer           */
 
 /* compute flags */
 #define GCS_CF_NO_INPLACE   0x1u  /* do not write the frames; only fill csums[]         */
+#define GCS_CF_ICMP         0x2u  /* also fill the ICMP checksum of IPv4 ICMP frames, as
+                                     ICMPOutput does (icmp.c:57-69: checksum = 0, then
+                                     ICMPChecksum over the whole message); csums[] then
+                                     holds ip | icmp << 16                             */
 
 typedef struct gcs_ctx gcs_ctx;
 
@@ -151,6 +172,43 @@ int gcs_tcp_checksum_dev(gcs_ctx *ctx, const uint8_t *d_buf, uint64_t buf_bytes,
 int gcs_ip_checksum_dev(gcs_ctx *ctx, const uint8_t *d_buf, uint64_t buf_bytes,
                         const uint64_t *d_off, const uint8_t *d_ihl, uint32_t n,
                         uint16_t *d_out, void *stream);
+/*   icmp: out[i] = ICMPChecksum(buf+off[i], len[i]).  An odd final byte is the
+ *   low byte of a word with a zero high byte: the C leaves that high byte
+ *   uninitialised (icmp.c:24,33-34) and the reference's gcc -O3 object
+ *   zero-extends it (movzbl).                                            */
+int gcs_icmp_checksum_dev(gcs_ctx *ctx, const uint8_t *d_buf, uint64_t buf_bytes,
+                          const uint64_t *d_off, const uint16_t *d_len, uint32_t n,
+                          uint16_t *d_out, void *stream);
+
+/* ---- RSS steering (rss.c) ----------------------------------------------
+ * gcs_ctx_set_rss: the Toeplitz key (key_len >= 16; only the first 16 bytes
+ * reach the 96 windows GetRSSHash uses, rss.c:27-40; NULL = the reference's
+ * built-in key of 40 x 0x05, rss.c:19-25), the number of RX queues / mTCP
+ * cores, and GetRSSCPUCore's endian_check (non-zero: the i40e mapping, 9
+ * hash bits + {3,1,-1,-3}[h & 3]; zero: ixgbe / mlx, 7 bits), rss.c:97-115.
+ * Until it is called the context uses NULL key, 1 queue, endian_check 0.
+ *
+ * gcs_classify_*: gcs_verify_* plus, for every ACCEPT frame, the Toeplitz
+ * hash of (saddr, daddr, source, dest) taken as host-order integers -- the
+ * argument order addr_pool.c:168,251 uses for an incoming packet -- and the
+ * queue GetRSSCPUCore maps it to: the mTCP core that owns the flow.  Other
+ * verdicts get hash 0 and queue 0xFFFF.  d_hash / d_queue may be NULL.
+ *
+ * gcs_rss_dev: element-wise GetRSSHash / GetRSSCPUCore over host-order
+ * tuples (d_hash or d_queue may be NULL). */
+int gcs_ctx_set_rss(gcs_ctx *ctx, const uint8_t *key, uint32_t key_len,
+                    uint32_t num_queues, int endian_check);
+int gcs_classify_fixed_dev(gcs_ctx *ctx, uint8_t *d_frames, uint64_t stride,
+                           uint32_t frame_len, uint32_t n, uint8_t *d_verdict,
+                           uint32_t *d_hash, uint16_t *d_queue, uint32_t flags,
+                           void *stream);
+int gcs_classify_dev(gcs_ctx *ctx, uint8_t *d_frames, uint64_t frames_bytes,
+                     const uint64_t *d_off, const uint16_t *d_len, uint32_t n,
+                     uint8_t *d_verdict, uint32_t *d_hash, uint16_t *d_queue,
+                     uint32_t flags, void *stream);
+int gcs_rss_dev(gcs_ctx *ctx, const uint32_t *d_sip, const uint32_t *d_dip,
+                const uint16_t *d_sp, const uint16_t *d_dp, uint32_t n,
+                uint32_t *d_hash, uint16_t *d_queue, void *stream);
 
 /* ---- host-memory batches (synchronous) --------------------------------
  * frames[off[i] .. off[i]+len[i]) in host memory (any alignment).  The
@@ -168,6 +226,15 @@ int gcs_verify_ptrs(gcs_ctx *ctx, uint8_t *const *pkts, const uint16_t *len,
                     uint32_t n, uint8_t *verdict, uint32_t flags);
 int gcs_compute_ptrs(gcs_ctx *ctx, uint8_t *const *pkts, const uint16_t *len,
                      uint32_t n, uint8_t *status, uint32_t *csums);
+
+/* Host-memory RX verify + RSS steering (see gcs_classify_dev); hash or queue
+ * may be NULL, not both.  The host entry points take GCS_VF_ICMP as well. */
+int gcs_classify(gcs_ctx *ctx, uint8_t *frames, const uint64_t *off,
+                 const uint16_t *len, uint32_t n, uint8_t *verdict, uint32_t *hash,
+                 uint16_t *queue, uint32_t flags);
+int gcs_classify_ptrs(gcs_ctx *ctx, uint8_t *const *pkts, const uint16_t *len,
+                      uint32_t n, uint8_t *verdict, uint32_t *hash, uint16_t *queue,
+                      uint32_t flags);
 
 #ifdef __cplusplus
 }

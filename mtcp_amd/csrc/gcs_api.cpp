@@ -58,6 +58,10 @@ struct Slot {
     uint8_t* d_code = nullptr;
     uint32_t* h_csum = nullptr;
     uint32_t* d_csum = nullptr;
+    uint32_t* h_hash = nullptr;    // RSS outputs (gcs_classify*)
+    uint32_t* d_hash = nullptr;
+    uint16_t* h_queue = nullptr;
+    uint16_t* d_queue = nullptr;
     // bookkeeping of the chunk in flight
     bool busy = false;
     uint32_t first = 0, count = 0;
@@ -169,6 +173,9 @@ class GatherPool {
 struct gcs_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    // RSS steering (gcs_ctx_set_rss), see set_rss_params
+    uint32_t rss_key[4] = {0x05050505u, 0x05050505u, 0x05050505u, 0x05050505u};
+    uint32_t rss_nq = 1, rss_magic = 0, rss_endian = 0;
     uint32_t max_frames = 0;   // per slot
     uint64_t max_bytes = 0;    // per slot
     Slot slot[kSlots];
@@ -220,6 +227,10 @@ void free_slot(Slot& s)
     if (s.h_len) (void)hipHostFree(s.h_len);
     if (s.h_code) (void)hipHostFree(s.h_code);
     if (s.h_csum) (void)hipHostFree(s.h_csum);
+    if (s.h_hash) (void)hipHostFree(s.h_hash);
+    if (s.h_queue) (void)hipHostFree(s.h_queue);
+    if (s.d_hash) (void)hipFree(s.d_hash);
+    if (s.d_queue) (void)hipFree(s.d_queue);
     if (s.d_frames) (void)hipFree(s.d_frames);
     if (s.d_off) (void)hipFree(s.d_off);
     if (s.d_len) (void)hipFree(s.d_len);
@@ -244,7 +255,35 @@ int alloc_slot(Slot& s, uint32_t frames, uint64_t bytes)
     HIP_TRY(hipMalloc((void**)&s.d_len, frames * sizeof(uint16_t)));
     HIP_TRY(hipMalloc((void**)&s.d_code, frames));
     HIP_TRY(hipMalloc((void**)&s.d_csum, frames * sizeof(uint32_t)));
+    HIP_TRY(hipHostMalloc((void**)&s.h_hash, frames * sizeof(uint32_t), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&s.h_queue, frames * sizeof(uint16_t), hipHostMallocDefault));
+    HIP_TRY(hipMalloc((void**)&s.d_hash, frames * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc((void**)&s.d_queue, frames * sizeof(uint16_t)));
     return GCS_OK;
+}
+
+// The reference's built-in RSS key (rss.c:19-25).
+constexpr uint8_t kDefaultRssKey[40] = {5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5,
+                                        5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5,
+                                        5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5};
+
+// RSS parameters as the kernels take them: key bits 0..127 as big-endian
+// words (GetRSSHash only reaches key bit 127, rss.c:27-40) and the queue
+// count with its division magic.
+void set_rss_params(gcs_ctx* ctx, const uint8_t* key, uint32_t nq, uint32_t endian)
+{
+    for (int w = 0; w < 4; w++)
+        ctx->rss_key[w] = ((uint32_t)key[4 * w] << 24) | ((uint32_t)key[4 * w + 1] << 16) |
+                          ((uint32_t)key[4 * w + 2] << 8) | key[4 * w + 3];
+    ctx->rss_nq = nq;
+    ctx->rss_magic = nq > 1 ? (uint32_t)(((1ull << 32) + nq - 1) / nq) : 0u;
+    ctx->rss_endian = endian;
+}
+
+gcs::Ext rss_ext(const gcs_ctx* ctx, uint32_t* hash, uint16_t* queue)
+{
+    return gcs::Ext{{ctx->rss_key[0], ctx->rss_key[1], ctx->rss_key[2], ctx->rss_key[3]}, hash,
+                    queue, ctx->rss_nq, ctx->rss_magic, ctx->rss_endian};
 }
 
 // Write back the check fields the device computed for one TX frame.
@@ -294,8 +333,10 @@ bool is_pinned(const void* p, uint64_t bytes)
 //                gather threads when the chunk is large.
 int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* const* ptrs,
                    const uint16_t* len, uint32_t n, uint8_t* code, uint32_t* csums,
-                   uint32_t flags, bool compute)
+                   uint32_t flags, bool compute, uint32_t* hash = nullptr,
+                   uint16_t* queue = nullptr)
 {
+    const bool classify = !compute && (hash || queue);
     if (!ctx || !len || (!base && !ptrs) || (base && !off))
         return GCS_EINVAL;
     if (!compute && !code)
@@ -325,6 +366,10 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
         s.busy = false;
         if (!compute) {
             std::memcpy(code + s.first, s.h_code, s.count);
+            if (hash)
+                std::memcpy(hash + s.first, s.h_hash, s.count * sizeof(uint32_t));
+            if (queue)
+                std::memcpy(queue + s.first, s.h_queue, s.count * sizeof(uint16_t));
             return GCS_OK;
         }
         const uint32_t first = s.first;
@@ -403,10 +448,20 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
                                              s.d_csum, GCS_CF_NO_INPLACE, s.stream));
             HIP_TRY(hipMemcpyAsync(s.h_csum, s.d_csum, cnt * sizeof(uint32_t),
                                    hipMemcpyDeviceToHost, s.stream));
+        } else if (classify) {
+            HIP_TRY(gcs::launch_classify_desc(s.d_frames, used, s.d_off, s.d_len, cnt, s.d_code,
+                                              flags & GCS_VF_ICMP,
+                                              rss_ext(ctx, s.d_hash, s.d_queue), s.stream));
+            if (hash)
+                HIP_TRY(hipMemcpyAsync(s.h_hash, s.d_hash, cnt * sizeof(uint32_t),
+                                       hipMemcpyDeviceToHost, s.stream));
+            if (queue)
+                HIP_TRY(hipMemcpyAsync(s.h_queue, s.d_queue, cnt * sizeof(uint16_t),
+                                       hipMemcpyDeviceToHost, s.stream));
         } else {
             // the tcp_in.c:1237 side effect is applied on the host copy below
             HIP_TRY(gcs::launch_verify_desc(s.d_frames, used, s.d_off, s.d_len, cnt, s.d_code,
-                                            0u, s.stream));
+                                            flags & GCS_VF_ICMP, s.stream));
         }
         HIP_TRY(hipMemcpyAsync(s.h_code, s.d_code, cnt, hipMemcpyDeviceToHost, s.stream));
         HIP_TRY(hipEventRecord(s.done, s.stream));
@@ -487,6 +542,7 @@ int gcs_ctx_create(gcs_ctx** out, int device, uint32_t max_frames, uint64_t max_
         delete ctx;
         return hip_fail(e, "hipStreamCreateWithFlags");
     }
+    set_rss_params(ctx, kDefaultRssKey, 1, 0);
     if (max_frames && max_bytes) {
         // split the requested staging between the two slots
         ctx->max_frames = std::max<uint32_t>(1, max_frames / kSlots + 1);
@@ -518,6 +574,7 @@ int gcs_ctx_destroy(gcs_ctx* ctx)
             (void)hipStreamSynchronize(ctx->stream);
             (void)hipStreamDestroy(ctx->stream);
         }
+
     }
     delete ctx;
     return GCS_OK;
@@ -678,6 +735,96 @@ int gcs_ip_checksum_dev(gcs_ctx* ctx, const uint8_t* d_buf, uint64_t buf_bytes,
     DeviceGuard g(ctx->device);
     HIP_TRY(gcs::launch_ip_fn(d_buf, buf_bytes, d_off, d_ihl, n, d_out, pick_stream(ctx, stream)));
     return GCS_OK;
+}
+
+int gcs_icmp_checksum_dev(gcs_ctx* ctx, const uint8_t* d_buf, uint64_t buf_bytes,
+                          const uint64_t* d_off, const uint16_t* d_len, uint32_t n,
+                          uint16_t* d_out, void* stream)
+{
+    if (!ctx || (n && (!d_buf || !d_off || !d_len || !d_out)))
+        return GCS_EINVAL;
+    if (n == 0)
+        return GCS_OK;
+    DeviceGuard g(ctx->device);
+    HIP_TRY(gcs::launch_icmp_fn(d_buf, buf_bytes, d_off, d_len, n, d_out,
+                                pick_stream(ctx, stream)));
+    return GCS_OK;
+}
+
+int gcs_ctx_set_rss(gcs_ctx* ctx, const uint8_t* key, uint32_t key_len, uint32_t num_queues,
+                    int endian_check)
+{
+    if (!ctx || num_queues == 0 || num_queues > 0xFFFFu || (key && key_len < 16))
+        return GCS_EINVAL;
+    uint8_t k[40];
+    std::memcpy(k, kDefaultRssKey, sizeof k);
+    if (key)
+        std::memcpy(k, key, std::min<uint32_t>(key_len, sizeof k));
+    // the parameters travel by value in each launch: no device state to fence
+    set_rss_params(ctx, k, num_queues, endian_check ? 1u : 0u);
+    return GCS_OK;
+}
+
+int gcs_classify_fixed_dev(gcs_ctx* ctx, uint8_t* d_frames, uint64_t stride, uint32_t frame_len,
+                           uint32_t n, uint8_t* d_verdict, uint32_t* d_hash, uint16_t* d_queue,
+                           uint32_t flags, void* stream)
+{
+    if (!ctx || (n && (!d_frames || !d_verdict)) || stride % 16 || stride == 0 ||
+        (frame_len + 15u) / 16u * 16u > stride)
+        return GCS_EINVAL;
+    if (n == 0)
+        return GCS_OK;
+    DeviceGuard g(ctx->device);
+    HIP_TRY(gcs::launch_classify_fixed(d_frames, stride, frame_len, n, d_verdict, flags,
+                                       rss_ext(ctx, d_hash, d_queue), pick_stream(ctx, stream)));
+    return GCS_OK;
+}
+
+int gcs_classify_dev(gcs_ctx* ctx, uint8_t* d_frames, uint64_t frames_bytes,
+                     const uint64_t* d_off, const uint16_t* d_len, uint32_t n,
+                     uint8_t* d_verdict, uint32_t* d_hash, uint16_t* d_queue, uint32_t flags,
+                     void* stream)
+{
+    if (!ctx || (n && (!d_frames || !d_off || !d_len || !d_verdict)))
+        return GCS_EINVAL;
+    if (n == 0)
+        return GCS_OK;
+    DeviceGuard g(ctx->device);
+    HIP_TRY(gcs::launch_classify_desc(d_frames, frames_bytes, d_off, d_len, n, d_verdict, flags,
+                                      rss_ext(ctx, d_hash, d_queue), pick_stream(ctx, stream)));
+    return GCS_OK;
+}
+
+int gcs_rss_dev(gcs_ctx* ctx, const uint32_t* d_sip, const uint32_t* d_dip, const uint16_t* d_sp,
+                const uint16_t* d_dp, uint32_t n, uint32_t* d_hash, uint16_t* d_queue,
+                void* stream)
+{
+    if (!ctx || (n && (!d_sip || !d_dip || !d_sp || !d_dp || (!d_hash && !d_queue))))
+        return GCS_EINVAL;
+    if (n == 0)
+        return GCS_OK;
+    DeviceGuard g(ctx->device);
+    HIP_TRY(gcs::launch_rss_fn(d_sip, d_dip, d_sp, d_dp, n, rss_ext(ctx, d_hash, d_queue),
+                               pick_stream(ctx, stream)));
+    return GCS_OK;
+}
+
+int gcs_classify(gcs_ctx* ctx, uint8_t* frames, const uint64_t* off, const uint16_t* len,
+                 uint32_t n, uint8_t* verdict, uint32_t* hash, uint16_t* queue, uint32_t flags)
+{
+    if (!hash && !queue)
+        return GCS_EINVAL;
+    return run_host_batch(ctx, frames, off, nullptr, len, n, verdict, nullptr, flags, false,
+                          hash, queue);
+}
+
+int gcs_classify_ptrs(gcs_ctx* ctx, uint8_t* const* pkts, const uint16_t* len, uint32_t n,
+                      uint8_t* verdict, uint32_t* hash, uint16_t* queue, uint32_t flags)
+{
+    if (!hash && !queue)
+        return GCS_EINVAL;
+    return run_host_batch(ctx, nullptr, nullptr, pkts, len, n, verdict, nullptr, flags, false,
+                          hash, queue);
 }
 
 int gcs_verify(gcs_ctx* ctx, uint8_t* frames, const uint64_t* off, const uint16_t* len,

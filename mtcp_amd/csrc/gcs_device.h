@@ -286,6 +286,11 @@ __device__ __forceinline__ void accum_fast5(uint4 v, int c, int te, const Mask5&
 {
     const int cb = 16 * c;
     u32 t0 = HDR ? m.tcp[0] : 0xFFFFFFFFu, t1 = HDR ? m.tcp[1] : 0xFFFFFFFFu;
+    // COMPUTE leaves out tcph->check only when the whole word lies in the
+    // segment (te >= 52), exactly as accum_chunk does; the ICMP fill
+    // (epilogue) relies on the two paths agreeing for short messages.
+    if (COMPUTE && HDR && c == 3 && te < 52)
+        t0 = 0xFFFFFFFFu;
     u32 t2 = HDR ? m.tcp[2] : 0xFFFFFFFFu, t3 = HDR ? m.tcp[3] : 0xFFFFFFFFu;
     if (HDR) {
         a.ip = sad(v.x & m.ip[0], a.ip);
@@ -307,8 +312,133 @@ __device__ __forceinline__ void accum_fast5(uint4 v, int c, int te, const Mask5&
     a.tcp = sad(v.w & t3, a.tcp);
 }
 
-// Verdict for one frame, in the reference's order.
-__device__ __forceinline__ u32 rx_verdict(const Hdr& h, const Acc& a, u32 len, bool desc_ok)
+// ---------------------------------------------------------------------------
+// Extensions: the ICMP fold and RSS steering.
+
+// Per-frame extension outputs; pointers already offset to this frame.
+struct XFrame {
+    u32 key[4];                // RSS key bits 0..127, big-endian words (rss.c:19-40)
+    uint32_t* hash;            // this frame's RSS outputs (nullable)
+    uint16_t* queue;
+    u32 nq, nq_magic, endian;  // GetRSSCPUCore mapping; nq_magic = ceil(2^32 / nq)
+    const u32* nib;            // one-lane groups: LDS nibble tables (rss_nibble_tables)
+};
+
+// The 16-bit word at frame byte b (b even) if this lane loaded it, else 0.
+// Every word of the first G*U chunks is held by exactly one lane of the
+// group, so a group_sum of the results is that word.
+template <int G, int U>
+__device__ __forceinline__ u32 held_hw(const uint4 (&v)[U], int sub, int b)
+{
+    const int c = b >> 4;
+    u32 d = 0;
+#pragma unroll
+    for (int j = 0; j < U; j++)
+        d = (c == j * G + sub) ? pick(v[j], (b >> 2) & 3) : d;
+    return (b & 2) ? (d >> 16) : (d & 0xFFFFu);
+}
+
+template <int G>
+__device__ __forceinline__ u32 group_xor(u32 x)
+{
+    if constexpr (G >= 2)
+        x ^= (u32)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
+    if constexpr (G >= 4)
+        x ^= (u32)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);
+    if constexpr (G >= 8)
+        x ^= (u32)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);
+    if constexpr (G >= 16)
+        x ^= (u32)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, false);
+    if constexpr (G >= 32)
+        x ^= (u32)__builtin_amdgcn_ds_swizzle((int)x, 0x401F);
+    if constexpr (G >= 64)
+        x ^= __shfl_xor(x, 32, 64);
+    return x;
+}
+
+// The 32 key bits starting at bit i (BuildKeyCache's cache[i], rss.c:27-40):
+// a funnel shift of two key words (v_alignbit).
+__device__ __forceinline__ u32 key_window(const u32 (&K)[4], int i)
+{
+    const int w = i >> 5, s = i & 31;
+    const u32 hi = w == 0 ? K[0] : (w == 1 ? K[1] : K[2]);
+    const u32 lo = w == 0 ? K[1] : (w == 1 ? K[2] : K[3]);
+    return (u32)((((uint64_t)hi << 32) | lo) >> (32 - s));
+}
+
+constexpr int kNibEntries = 24 * 16;
+
+// For one-lane groups (k_small, k_rss_fn) every lane hashes its own frame, so
+// the 96 bit-steps cannot be spread over idle lanes.  Instead the block
+// builds, in LDS, the table of each input nibble's contribution: nib[p*16+v]
+// = XOR of key windows 4p+t over the set bits t of v (MSB-first); a hash is
+// then 24 LDS lookups.  Built from the key alone (no memory reads); every
+// thread of the block must call this before its first lookup.
+__device__ __forceinline__ void rss_nibble_tables(const u32 (&K)[4], u32* nib)
+{
+    for (int e = threadIdx.x; e < kNibEntries; e += blockDim.x) {
+        const int p = e >> 4, v = e & 15;
+        u32 h = 0;
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+            h ^= ((v >> (3 - t)) & 1) ? key_window(K, 4 * p + t) : 0u;
+        nib[e] = h;
+    }
+    __syncthreads();
+}
+
+// GetRSSHash (rss.c:44-86) of the host-order tuple words T0 = sip, T1 = dip,
+// T2 = sp << 16 | dp (uniform in the group): input bit i (MSB-first) selects
+// key window i.  The 96 bits are split over the group's lanes (lane sub takes
+// i = sub, sub + G, ...) and XOR-reduced on DPP: no memory, a few VALU ops
+// per lane.
+template <int G>
+__device__ __forceinline__ u32 rss_hash(const u32 (&K)[4], u32 T0, u32 T1, u32 T2, int sub,
+                                        const u32* nib = nullptr)
+{
+    if constexpr (G == 1) {
+        u32 h = 0;
+#pragma unroll
+        for (int p = 0; p < 24; p++) {
+            const u32 word = p < 8 ? T0 : (p < 16 ? T1 : T2);
+            h ^= nib[p * 16 + ((word >> (28 - 4 * (p & 7))) & 15u)];
+        }
+        return h;
+    }
+    constexpr int M = (96 + G - 1) / G;
+    u32 h = 0;
+#pragma unroll
+    for (int m = 0; m < M; m++) {
+        const int i = sub + G * m;
+        const u32 word = i < 32 ? T0 : (i < 64 ? T1 : T2);
+        const u32 bit = (word >> (31 - (i & 31))) & 1u;
+        h ^= (bit && i < 96) ? key_window(K, i) : 0u;
+    }
+    return group_xor<G>(h);
+}
+
+// GetRSSCPUCore's mapping (rss.c:97-115) of hash h: i40e (endian) takes 9
+// bits plus {3,1,-1,-3}[m & 3], ixgbe / mlx 7 bits; then % nq, as
+// m - nq * umulhi(m, ceil(2^32 / nq)) (exact: m < 2^10, nq < 2^16).
+__device__ __forceinline__ u32 rss_queue(const XFrame& x, u32 h)
+{
+    u32 m;
+    if (x.endian) {
+        m = h & 0x1FFu;
+        const u32 r = m & 3u;
+        m += r == 0 ? 3u : (r == 1 ? 1u : (r == 2 ? 0xFFFFFFFFu : 0xFFFFFFFDu));
+    } else {
+        m = h & 0x7Fu;
+    }
+    return x.nq == 1 ? 0u : m - x.nq * __umulhi(m, x.nq_magic);
+}
+
+// Verdict for one frame, in the reference's order.  EXT with GCS_VF_ICMP:
+// IPv4 ICMP frames get the verdict of ICMPChecksum (icmp.c:89), whose sum
+// over [ts, te) is `icmp`.
+template <bool EXT = false>
+__device__ __forceinline__ u32 rx_verdict(const Hdr& h, const Acc& a, u32 len, bool desc_ok,
+                                          u32 flags = 0, u32 icmp = 0)
 {
     if (!desc_ok) return GCS_V_BAD_DESC;
     if (len < 14) return GCS_V_DROP_TRUNC;
@@ -323,6 +453,11 @@ __device__ __forceinline__ u32 rx_verdict(const Hdr& h, const Acc& a, u32 len, b
     u32 ipc = ihl <= 4 ? (h.d3 >> 16) : csum16(a.ip);               // ps.h:72-73 quirk
     if (ipc != 0) return GCS_V_DROP_IPCSUM;                          // ip_in.c:35
     if (version != 4) return GCS_V_NOT_V4;                           // ip_in.c:47
+    if (EXT && proto == 1 && (flags & GCS_VF_ICMP)) {                // ip_in.c:56
+        if (tot < 4 * ihl) return GCS_V_ICMP_BADCSUM;                 // folds nothing: 0xFFFF
+        if (14 + tot > len) return GCS_V_DROP_TRUNC;
+        return csum16(icmp) != 0 ? GCS_V_ICMP_BADCSUM : GCS_V_ICMP_OK; // icmp.c:89-91
+    }
     if (proto != 6) return GCS_V_NOT_TCP;                            // ip_in.c:52-59
     u32 ts = 14 + 4 * ihl;
     if (ts + 13 > len) return GCS_V_DROP_TRUNC;
@@ -333,39 +468,86 @@ __device__ __forceinline__ u32 rx_verdict(const Hdr& h, const Acc& a, u32 len, b
     return csum16(s) != 0 ? GCS_V_DROP_TCPCSUM : GCS_V_ACCEPT;        // tcp_in.c:1231-1239
 }
 
+// Replace the low half of dword k of v by `lo16`.
+__device__ __forceinline__ uint4 patch_lo(uint4 v, int k, u32 lo16)
+{
+    const u32 m = 0xFFFF0000u;
+    v.x = k == 0 ? (v.x & m) | lo16 : v.x;
+    v.y = k == 1 ? (v.y & m) | lo16 : v.y;
+    v.z = k == 2 ? (v.z & m) | lo16 : v.z;
+    v.w = k == 3 ? (v.w & m) | lo16 : v.w;
+    return v;
+}
+
 // Group reduction, then the verdict (RX) or the check-field fill (TX).
 // `v` holds this lane's chunks c = j*G + sub of the frame's FIRST U*G chunks
 // (the check fields always lie in chunks 1..5); `active` = false for padding
 // groups, which take part in the cross-lane steps but write nothing.
-template <int G, int U, bool COMPUTE, int WM>
+// EXT adds the ICMP fold (GCS_VF_ICMP / GCS_CF_ICMP) and RSS steering: the
+// tuple words are gathered from the lanes holding them (held_hw).
+template <int G, int U, bool COMPUTE, int WM, bool EXT = false>
 __device__ __forceinline__ void epilogue(const Hdr& h, Acc a, uint8_t* __restrict__ f, u32 len,
                                          bool desc_ok, int sub, u32 flags,
                                          uint8_t* __restrict__ out_code,
                                          uint32_t* __restrict__ out_csum, bool active,
-                                         const uint4 (&v)[U])
+                                         const uint4 (&v)[U], const XFrame& xf = XFrame{})
 {
+    const u32 ihl = (h.d3 >> 16) & 15u;
+    const u32 ts = 14 + 4 * ihl;
+    // EXT: g_sip / g_dip / g_l4 = the wire bytes 26..29, 30..33, ts..ts+3 as
+    // LE dwords (ICMP: type, code, checksum); g_tc = the word at ts+16.
     a.ip = group_sum<G>(a.ip);
     a.tcp = group_sum<G>(a.tcp);
     if (!COMPUTE)
         a.x = group_sum<G>(a.x);
+    u32 g_sip = 0, g_dip = 0, g_l4 = 0, g_tc = 0, rh = 0;
+    if constexpr (EXT) {
+        static_assert(GCS_VF_ICMP == GCS_CF_ICMP, "one ICMP flag bit for RX and TX");
+        // wave-uniform: the tuple is gathered only when RSS is on (kernel-
+        // uniform) or an ICMP frame is in this wave
+        const bool want_rss = !COMPUTE && (xf.hash || xf.queue);
+        const bool want_icmp = (flags & GCS_VF_ICMP) && __any(active && (h.d5 >> 24) == 1u);
+        if (want_rss || want_icmp) {
+            g_sip = held_hw<G, U>(v, sub, 26) | (held_hw<G, U>(v, sub, 28) << 16);
+            g_dip = held_hw<G, U>(v, sub, 30) | (held_hw<G, U>(v, sub, 32) << 16);
+            g_l4 = held_hw<G, U>(v, sub, (int)ts) | (held_hw<G, U>(v, sub, (int)ts + 2) << 16);
+            g_sip = group_sum<G>(g_sip);
+            g_dip = group_sum<G>(g_dip);
+            g_l4 = group_sum<G>(g_l4);
+            if (COMPUTE)
+                g_tc = group_sum<G>(held_hw<G, U>(v, sub, (int)ts + 16));
+        }
+        if (want_rss)
+            rh = rss_hash<G>(xf.key, __builtin_bswap32(g_sip), __builtin_bswap32(g_dip),
+                             __builtin_bswap32(g_l4), sub, xf.nib);
+    }
     if (!active)
         return;
-    const u32 ihl = (h.d3 >> 16) & 15u;
-    const u32 ts = 14 + 4 * ihl;
+    // a.tcp less the pseudo-header address halves: the plain word sum over
+    // [ts, te) that ICMPChecksum folds (no pseudo header, icmp.c:18-42).
+    const u32 l4sum = EXT ? a.tcp - hsum(g_sip) - hsum(g_dip) : 0u;
 
     if (!COMPUTE) {
         if (sub != 0)
             return;
-        u32 vd = rx_verdict(h, a, len, desc_ok);
+        u32 vd = rx_verdict<EXT>(h, a, len, desc_ok, flags, l4sum);
         if (vd == GCS_V_DROP_TCPCSUM && (flags & GCS_VF_ZERO_BAD_TCP_CHECK) && ts + 18u <= len)
             *reinterpret_cast<uint16_t*>(f + ts + 16) = 0;         // tcp_in.c:1237
         out_code[0] = (uint8_t)vd;
+        if constexpr (EXT) {
+            const bool acc = vd == GCS_V_ACCEPT;
+            if (xf.hash)
+                *xf.hash = acc ? rh : 0u;
+            if (xf.queue)
+                *xf.queue = (uint16_t)(acc ? rss_queue(xf, rh) : 0xFFFFu);
+        }
         return;
     }
-    // TX fill: ip_out.c:143-173, tcp_out.c:244, 323-333.  Every lane of the
-    // group evaluates the (uniform) status so that WM_CHUNK / WM_SECTOR can
-    // rewrite whole chunks from the lanes that hold them.
-    u32 st, ipc = 0, tcpc = 0;
+    // TX fill: ip_out.c:143-173, tcp_out.c:244, 323-333; EXT + GCS_CF_ICMP:
+    // icmp.c:57-69.  Every lane of the group evaluates the (uniform) status so
+    // that WM_CHUNK / WM_SECTOR can rewrite whole chunks from the lanes that
+    // hold them.
+    u32 st, ipc = 0, l4c = 0;
     if (!desc_ok) {
         st = GCS_TX_BAD_DESC;
     } else if (len < 14 || (h.d3 & 0xFFFFu) != 0x0008u) {
@@ -374,28 +556,48 @@ __device__ __forceinline__ void epilogue(const Hdr& h, Acc a, uint8_t* __restric
         st = GCS_TX_BAD_HDR;
     } else {
         u32 tot = bswap16(h.d4 & 0xFFFFu);
+        const u32 proto = h.d5 >> 24;
         ipc = csum16(a.ip);
-        if ((h.d5 >> 24) != 6) {
-            st = GCS_TX_IP_ONLY;
-        } else if (tot < 4u * ihl + 20u || 14u + tot > len) {
-            st = GCS_TX_BAD_TCPLEN;
+        if (proto == 6) {
+            if (tot < 4u * ihl + 20u || 14u + tot > len) {
+                st = GCS_TX_BAD_TCPLEN;
+            } else {
+                l4c = csum16(a.tcp + bswap16((tot - 4 * ihl) & 0xFFFFu) + 0x0600u);
+                st = GCS_TX_OK;
+            }
+        } else if (EXT && proto == 1 && (flags & GCS_CF_ICMP)) {
+            if (tot < 4u * ihl + 8u || 14u + tot > len) {
+                st = GCS_TX_BAD_ICMPLEN;
+            } else {
+                // the accumulation left out the word at ts+16 (the TCP check's
+                // place) when it lies in the message: add it back; the ICMP
+                // check itself (ts+2) counts as zero (icmp.c:60)
+                const u32 te = 14u + tot;
+                const u32 s = l4sum + (ts + 18u <= te ? g_tc : 0u) - (g_l4 >> 16);
+                l4c = csum16(s);
+                st = GCS_TX_ICMP_OK;
+            }
         } else {
-            tcpc = csum16(a.tcp + bswap16((tot - 4 * ihl) & 0xFFFFu) + 0x0600u);
-            st = GCS_TX_OK;
+            st = GCS_TX_IP_ONLY;
         }
     }
-    const bool wip = st == GCS_TX_OK || st == GCS_TX_IP_ONLY || st == GCS_TX_BAD_TCPLEN;
+    const bool wip = st == GCS_TX_OK || st == GCS_TX_IP_ONLY || st == GCS_TX_BAD_TCPLEN ||
+                     (EXT && (st == GCS_TX_ICMP_OK || st == GCS_TX_BAD_ICMPLEN));
     const bool wtcp = st == GCS_TX_OK;
+    const bool wicmp = EXT && st == GCS_TX_ICMP_OK;
     if (!(flags & GCS_CF_NO_INPLACE) && wip) {
         if constexpr (WM == WM_HALFWORD) {
             if (sub == 0) {
                 *reinterpret_cast<uint16_t*>(f + 24) = (uint16_t)ipc;
                 if (wtcp)
-                    *reinterpret_cast<uint16_t*>(f + ts + 16) = (uint16_t)tcpc;
+                    *reinterpret_cast<uint16_t*>(f + ts + 16) = (uint16_t)l4c;
+                if (wicmp)
+                    *reinterpret_cast<uint16_t*>(f + ts + 2) = (uint16_t)l4c;
             }
         } else {
             const int nchunks = (int)((len + 15) >> 4);
             const int ctcp = (int)(ts + 16) >> 4;            // chunk holding tcph->check
+            const int cicmp = (int)(ts + 2) >> 4;            // chunk holding icmph->checksum
 #pragma unroll
             for (int j = 0; j < U; j++) {
                 const int c = j * G + sub;
@@ -403,18 +605,22 @@ __device__ __forceinline__ void epilogue(const Hdr& h, Acc a, uint8_t* __restric
                     continue;
                 const bool has_ip = c == 1;
                 const bool has_tcp = wtcp && c == ctcp;
+                const bool has_icmp = wicmp && c == cicmp;
                 const bool take = (WM == WM_CHUNK || WM == WM_CHUNK_SC1)
-                                      ? (has_ip || has_tcp)
+                                      ? (has_ip || has_tcp || has_icmp)
                                       : WM == WM_LINE_SC1
-                                      ? true                       // c < 8: line 0 holds both
-                                      : ((c >> 2) == 0 || (wtcp && (c >> 2) == (ctcp >> 2)));
+                                      ? true                       // c < 8: line 0 holds all
+                                      : ((c >> 2) == 0 || (wtcp && (c >> 2) == (ctcp >> 2)) ||
+                                         (wicmp && (c >> 2) == (cicmp >> 2)));
                 if (!take)
                     continue;
                 uint4 w = v[j];
                 if (has_ip)
                     w.z = (w.z & 0xFFFF0000u) | ipc;                 // bytes 24..25
                 if (has_tcp)
-                    w = patch_hi(w, (int)((ts + 14) >> 2) & 3, tcpc); // bytes ts+16..17
+                    w = patch_hi(w, (int)((ts + 14) >> 2) & 3, l4c); // bytes ts+16..17
+                if (has_icmp)
+                    w = patch_lo(w, (int)((ts + 2) >> 2) & 3, l4c);  // bytes ts+2..3
                 stg16<WM>(f + 16 * c, w);
             }
         }
@@ -423,7 +629,7 @@ __device__ __forceinline__ void epilogue(const Hdr& h, Acc a, uint8_t* __restric
         if (out_code)
             out_code[0] = (uint8_t)st;
         if (out_csum)
-            out_csum[0] = ipc | (tcpc << 16);
+            out_csum[0] = ipc | (l4c << 16);
     }
 }
 
@@ -446,12 +652,13 @@ __device__ __forceinline__ void load_first(const uint8_t* __restrict__ f, int nc
 
 // The frame's first U*G chunks are already in v (load_first); `wf` is where
 // the TX write-back goes (normally f).
-template <int G, int U, bool COMPUTE, bool LOOP, bool SAFE, bool NT, int WM>
+template <int G, int U, bool COMPUTE, bool LOOP, bool SAFE, bool NT, int WM, bool EXT = false>
 __device__ __forceinline__ void frame_body(const uint4 (&v)[U], uint8_t* __restrict__ f,
                                            uint8_t* __restrict__ wf, u32 len, int64_t avail,
                                            bool desc_ok, int sub, u32 flags,
                                            uint8_t* __restrict__ out_code,
-                                           uint32_t* __restrict__ out_csum, bool active)
+                                           uint32_t* __restrict__ out_csum, bool active,
+                                           const XFrame& xf = XFrame{})
 {
     const int nchunks = (desc_ok && active) ? (int)((len + 15) >> 4) : 0;
     // header words: chunk 0 lives in group lane 0, chunk 1 in group lane 1 (j = 0)
@@ -488,21 +695,22 @@ __device__ __forceinline__ void frame_body(const uint4 (&v)[U], uint8_t* __restr
                 accum_chunk<COMPUTE>(w[j], 16 * (base + j * G + sub), ts, te, a);
         }
     }
-    epilogue<G, U, COMPUTE, WM>(h, a, wf, len, desc_ok, sub, flags, out_code, out_csum, active,
-                                v);
+    epilogue<G, U, COMPUTE, WM, EXT>(h, a, wf, len, desc_ok, sub, flags, out_code, out_csum,
+                                     active, v, xf);
 }
 
-template <int G, int U, bool COMPUTE, bool LOOP, bool SAFE, bool NT, int WM>
+template <int G, int U, bool COMPUTE, bool LOOP, bool SAFE, bool NT, int WM, bool EXT = false>
 __device__ __forceinline__ void do_frame(uint8_t* __restrict__ f, u32 len, int64_t avail,
                                          bool desc_ok, int sub, u32 flags,
                                          uint8_t* __restrict__ out_code,
-                                         uint32_t* __restrict__ out_csum, bool active = true)
+                                         uint32_t* __restrict__ out_csum, bool active = true,
+                                         const XFrame& xf = XFrame{})
 {
     const int nchunks = (desc_ok && active) ? (int)((len + 15) >> 4) : 0;
     uint4 v[U];
     load_first<G, U, SAFE, NT>(f, nchunks, avail, sub, v);
-    frame_body<G, U, COMPUTE, LOOP, SAFE, NT, WM>(v, f, f, len, avail, desc_ok, sub, flags,
-                                                  out_code, out_csum, active);
+    frame_body<G, U, COMPUTE, LOOP, SAFE, NT, WM, EXT>(v, f, f, len, avail, desc_ok, sub, flags,
+                                                       out_code, out_csum, active, xf);
 }
 
 }  // namespace gcs

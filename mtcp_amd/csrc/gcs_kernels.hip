@@ -38,10 +38,18 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb)
     return x < r ? x * (q + 1) + k : r * (q + 1) + (x - r) * q + k;
 }
 
-template <int G, int U, bool COMPUTE, bool LOOP, bool NT, int WM, bool XCD = false>
-__global__ void __launch_bounds__(kBlock)
-k_fixed(uint8_t* __restrict__ frames, uint64_t stride, u32 frame_len, u32 n,
-        uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags)
+// The extension outputs of frame i (EXT kernels only).
+__device__ __forceinline__ XFrame xframe(const Ext& x, uint64_t i)
+{
+    return XFrame{{x.key[0], x.key[1], x.key[2], x.key[3]}, x.hash ? x.hash + i : nullptr,
+                  x.queue ? x.queue + i : nullptr, x.nq, x.nq_magic, x.endian, nullptr};
+}
+
+template <int G, int U, bool COMPUTE, bool LOOP, bool NT, int WM, bool XCD, bool EXT>
+__device__ __forceinline__ void fixed_frame(uint8_t* __restrict__ frames, uint64_t stride,
+                                            u32 frame_len, u32 n, uint8_t* __restrict__ out_code,
+                                            uint32_t* __restrict__ out_csum, u32 flags,
+                                            const Ext& ext)
 {
     constexpr int FPB = kBlock / G;                    // frames per block
     const int sub = threadIdx.x & (G - 1);
@@ -49,10 +57,31 @@ k_fixed(uint8_t* __restrict__ frames, uint64_t stride, u32 frame_len, u32 n,
     const uint64_t i = (uint64_t)blk * FPB + threadIdx.x / G;
     if (i >= n)
         return;                                        // whole group leaves together
-    do_frame<G, U, COMPUTE, LOOP, false, NT, WM>(frames + i * stride, frame_len,
-                                                 (int64_t)stride, true, sub, flags,
-                                                 out_code ? out_code + i : nullptr,
-                                                 out_csum ? out_csum + i : nullptr);
+    do_frame<G, U, COMPUTE, LOOP, false, NT, WM, EXT>(frames + i * stride, frame_len,
+                                                      (int64_t)stride, true, sub, flags,
+                                                      out_code ? out_code + i : nullptr,
+                                                      out_csum ? out_csum + i : nullptr, true,
+                                                      EXT ? xframe(ext, i) : XFrame{});
+}
+
+template <int G, int U, bool COMPUTE, bool LOOP, bool NT, int WM, bool XCD = false>
+__global__ void __launch_bounds__(kBlock)
+k_fixed(uint8_t* __restrict__ frames, uint64_t stride, u32 frame_len, u32 n,
+        uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags)
+{
+    fixed_frame<G, U, COMPUTE, LOOP, NT, WM, XCD, false>(frames, stride, frame_len, n, out_code,
+                                                         out_csum, flags, Ext{});
+}
+
+// k_fixed with the extensions (ICMP fold, RSS steering): a separate
+// instantiation so the plain path carries none of their registers.
+template <int G, int U, bool COMPUTE, bool LOOP, bool NT, int WM, bool XCD>
+__global__ void __launch_bounds__(kBlock)
+k_fixed_x(uint8_t* __restrict__ frames, uint64_t stride, u32 frame_len, u32 n,
+          uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags, Ext ext)
+{
+    fixed_frame<G, U, COMPUTE, LOOP, NT, WM, XCD, true>(frames, stride, frame_len, n, out_code,
+                                                        out_csum, flags, ext);
 }
 
 // Small frames (<= 64 B, C1): ONE LANE PER FRAME.  A lane loads its frame's
@@ -61,11 +90,23 @@ k_fixed(uint8_t* __restrict__ frames, uint64_t stride, u32 frame_len, u32 n,
 // verdict bytes of a wave are one coalesced 64 B store.  (The G-lane kernels
 // spend most of their instructions on reductions and a per-group epilogue at
 // this size: tools/kbench.hip)
-template <bool COMPUTE, bool NT, bool XCD>
-__global__ void __launch_bounds__(kBlock)
-k_small(uint8_t* __restrict__ frames, uint64_t stride, u32 frame_len, u32 n,
-        uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags)
+__device__ __forceinline__ XFrame small_xframe(const Ext& x, uint64_t i, const u32* nib)
 {
+    XFrame f = xframe(x, i);
+    f.nib = nib;
+    return f;
+}
+
+template <bool COMPUTE, bool NT, bool XCD, bool EXT>
+__device__ __forceinline__ void small_frame(uint8_t* __restrict__ frames, uint64_t stride,
+                                            u32 frame_len, u32 n, uint8_t* __restrict__ out_code,
+                                            uint32_t* __restrict__ out_csum, u32 flags,
+                                            const Ext& ext)
+{
+    __shared__ u32 nib[EXT ? kNibEntries : 1];
+    const bool rss = EXT && !COMPUTE && (ext.hash || ext.queue);   // kernel-uniform
+    if (rss)
+        rss_nibble_tables(ext.key, nib);
     const uint32_t blk = XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
     const uint64_t i = (uint64_t)blk * kBlock + threadIdx.x;
     if (i >= n)
@@ -91,9 +132,28 @@ k_small(uint8_t* __restrict__ frames, uint64_t stride, u32 frame_len, u32 n,
             accum_chunk<COMPUTE>(v[c], 16 * c, ts, te, a);
     }
     // one-lane "group": epilogue<1, 4> finishes the frame (no reduction steps)
-    epilogue<1, 4, COMPUTE, kWM>(h, a, f, frame_len, true, 0, flags,
-                                 out_code ? out_code + i : nullptr,
-                                 out_csum ? out_csum + i : nullptr, true, v);
+    epilogue<1, 4, COMPUTE, kWM, EXT>(h, a, f, frame_len, true, 0, flags,
+                                      out_code ? out_code + i : nullptr,
+                                      out_csum ? out_csum + i : nullptr, true, v,
+                                      EXT ? small_xframe(ext, i, nib) : XFrame{});
+}
+
+template <bool COMPUTE, bool NT, bool XCD>
+__global__ void __launch_bounds__(kBlock)
+k_small(uint8_t* __restrict__ frames, uint64_t stride, u32 frame_len, u32 n,
+        uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags)
+{
+    small_frame<COMPUTE, NT, XCD, false>(frames, stride, frame_len, n, out_code, out_csum, flags,
+                                         Ext{});
+}
+
+template <bool COMPUTE, bool NT, bool XCD>
+__global__ void __launch_bounds__(kBlock)
+k_small_x(uint8_t* __restrict__ frames, uint64_t stride, u32 frame_len, u32 n,
+          uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags, Ext ext)
+{
+    small_frame<COMPUTE, NT, XCD, true>(frames, stride, frame_len, n, out_code, out_csum, flags,
+                                        ext);
 }
 
 // Descriptor batch: frame i at frames + off[i], length len[i].
@@ -125,12 +185,13 @@ k_desc(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __re
 // lane, then further batches).  Each list is walked by a block-uniform loop
 // so every cross-lane step sees its whole group.  Verdicts / statuses / checks
 // are staged in LDS and leave as one coalesced store per block.
-template <int G, int U, bool COMPUTE, bool LOOP>
+template <int G, int U, bool COMPUTE, bool LOOP, bool EXT>
 __device__ __forceinline__ void desc_class(uint8_t* __restrict__ frames, uint64_t frames_bytes,
                                            const uint64_t* __restrict__ off,
                                            const uint16_t* __restrict__ lens, uint64_t f0,
                                            const uint16_t* list, int count, u32 flags,
-                                           uint8_t* codes, uint32_t* csums)
+                                           uint8_t* codes, uint32_t* csums, const Ext& ext,
+                                           uint32_t* hashes, uint16_t* queues)
 {
     constexpr int GPB = kBlock / G;                    // groups per block
     const int g = threadIdx.x / G, sub = threadIdx.x & (G - 1);
@@ -141,22 +202,32 @@ __device__ __forceinline__ void desc_class(uint8_t* __restrict__ frames, uint64_
         const uint64_t o = off[f0 + t];
         const u32 len = lens[f0 + t];
         uint8_t* f = frames + o;                       // descriptor validated in phase 0
-        do_frame<G, U, COMPUTE, LOOP, true, kNT, kWM>(f, len, (int64_t)(frames_bytes - o), true,
-                                                      sub, flags, codes + t,
-                                                      COMPUTE ? csums + t : nullptr, active);
+        const XFrame xf =
+            EXT ? XFrame{{ext.key[0], ext.key[1], ext.key[2], ext.key[3]},
+                         hashes ? hashes + t : nullptr, queues ? queues + t : nullptr, ext.nq,
+                         ext.nq_magic, ext.endian, nullptr}
+                : XFrame{};
+        do_frame<G, U, COMPUTE, LOOP, true, kNT, kWM, EXT>(f, len, (int64_t)(frames_bytes - o),
+                                                           true, sub, flags, codes + t,
+                                                           COMPUTE ? csums + t : nullptr, active,
+                                                           xf);
     }
 }
 
-template <bool COMPUTE, bool XCD, int OCC = 1>
-__global__ void __launch_bounds__(kBlock, OCC)
-k_desc_mixed(uint8_t* __restrict__ frames, uint64_t frames_bytes,
-             const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens, u32 n,
-             uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags)
+template <bool COMPUTE, bool XCD, int OCC, bool EXT>
+__device__ __forceinline__ void desc_mixed(uint8_t* __restrict__ frames, uint64_t frames_bytes,
+                                           const uint64_t* __restrict__ off,
+                                           const uint16_t* __restrict__ lens, u32 n,
+                                           uint8_t* __restrict__ out_code,
+                                           uint32_t* __restrict__ out_csum, u32 flags,
+                                           const Ext& ext)
 {
     __shared__ uint16_t list[3][kBlock];
     __shared__ int cnt[3];
     __shared__ uint8_t codes[kBlock];
     __shared__ uint32_t csums[COMPUTE ? kBlock : 1];
+    __shared__ uint32_t hashes[EXT && !COMPUTE ? kBlock : 1];
+    __shared__ uint16_t queues[EXT && !COMPUTE ? kBlock : 1];
     const uint32_t blk = XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
     const uint64_t f0 = (uint64_t)blk * kBlock;
     const int t = threadIdx.x;
@@ -173,6 +244,10 @@ k_desc_mixed(uint8_t* __restrict__ frames, uint64_t frames_bytes,
             codes[t] = COMPUTE ? GCS_TX_BAD_DESC : GCS_V_BAD_DESC;
             if (COMPUTE)
                 csums[t] = 0;
+            if (EXT && !COMPUTE) {
+                hashes[t] = 0;
+                queues[t] = 0xFFFF;
+            }
         } else {
             const int c = len <= 64 ? 0 : (len <= 768 ? 1 : 2);
             list[c][atomicAdd(&cnt[c], 1)] = (uint16_t)t;
@@ -180,20 +255,51 @@ k_desc_mixed(uint8_t* __restrict__ frames, uint64_t frames_bytes,
     }
     __syncthreads();
     const int n0 = cnt[0], n1 = cnt[1], n2 = cnt[2];
-    if (n0) desc_class<4, 1, COMPUTE, false>(frames, frames_bytes, off, lens, f0, list[0], n0, flags, codes, csums);
-    if (n1) desc_class<16, 3, COMPUTE, false>(frames, frames_bytes, off, lens, f0, list[1], n1, flags, codes, csums);
-    if (n2) desc_class<32, 3, COMPUTE, true>(frames, frames_bytes, off, lens, f0, list[2], n2, flags, codes, csums);
+    uint32_t* hl = EXT && !COMPUTE ? hashes : nullptr;
+    uint16_t* ql = EXT && !COMPUTE ? queues : nullptr;
+    if (n0) desc_class<4, 1, COMPUTE, false, EXT>(frames, frames_bytes, off, lens, f0, list[0], n0, flags, codes, csums, ext, hl, ql);
+    if (n1) desc_class<16, 3, COMPUTE, false, EXT>(frames, frames_bytes, off, lens, f0, list[1], n1, flags, codes, csums, ext, hl, ql);
+    if (n2) desc_class<32, 3, COMPUTE, true, EXT>(frames, frames_bytes, off, lens, f0, list[2], n2, flags, codes, csums, ext, hl, ql);
     __syncthreads();
     if (i < n) {
         if (out_code)
             out_code[i] = codes[t];
         if (COMPUTE && out_csum)
             out_csum[i] = csums[t];
+        if (EXT && !COMPUTE) {
+            if (ext.hash)
+                ext.hash[i] = hashes[t];
+            if (ext.queue)
+                ext.queue[i] = queues[t];
+        }
     }
 }
 
-// TCPCalcChecksum(buf + off[i], len[i], saddr[i], daddr[i]), G lanes per item.
-template <int G>
+template <bool COMPUTE, bool XCD, int OCC = 1>
+__global__ void __launch_bounds__(kBlock, OCC)
+k_desc_mixed(uint8_t* __restrict__ frames, uint64_t frames_bytes,
+             const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens, u32 n,
+             uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags)
+{
+    desc_mixed<COMPUTE, XCD, OCC, false>(frames, frames_bytes, off, lens, n, out_code, out_csum,
+                                         flags, Ext{});
+}
+
+template <bool COMPUTE, bool XCD, int OCC = 1>
+__global__ void __launch_bounds__(kBlock, OCC)
+k_desc_mixed_x(uint8_t* __restrict__ frames, uint64_t frames_bytes,
+               const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens, u32 n,
+               uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags,
+               Ext ext)
+{
+    desc_mixed<COMPUTE, XCD, OCC, true>(frames, frames_bytes, off, lens, n, out_code, out_csum,
+                                        flags, ext);
+}
+
+// TCPCalcChecksum(buf + off[i], len[i], saddr[i], daddr[i]), G lanes per item;
+// PSEUDO = false: ICMPChecksum(buf + off[i], len[i]) (icmp.c:18-42), the same
+// word loop and odd-byte rule without the pseudo header.
+template <int G, bool PSEUDO = true>
 __global__ void __launch_bounds__(kBlock)
 k_tcp_fn(const uint8_t* __restrict__ buf, uint64_t buf_bytes, const uint64_t* __restrict__ off,
          const uint16_t* __restrict__ lens, const uint32_t* __restrict__ saddr,
@@ -229,10 +335,31 @@ k_tcp_fn(const uint8_t* __restrict__ buf, uint64_t buf_bytes, const uint64_t* __
         out[i] = 0;
         return;
     }
-    const u32 sa = saddr[i], da = daddr[i];
-    s += (sa & 0xFFFFu) + (sa >> 16) + (da & 0xFFFFu) + (da >> 16);   // tcp_util.c:266-267
-    s += bswap16(len) + 0x0600u;                                       // :268-269
+    if (PSEUDO) {
+        const u32 sa = saddr[i], da = daddr[i];
+        s += (sa & 0xFFFFu) + (sa >> 16) + (da & 0xFFFFu) + (da >> 16);   // tcp_util.c:266-267
+        s += bswap16(len) + 0x0600u;                                       // :268-269
+    }
     out[i] = (uint16_t)csum16(s);
+}
+
+// GetRSSHash / GetRSSCPUCore (rss.c:44-115) of host-order tuples, one lane
+// per item (the same hash as the fused path, with a one-lane "group").
+__global__ void __launch_bounds__(kBlock)
+k_rss_fn(const uint32_t* __restrict__ sip, const uint32_t* __restrict__ dip,
+         const uint16_t* __restrict__ sp, const uint16_t* __restrict__ dp, u32 n, Ext ext)
+{
+    __shared__ u32 nib[kNibEntries];
+    rss_nibble_tables(ext.key, nib);
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n)
+        return;
+    const XFrame xf = xframe(ext, i);
+    const u32 h = rss_hash<1>(xf.key, sip[i], dip[i], ((u32)sp[i] << 16) | dp[i], 0, nib);
+    if (xf.hash)
+        *xf.hash = h;
+    if (xf.queue)
+        *xf.queue = (uint16_t)rss_queue(xf, h);
 }
 
 // ip_fast_csum(buf + off[i], ihl[i]), one lane per item (<= 60 bytes each).
@@ -264,21 +391,27 @@ k_ip_fn(const uint8_t* __restrict__ buf, uint64_t buf_bytes, const uint64_t* __r
 // ---------------------------------------------------------------------------
 // launchers (called from gcs_api.cpp)
 
-template <int G, int U, bool COMPUTE, bool LOOP>
+template <int G, int U, bool COMPUTE, bool LOOP, bool EXT>
 static hipError_t launch_fixed(uint8_t* frames, uint64_t stride, u32 frame_len, u32 n,
-                               uint8_t* code, uint32_t* csum, u32 flags, hipStream_t s)
+                               uint8_t* code, uint32_t* csum, u32 flags, const Ext& ext,
+                               hipStream_t s)
 {
     constexpr int FPB = kBlock / G;
     dim3 grid((n + FPB - 1) / FPB);
-    hipLaunchKernelGGL((k_fixed<G, U, COMPUTE, LOOP, kNT, kWM, kXCD>), grid, dim3(kBlock), 0,
-                       s, frames, stride, frame_len, n, code, csum, flags);
+    if (EXT)
+        hipLaunchKernelGGL((k_fixed_x<G, U, COMPUTE, LOOP, kNT, kWM, kXCD>), grid, dim3(kBlock), 0,
+                           s, frames, stride, frame_len, n, code, csum, flags, ext);
+    else
+        hipLaunchKernelGGL((k_fixed<G, U, COMPUTE, LOOP, kNT, kWM, kXCD>), grid, dim3(kBlock), 0,
+                           s, frames, stride, frame_len, n, code, csum, flags);
     return hipGetLastError();
 }
 
 // (G, U) by frame size: G*16 B per load instruction of a group, U loads per lane.
-template <bool COMPUTE>
+template <bool COMPUTE, bool EXT>
 static hipError_t dispatch_fixed(uint8_t* frames, uint64_t stride, u32 frame_len, u32 n,
-                                 uint8_t* code, uint32_t* csum, u32 flags, hipStream_t s)
+                                 uint8_t* code, uint32_t* csum, u32 flags, const Ext& ext,
+                                 hipStream_t s)
 {
     const u32 chunks = (frame_len + 15) / 16;
     if (chunks <= 4) {
@@ -287,51 +420,107 @@ static hipError_t dispatch_fixed(uint8_t* frames, uint64_t stride, u32 frame_len
         // coalesced 1 KiB store per wave, where one lane per frame scatters 64
         // sectors per store instruction (74 us).
         if (COMPUTE)
-            return launch_fixed<4, 1, COMPUTE, false>(frames, stride, frame_len, n, code, csum,
-                                                      flags, s);
-        hipLaunchKernelGGL((k_small<COMPUTE, kNT, kXCD>), dim3((n + kBlock - 1) / kBlock),
-                           dim3(kBlock), 0, s, frames, stride, frame_len, n, code, csum, flags);
+            return launch_fixed<4, 1, COMPUTE, false, EXT>(frames, stride, frame_len, n, code,
+                                                           csum, flags, ext, s);
+        const dim3 grid((n + kBlock - 1) / kBlock);
+        if (EXT)
+            hipLaunchKernelGGL((k_small_x<COMPUTE, kNT, kXCD>), grid, dim3(kBlock), 0, s, frames,
+                               stride, frame_len, n, code, csum, flags, ext);
+        else
+            hipLaunchKernelGGL((k_small<COMPUTE, kNT, kXCD>), grid, dim3(kBlock), 0, s, frames,
+                               stride, frame_len, n, code, csum, flags);
         return hipGetLastError();
     }
-    if (chunks <= 8)   return launch_fixed<8, 1, COMPUTE, false>(frames, stride, frame_len, n, code, csum, flags, s);
-    if (chunks <= 16)  return launch_fixed<16, 1, COMPUTE, false>(frames, stride, frame_len, n, code, csum, flags, s);
-    if (chunks <= 32)  return launch_fixed<32, 1, COMPUTE, false>(frames, stride, frame_len, n, code, csum, flags, s);
-    if (chunks <= 64)  return launch_fixed<32, 2, COMPUTE, false>(frames, stride, frame_len, n, code, csum, flags, s);
-    if (chunks <= 96)  return launch_fixed<32, 3, COMPUTE, false>(frames, stride, frame_len, n, code, csum, flags, s);
-    if (chunks <= 128) return launch_fixed<64, 2, COMPUTE, false>(frames, stride, frame_len, n, code, csum, flags, s);
-    return launch_fixed<64, 4, COMPUTE, true>(frames, stride, frame_len, n, code, csum, flags, s);
+    if (chunks <= 8)   return launch_fixed<8, 1, COMPUTE, false, EXT>(frames, stride, frame_len, n, code, csum, flags, ext, s);
+    if (chunks <= 16)  return launch_fixed<16, 1, COMPUTE, false, EXT>(frames, stride, frame_len, n, code, csum, flags, ext, s);
+    if (chunks <= 32)  return launch_fixed<32, 1, COMPUTE, false, EXT>(frames, stride, frame_len, n, code, csum, flags, ext, s);
+    if (chunks <= 64)  return launch_fixed<32, 2, COMPUTE, false, EXT>(frames, stride, frame_len, n, code, csum, flags, ext, s);
+    if (chunks <= 96)  return launch_fixed<32, 3, COMPUTE, false, EXT>(frames, stride, frame_len, n, code, csum, flags, ext, s);
+    if (chunks <= 128) return launch_fixed<64, 2, COMPUTE, false, EXT>(frames, stride, frame_len, n, code, csum, flags, ext, s);
+    return launch_fixed<64, 4, COMPUTE, true, EXT>(frames, stride, frame_len, n, code, csum, flags, ext, s);
 }
 
 hipError_t launch_verify_fixed(uint8_t* frames, uint64_t stride, u32 frame_len, u32 n,
                                uint8_t* verdict, u32 flags, hipStream_t s)
 {
-    return dispatch_fixed<false>(frames, stride, frame_len, n, verdict, nullptr, flags, s);
+    if (flags & GCS_VF_ICMP)
+        return dispatch_fixed<false, true>(frames, stride, frame_len, n, verdict, nullptr, flags,
+                                           Ext{}, s);
+    return dispatch_fixed<false, false>(frames, stride, frame_len, n, verdict, nullptr, flags,
+                                        Ext{}, s);
 }
 
 hipError_t launch_compute_fixed(uint8_t* frames, uint64_t stride, u32 frame_len, u32 n,
                                 uint8_t* status, uint32_t* csums, u32 flags, hipStream_t s)
 {
-    return dispatch_fixed<true>(frames, stride, frame_len, n, status, csums, flags, s);
+    if (flags & GCS_CF_ICMP)
+        return dispatch_fixed<true, true>(frames, stride, frame_len, n, status, csums, flags,
+                                          Ext{}, s);
+    return dispatch_fixed<true, false>(frames, stride, frame_len, n, status, csums, flags, Ext{},
+                                       s);
 }
 
+hipError_t launch_classify_fixed(uint8_t* frames, uint64_t stride, u32 frame_len, u32 n,
+                                 uint8_t* verdict, u32 flags, const Ext& ext, hipStream_t s)
+{
+    return dispatch_fixed<false, true>(frames, stride, frame_len, n, verdict, nullptr, flags, ext,
+                                       s);
+}
+
+template <bool COMPUTE>
+static hipError_t launch_desc(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
+                              const uint16_t* len, u32 n, uint8_t* code, uint32_t* csums,
+                              u32 flags, bool ext_on, const Ext& ext, hipStream_t s)
+{
+    const dim3 grid((n + kBlock - 1) / kBlock);
+    if (ext_on)
+        hipLaunchKernelGGL((k_desc_mixed_x<COMPUTE, kXCD, kDescOcc>), grid, dim3(kBlock), 0, s,
+                           frames, frames_bytes, off, len, n, code, csums, flags, ext);
+    else
+        hipLaunchKernelGGL((k_desc_mixed<COMPUTE, kXCD, kDescOcc>), grid, dim3(kBlock), 0, s,
+                           frames, frames_bytes, off, len, n, code, csums, flags);
+    return hipGetLastError();
+}
 
 hipError_t launch_verify_desc(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
                               const uint16_t* len, u32 n, uint8_t* verdict, u32 flags,
                               hipStream_t s)
 {
-    hipLaunchKernelGGL((k_desc_mixed<false, kXCD, kDescOcc>), dim3((n + kBlock - 1) / kBlock),
-                       dim3(kBlock), 0, s, frames, frames_bytes, off, len, n, verdict,
-                       (uint32_t*)nullptr, flags);
-    return hipGetLastError();
+    return launch_desc<false>(frames, frames_bytes, off, len, n, verdict, nullptr, flags,
+                              (flags & GCS_VF_ICMP) != 0, Ext{}, s);
 }
 
 hipError_t launch_compute_desc(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
                                const uint16_t* len, u32 n, uint8_t* status, uint32_t* csums,
                                u32 flags, hipStream_t s)
 {
-    hipLaunchKernelGGL((k_desc_mixed<true, kXCD, kDescOcc>), dim3((n + kBlock - 1) / kBlock),
-                       dim3(kBlock), 0, s, frames, frames_bytes, off, len, n, status, csums,
-                       flags);
+    return launch_desc<true>(frames, frames_bytes, off, len, n, status, csums, flags,
+                             (flags & GCS_CF_ICMP) != 0, Ext{}, s);
+}
+
+hipError_t launch_classify_desc(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
+                                const uint16_t* len, u32 n, uint8_t* verdict, u32 flags,
+                                const Ext& ext, hipStream_t s)
+{
+    return launch_desc<false>(frames, frames_bytes, off, len, n, verdict, nullptr, flags, true,
+                              ext, s);
+}
+
+hipError_t launch_icmp_fn(const uint8_t* buf, uint64_t buf_bytes, const uint64_t* off,
+                          const uint16_t* len, u32 n, uint16_t* out, hipStream_t s)
+{
+    constexpr int G = 16, FPB = kBlock / G;
+    hipLaunchKernelGGL((k_tcp_fn<G, false>), dim3((n + FPB - 1) / FPB), dim3(kBlock), 0, s, buf,
+                       buf_bytes, off, len, (const uint32_t*)nullptr, (const uint32_t*)nullptr,
+                       n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_rss_fn(const uint32_t* sip, const uint32_t* dip, const uint16_t* sp,
+                         const uint16_t* dp, u32 n, const Ext& ext, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_rss_fn, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, sip, dip,
+                       sp, dp, n, ext);
     return hipGetLastError();
 }
 

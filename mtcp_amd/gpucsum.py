@@ -76,6 +76,13 @@ def lib() -> C.CDLL:
             "gcs_compute": (i, [vp, vp, vp, vp, u32, vp, vp]),
             "gcs_verify_ptrs": (i, [vp, vp, vp, u32, vp, u32]),
             "gcs_compute_ptrs": (i, [vp, vp, vp, u32, vp, vp]),
+            "gcs_icmp_checksum_dev": (i, [vp, vp, u64, vp, vp, u32, vp, vp]),
+            "gcs_ctx_set_rss": (i, [vp, vp, u32, u32, i]),
+            "gcs_classify_fixed_dev": (i, [vp, vp, u64, u32, u32, vp, vp, vp, u32, vp]),
+            "gcs_classify_dev": (i, [vp, vp, u64, vp, vp, u32, vp, vp, vp, u32, vp]),
+            "gcs_rss_dev": (i, [vp, vp, vp, vp, vp, u32, vp, vp, vp]),
+            "gcs_classify": (i, [vp, vp, vp, vp, u32, vp, vp, vp, u32]),
+            "gcs_classify_ptrs": (i, [vp, vp, vp, u32, vp, vp, vp, u32]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -230,7 +237,62 @@ class Context:
         check(self.L.gcs_ip_checksum_dev(self.h, _daddr(buf), bb, _daddr(off), _daddr(ihl), n,
                                          _daddr(out), stream), "ip_checksum")
 
+    def icmp_checksum(self, buf, off, lens, n, out, stream=None, buf_bytes=None):
+        bb = _nbytes(buf) if buf_bytes is None else buf_bytes
+        self._need(buf, bb, "buf")
+        for a, w in ((off, 8), (lens, 2), (out, 2)):
+            self._need(a, w * n, "array")
+        check(self.L.gcs_icmp_checksum_dev(self.h, _daddr(buf), bb, _daddr(off), _daddr(lens), n,
+                                           _daddr(out), stream), "icmp_checksum")
+
+    # -- RSS steering (rss.c) -------------------------------------------------
+    def set_rss(self, key: bytes | None = None, num_queues: int = 1, endian_check: int = 0):
+        k = None if key is None else np.frombuffer(bytes(key), dtype=np.uint8).copy()
+        check(self.L.gcs_ctx_set_rss(self.h, _addr(k), 0 if k is None else k.size, num_queues,
+                                     endian_check), "gcs_ctx_set_rss")
+
+    def classify_fixed(self, frames, stride, frame_len, n, verdict, hash=None, queue=None,
+                       flags=0, stream=None):
+        self._need(frames, n * stride, "frames")
+        self._need(verdict, n, "verdict")
+        self._need(hash, 4 * n, "hash")
+        self._need(queue, 2 * n, "queue")
+        check(self.L.gcs_classify_fixed_dev(self.h, _daddr(frames), stride, frame_len, n,
+                                            _daddr(verdict), _daddr(hash), _daddr(queue), flags,
+                                            stream), "classify_fixed")
+
+    def classify(self, frames, off, lens, n, verdict, hash=None, queue=None, flags=0,
+                 stream=None, frames_bytes=None):
+        fb = _nbytes(frames) if frames_bytes is None else frames_bytes
+        self._need(frames, fb, "frames")
+        self._need(off, 8 * n, "off")
+        self._need(lens, 2 * n, "lens")
+        self._need(verdict, n, "verdict")
+        self._need(hash, 4 * n, "hash")
+        self._need(queue, 2 * n, "queue")
+        check(self.L.gcs_classify_dev(self.h, _daddr(frames), fb, _daddr(off), _daddr(lens), n,
+                                      _daddr(verdict), _daddr(hash), _daddr(queue), flags,
+                                      stream), "classify")
+
+    def rss(self, sip, dip, sp, dp, n, hash=None, queue=None, stream=None):
+        for a, w in ((sip, 4), (dip, 4), (sp, 2), (dp, 2), (hash, 4), (queue, 2)):
+            self._need(a, w * n, "array")
+        check(self.L.gcs_rss_dev(self.h, _daddr(sip), _daddr(dip), _daddr(sp), _daddr(dp), n,
+                                 _daddr(hash), _daddr(queue), stream), "rss")
+
     # -- host-memory batches (synchronous) ----------------------------------
+    def classify_host(self, frames: np.ndarray, off: np.ndarray, lens: np.ndarray,
+                      flags: int = 0):
+        n = len(off)
+        vd = np.zeros(n, dtype=np.uint8)
+        h = np.zeros(n, dtype=np.uint32)
+        q = np.zeros(n, dtype=np.uint16)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint16)
+        check(self.L.gcs_classify(self.h, _addr(frames), _addr(off), _addr(lens), n, _addr(vd),
+                                  _addr(h), _addr(q), flags), "gcs_classify")
+        return vd, h, q
+
     def verify_host(self, frames: np.ndarray, off: np.ndarray, lens: np.ndarray,
                     flags: int = 0) -> np.ndarray:
         n = len(off)

@@ -168,3 +168,36 @@ def fixed_frames_device(n: int, frame_len: int, stride: int | None = None,
     vals = torch.tensor([fixed[k] for k in sorted(fixed)], dtype=torch.uint8, device=device)
     b[:, cols] = vals
     return buf, stride
+
+
+def icmp_fixed_frames(n: int, frame_len: int, stride: int | None = None,
+                      seed: int = DEFAULT_SEED) -> tuple[np.ndarray, int]:
+    """``n`` ICMP echo-request frames of ``frame_len`` bytes (>= 42: Ethernet
+    + IPv4 + the 8 B icmphdr, icmp.h) at a fixed stride, as ICMPOutput builds
+    them through IPOutputStandalone (ip_out.c:72-101, icmp.c:44-77).  Check
+    fields are 0."""
+    stride = stride or stride_for(frame_len)
+    assert stride >= frame_len and stride % 16 == 0 and frame_len >= 42
+    rng = np.random.default_rng(seed)
+    buf = rng.integers(0, 256, size=n * stride, dtype=np.uint8)
+    b = buf.reshape(n, stride)
+    b[:, 12], b[:, 13], b[:, 14], b[:, 15] = 0x08, 0x00, 0x45, 0
+    tot = frame_len - ETH_LEN
+    b[:, 16], b[:, 17] = (tot >> 8) & 0xFF, tot & 0xFF
+    b[:, 20], b[:, 21], b[:, 22], b[:, 23] = 0x40, 0, 64, 1
+    b[:, 24] = b[:, 25] = 0
+    b[:, 34], b[:, 35] = 8, 0          # ICMP_ECHO, code 0
+    b[:, 36] = b[:, 37] = 0            # icmp_checksum
+    return buf, stride
+
+
+def to_icmp(buf: np.ndarray, off: np.ndarray, lengths: np.ndarray, which: np.ndarray) -> None:
+    """Turn the selected TCP frames (valid headers, any ihl) into ICMP echo
+    requests in place: protocol 1, type 8 / code 0 at the L4 offset.  Frame
+    and IP lengths are kept, so every frame >= 14 + 4*ihl + 8 stays valid."""
+    for i in np.asarray(which):
+        o = int(off[i])
+        ihl = int(buf[o + 14]) & 15
+        ts = o + ETH_LEN + 4 * ihl
+        buf[o + 23] = 1
+        buf[ts], buf[ts + 1] = 8, 0

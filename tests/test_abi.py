@@ -45,7 +45,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_strerror():
     L = gpucsum.lib()
-    assert L.gcs_abi_version() == gpucsum.K["GCS_ABI_VERSION"] == 1
+    assert L.gcs_abi_version() == gpucsum.K["GCS_ABI_VERSION"] == 2
     assert L.gcs_strerror(-1) == b"invalid argument"
     assert L.gcs_strerror(0) == b"ok"
 
@@ -57,6 +57,21 @@ def test_codes_match_oracle():
     for k, v in ref.items():
         assert K["GCS_" + k] == v, k
     assert K["GCS_VF_ZERO_BAD_TCP_CHECK"] == 1
+    assert K["GCS_VF_ICMP"] == 2 and K["GCS_CF_ICMP"] == 2
+    for k in ("V_ICMP_OK", "V_ICMP_BADCSUM", "TX_ICMP_OK", "TX_BAD_ICMPLEN"):
+        assert k in ref
+
+
+def test_error_predicate_excludes_icmp_verdicts():
+    """ICMP checksum failures are not mTCP errors (ProcessICMPPacket returns
+    TRUE, icmp.c:140): the plugin must not drop them."""
+    src = open(os.path.join(ROOT, "include", "mtcp_gpucsum.h")).read()
+    m = re.search(r"#define GCS_V_IS_ERROR\(v\)\s*(.+)", src)
+    pred = eval("lambda v: " + m.group(1).replace("&&", " and ").replace("||", " or "))
+    K = gpucsum.K
+    errs = {K[k] for k in K if k.startswith("GCS_V_") and k != "GCS_V_IS_ERROR" and
+            pred(K[k])}
+    assert errs == {2, 3, 6, 7, 8, 9}
 
 
 def test_argument_validation_without_gpu():
@@ -67,6 +82,11 @@ def test_argument_validation_without_gpu():
     p = C.c_void_p()
     assert L.gcs_ctx_create(None, 0, 0, 0) == gpucsum.K["GCS_EINVAL"]
     assert L.gcs_device_count(None) == gpucsum.K["GCS_EINVAL"]
+    assert L.gcs_ctx_set_rss(None, None, 0, 4, 0) == gpucsum.K["GCS_EINVAL"]
+    assert L.gcs_classify_fixed_dev(None, None, 64, 64, 1, None, None, None, 0, None) == \
+        gpucsum.K["GCS_EINVAL"]
+    assert L.gcs_rss_dev(None, None, None, None, None, 1, None, None, None) == \
+        gpucsum.K["GCS_EINVAL"]
 
 
 def test_no_device_here_is_reported_not_faked():

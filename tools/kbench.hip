@@ -282,6 +282,69 @@ int tx_main(uint64_t n, int rounds)
     return 0;
 }
 
+// Extension overhead: RX verify vs classify (RSS hash +
+// queue outputs) vs verify with the ICMP flag; TX fill vs fill with the ICMP
+// flag.  Frames: TCP, length L, stride per synth.stride_for.
+int ext_main(uint32_t L, uint64_t n, int rounds)
+{
+    const uint64_t stride = L <= 64 ? 64 : (L + 127) / 128 * 128;
+    uint8_t *tx, *rx, *v1;
+    uint32_t *h, *tab, *sink;
+    uint16_t* q;
+    CK(hipMalloc(&tx, n * stride));
+    CK(hipMalloc(&rx, n * stride));
+    CK(hipMalloc(&v1, n));
+    CK(hipMalloc(&h, 4 * n));
+    CK(hipMalloc(&q, 2 * n));
+    CK(hipMalloc(&tab, 12 * 256 * 4));
+    CK(hipMalloc(&sink, 4));
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    hipLaunchKernelGGL(k_init, dim3(4096), dim3(256), 0, s, tx, n, stride, L);
+    hipLaunchKernelGGL(k_hdr, dim3((n + 255) / 256), dim3(256), 0, s, tx, n, stride, L);
+    hipLaunchKernelGGL(k_init, dim3(16), dim3(256), 0, s, (uint8_t*)tab, (uint64_t)192,
+                       (uint64_t)64, 64u);
+    CK(hipMemcpyAsync(rx, tx, n * stride, hipMemcpyDeviceToDevice, s));
+    CK(launch_compute_fixed(rx, stride, L, n, nullptr, nullptr, 0, s));
+    CK(hipStreamSynchronize(s));
+    int dev = 0, cus = 0;
+    CK(hipGetDevice(&dev));
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    std::printf("extensions: frame_len %u stride %llu n %llu\n", L, (unsigned long long)stride,
+                (unsigned long long)n);
+    const double vbytes = (double)n * (L + 1), cbytes = (double)n * (L + 4);
+    const Ext ext{{0x6d5a56dau, 0x255b0ec2u, 0x4167253du, 0x43a38fb0u}, h, q, 16u,
+                  (uint32_t)(((1ull << 32) + 15) / 16), 0u};
+    std::vector<Variant> vs;
+    vs.push_back({"verify   (plain)", vbytes, [&](hipStream_t st) {
+        CK(launch_verify_fixed(rx, stride, L, (u32)n, v1, 0u, st));
+    }});
+    vs.push_back({"verify   + ICMP flag", vbytes, [&](hipStream_t st) {
+        CK(launch_verify_fixed(rx, stride, L, (u32)n, v1, (u32)GCS_VF_ICMP, st));
+    }});
+    vs.push_back({"classify (verify + RSS hash + queue)", vbytes + 6.0 * n, [&](hipStream_t st) {
+        CK(launch_classify_fixed(rx, stride, L, (u32)n, v1, 0u, ext, st));
+    }});
+    vs.push_back({"compute  (plain)", cbytes, [&](hipStream_t st) {
+        CK(launch_compute_fixed(tx, stride, L, (u32)n, nullptr, nullptr, 0u, st));
+    }});
+    vs.push_back({"compute  + ICMP flag", cbytes, [&](hipStream_t st) {
+        CK(launch_compute_fixed(tx, stride, L, (u32)n, nullptr, nullptr, (u32)GCS_CF_ICMP, st));
+    }});
+    vs.push_back({"read-ceiling uint4 NT (whole batch bytes)", (double)n * stride,
+                  [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_read<true>), dim3(cus * 8), dim3(256), 0, st, (const uint4*)rx,
+                           n * stride / 16, sink);
+    }});
+    run_variants(vs, s, rounds);
+    std::vector<uint8_t> hv(n);
+    CK(hipMemcpy(hv.data(), v1, n, hipMemcpyDeviceToHost));
+    size_t bad = 0;
+    for (auto b : hv) bad += b != 0;
+    std::printf("non-accept verdicts: %zu (expect 0)\n", bad);
+    return 0;
+}
+
 void run_variants(std::vector<Variant>& vs, hipStream_t s, int rounds)
 {
     hipEvent_t e0, e1;
@@ -316,6 +379,10 @@ int main(int argc, char** argv)
     if (argc > 1 && std::string(argv[1]) == "imix")
         return imix_main(argc > 2 ? std::strtoull(argv[2], nullptr, 10) : (4u << 20),
                          argc > 3 ? std::atoi(argv[3]) : 10);
+    if (argc > 1 && std::string(argv[1]) == "ext")
+        return ext_main(argc > 2 ? std::atoi(argv[2]) : 1500,
+                        argc > 3 ? std::strtoull(argv[3], nullptr, 10) : (1u << 20),
+                        argc > 4 ? std::atoi(argv[4]) : 15);
     if (argc > 1 && std::string(argv[1]) == "tx")
         return tx_main(argc > 2 ? std::strtoull(argv[2], nullptr, 10) : (1u << 20),
                        argc > 3 ? std::atoi(argv[3]) : 15);
