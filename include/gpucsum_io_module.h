@@ -28,6 +28,13 @@
  * Build mTCP WITHOUT -DDISABLE_HWCSUM so that ip_in.c / ip_out.c / tcp_in.c /
  * tcp_out.c consult dev_ioctl (configure.ac:119-125, Makefile.in:63-65).
  *
+ * RSS check (optional): with RSS configured (gpucsum_set_rss,
+ * or GPUCSUM_RSS_QUEUES=<n> [GPUCSUM_RSS_I40E=1] in the environment) each RX
+ * burst is classified instead of verified: the same verdicts plus, for every
+ * ACCEPT frame, the queue GetRSSCPUCore (rss.c:97-115) assigns its flow.
+ * Frames whose queue is not this thread's own are counted in rx_foreign --
+ * flows that mTCP's RSS-aware address pool (addr_pool.c:168,251) would have
+ * placed on another core.
  * Threading (core.c:1153-1245): load_module once on the main thread; every
  * other call from the owning mTCP thread.  Per-thread state is keyed by the
  * mtcp_thread_context pointer; mTCP thread k uses GPU k mod n_gpus (override:
@@ -91,6 +98,7 @@ struct gpucsum_stats {
 	uint64_t tx_frames;      /* frames filled in send_pkts                       */
 	uint64_t tx_batches;     /* GPU fill launches                                */
 	uint64_t gpu_failures;   /* GPU calls that failed (frames then dropped/unsent)*/
+	uint64_t rx_foreign;     /* RSS on: ACCEPT frames steered to another queue    */
 	int      device;         /* HIP device of this context                       */
 };
 int gpucsum_get_stats(struct mtcp_thread_context *ctx, struct gpucsum_stats *out);
@@ -98,6 +106,18 @@ int gpucsum_get_stats(struct mtcp_thread_context *ctx, struct gpucsum_stats *out
 /* Verdict of frame `index` of the last recv_pkts burst on `ifidx`
  * (GCS_V_* of mtcp_gpucsum.h), or -1. */
 int gpucsum_rx_verdict(struct mtcp_thread_context *ctx, int ifidx, int index);
+
+/* RSS steering check of this context: key (NULL = the reference's built-in
+ * key, rss.c:19-25; else >= 16 bytes), num_queues (0 = off), endian_check as
+ * GetRSSCPUCore takes it, and the queue this thread serves.  Environment
+ * default at init_handle: GPUCSUM_RSS_QUEUES / GPUCSUM_RSS_I40E, own queue =
+ * thread ordinal mod num_queues. */
+int gpucsum_set_rss(struct mtcp_thread_context *ctx, const uint8_t *key, uint32_t key_len,
+                    uint32_t num_queues, int endian_check, int own_queue);
+
+/* GetRSSCPUCore queue of frame `index` of the last burst on `ifidx` (RSS on,
+ * ACCEPT frames), 0xFFFF for other verdicts, or -1. */
+int gpucsum_rx_queue(struct mtcp_thread_context *ctx, int ifidx, int index);
 
 #ifdef __cplusplus
 }

@@ -32,6 +32,7 @@ struct rx_if {
 	uint8_t *ptr[GPUCSUM_MAX_BURST];
 	uint16_t len[GPUCSUM_MAX_BURST];
 	uint8_t verdict[GPUCSUM_MAX_BURST];
+	uint16_t queue[GPUCSUM_MAX_BURST];   /* RSS on */
 };
 
 struct tx_if {
@@ -47,6 +48,8 @@ struct gthr {
 	struct rx_if *rx[GPUCSUM_MAX_IFS];
 	struct tx_if *tx[GPUCSUM_MAX_IFS];
 	struct gpucsum_stats st;
+	int rss;                /* RSS steering check on */
+	int own_queue;
 };
 
 static io_module_func *g_inner;
@@ -140,6 +143,14 @@ static void gpucsum_init_handle(struct mtcp_thread_context *ctx)
 		die("gcs_ctx_create", rc);
 	g->st.device = dev;
 	t_cache = g;
+	env = getenv("GPUCSUM_RSS_QUEUES");
+	if (env && atoi(env) > 0) {
+		const char *e40 = getenv("GPUCSUM_RSS_I40E");
+		rc = gpucsum_set_rss(ctx, NULL, 0, (uint32_t)atoi(env), e40 && atoi(e40),
+		                     ordinal % atoi(env));
+		if (rc)
+			die("gpucsum_set_rss", rc);
+	}
 }
 
 static int32_t gpucsum_link_devices(struct mtcp_thread_context *ctx)
@@ -236,8 +247,12 @@ static int32_t gpucsum_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
 		if (!r->ptr[i])
 			r->len[i] = 0;
 	}
-	rc = gcs_verify_ptrs(g->gcs, r->ptr, r->len, (uint32_t)n, r->verdict,
-	                     GCS_VF_ZERO_BAD_TCP_CHECK);
+	if (g->rss)
+		rc = gcs_classify_ptrs(g->gcs, r->ptr, r->len, (uint32_t)n, r->verdict, NULL,
+		                       r->queue, GCS_VF_ZERO_BAD_TCP_CHECK);
+	else
+		rc = gcs_verify_ptrs(g->gcs, r->ptr, r->len, (uint32_t)n, r->verdict,
+		                     GCS_VF_ZERO_BAD_TCP_CHECK);
 	if (rc) {
 		g->st.gpu_failures++;
 		fprintf(stderr, "[gpucsum] RX verify of %d frames failed: %s %s\n", n,
@@ -249,6 +264,10 @@ static int32_t gpucsum_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
 	for (i = 0; i < n; i++)
 		if (!r->ptr[i])
 			r->verdict[i] = GCS_V_DROP_TRUNC;   /* the inner module's own drop */
+	if (g->rss && !rc)
+		for (i = 0; i < n; i++)
+			if (r->verdict[i] == GCS_V_ACCEPT && r->queue[i] != (uint16_t)g->own_queue)
+				g->st.rx_foreign++;
 	g->st.rx_frames += (uint64_t)n;
 	r->n = n;
 	return n;
@@ -352,4 +371,36 @@ int gpucsum_rx_verdict(struct mtcp_thread_context *ctx, int ifidx, int index)
 	if (!r || index < 0 || index >= r->n)
 		return -1;
 	return r->verdict[index];
+}
+
+int gpucsum_set_rss(struct mtcp_thread_context *ctx, const uint8_t *key, uint32_t key_len,
+                    uint32_t num_queues, int endian_check, int own_queue)
+{
+	struct gthr *g = lookup(ctx);
+	int rc;
+
+	if (!g)
+		return GCS_EINVAL;
+	if (num_queues == 0) {
+		g->rss = 0;
+		return GCS_OK;
+	}
+	if (own_queue < 0 || (uint32_t)own_queue >= num_queues)
+		return GCS_EINVAL;
+	rc = gcs_ctx_set_rss(g->gcs, key, key_len, num_queues, endian_check);
+	if (rc)
+		return rc;
+	g->rss = 1;
+	g->own_queue = own_queue;
+	return GCS_OK;
+}
+
+int gpucsum_rx_queue(struct mtcp_thread_context *ctx, int ifidx, int index)
+{
+	struct gthr *g = lookup(ctx);
+	struct rx_if *r = (g && ifidx >= 0 && ifidx < GPUCSUM_MAX_IFS) ? g->rx[ifidx] : NULL;
+
+	if (!r || !g->rss || index < 0 || index >= r->n)
+		return -1;
+	return r->verdict[index] == GCS_V_ACCEPT ? r->queue[index] : 0xFFFF;
 }

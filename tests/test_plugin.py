@@ -34,7 +34,7 @@ class Stats(C.Structure):
 class GStats(C.Structure):
     _fields_ = [(k, C.c_uint64) for k in
                 ("rx_frames", "rx_errors", "rx_batches", "tx_frames", "tx_batches",
-                 "gpu_failures")] + [("device", C.c_int)]
+                 "gpu_failures", "rx_foreign")] + [("device", C.c_int)]
 
 
 @pytest.fixture(scope="module")
@@ -62,6 +62,9 @@ def P():
     L.gpucsum_set_inner.argtypes = [C.c_void_p]
     L.gpucsum_get_stats.argtypes = [C.c_void_p, C.POINTER(GStats)]
     L.gpucsum_rx_verdict.argtypes = [C.c_void_p, C.c_int, C.c_int]
+    L.gpucsum_set_rss.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_int,
+                                  C.c_int]
+    L.gpucsum_rx_queue.argtypes = [C.c_void_p, C.c_int, C.c_int]
     return L
 
 
@@ -232,3 +235,32 @@ def test_decorator_rx_corrupted_imix(H, P, gpu_plugin):
     assert hw.rx_errors == len(bad)
     assert (hw_disp[bad] == MINI_NULL).all()
     assert (np.delete(hw_disp, bad) == MINI_ACCEPT).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nq,endian,own", [(8, 0, 3), (6, 1, 0)])
+def test_decorator_rss_steering_check(H, P, gpu_plugin, nq, endian, own):
+    """RSS on: the decorator classifies each burst; dispositions are unchanged
+    and rx_foreign counts the ACCEPT frames GetRSSCPUCore (rss.c:97-115)
+    assigns to another queue than this thread's."""
+    iom, ctx = gpu_plugin
+    n = 4000
+    buf, off, lens = synth.packed_frames(synth.imix_lengths(n, seed=18), seed=19)
+    O = Oracle()
+    O.compute_batch(buf, off, lens)
+    synth.corrupt(buf, off, lens, frac_log2=4, seed=20)
+    vd, _, q = O.classify_batch(buf.copy(), off, lens, nq, endian)
+    assert P.gpucsum_set_rss(ctx, None, 0, nq, endian, nq) != 0       # own queue out of range
+    assert P.gpucsum_set_rss(ctx, None, 0, nq, endian, own) == 0
+    try:
+        before = GStats()
+        P.gpucsum_get_stats(ctx, C.byref(before))
+        disp, st = rx_run(H, iom, ctx, buf.copy(), off, lens)
+        after = GStats()
+        P.gpucsum_get_stats(ctx, C.byref(after))
+        acc = vd == 0
+        assert st.accepted == acc.sum()
+        assert after.rx_foreign - before.rx_foreign == (acc & (q != own)).sum()
+        assert 0 < (acc & (q != own)).sum() < acc.sum()
+    finally:
+        assert P.gpucsum_set_rss(ctx, None, 0, 0, 0, 0) == 0
