@@ -21,6 +21,8 @@
  *                         ICMPOutput (icmp.c:57-69) inside the batched verify / fill.
  *   gcs_classify*, gcs_rss_dev  RSS steering: GetRSSHash / GetRSSCPUCore
  *                         (mtcp/src/rss.c:44-115), fused into the RX verify.
+ *   gcs_compute_copy_dev  SendTCPPacket's payload memcpy + both TX folds
+ *                         (tcp_out.c:316-333, ip_out.c:172) in one pass.
  *
  * The io_module_func plugin that sits on top of this ABI (the drop-in under
  * mtcp/src, io_module.h:60-72) is declared in gpucsum_io_module.h.
@@ -179,6 +181,23 @@ int gcs_ip_checksum_dev(gcs_ctx *ctx, const uint8_t *d_buf, uint64_t buf_bytes,
 int gcs_icmp_checksum_dev(gcs_ctx *ctx, const uint8_t *d_buf, uint64_t buf_bytes,
                           const uint64_t *d_off, const uint16_t *d_len, uint32_t n,
                           uint16_t *d_out, void *stream);
+
+/* ---- TX payload copy + fill (SendTCPPacket, tcp_out.c:316-333) ----------
+ * mTCP writes the headers of a data segment, memcpy's the payload behind them
+ * and then folds header + payload (and the IP header).  gcs_compute_copy_dev
+ * does the copy and both folds in one pass over device memory: frame i (at
+ * d_off[i], d_len[i] bytes, headers already written) receives its TCP payload
+ * -- tot_len + 14 - hl bytes, hl = 14 + ihl*4 + doff*4 -- from d_src +
+ * d_src_off[i] (any alignment), and its checks are filled as gcs_compute_dev
+ * fills them.  Only frames whose headers describe a complete TCP segment (the
+ * GCS_TX_OK conditions) are copied; the others get the plain fill.  A source
+ * range outside [0, src_bytes) gives GCS_TX_BAD_DESC and leaves the frame
+ * untouched.  flags: 0 (the copy is in place by definition). */
+int gcs_compute_copy_dev(gcs_ctx *ctx, uint8_t *d_frames, uint64_t frames_bytes,
+                         const uint64_t *d_off, const uint16_t *d_len,
+                         const uint8_t *d_src, uint64_t src_bytes,
+                         const uint64_t *d_src_off, uint32_t n, uint8_t *d_status,
+                         uint32_t *d_csums, uint32_t flags, void *stream);
 
 /* ---- RSS steering (rss.c) ----------------------------------------------
  * gcs_ctx_set_rss: the Toeplitz key (key_len >= 16; only the first 16 bytes

@@ -737,6 +737,22 @@ int gcs_ip_checksum_dev(gcs_ctx* ctx, const uint8_t* d_buf, uint64_t buf_bytes,
     return GCS_OK;
 }
 
+int gcs_compute_copy_dev(gcs_ctx* ctx, uint8_t* d_frames, uint64_t frames_bytes,
+                         const uint64_t* d_off, const uint16_t* d_len, const uint8_t* d_src,
+                         uint64_t src_bytes, const uint64_t* d_src_off, uint32_t n,
+                         uint8_t* d_status, uint32_t* d_csums, uint32_t flags, void* stream)
+{
+    if (!ctx || flags != 0 || (n && (!d_frames || !d_off || !d_len || !d_src || !d_src_off)))
+        return GCS_EINVAL;
+    if (n == 0)
+        return GCS_OK;
+    DeviceGuard g(ctx->device);
+    HIP_TRY(gcs::launch_copy_fill(d_frames, frames_bytes, d_off, d_len, d_src, src_bytes,
+                                  d_src_off, n, d_status, d_csums, flags,
+                                  pick_stream(ctx, stream)));
+    return GCS_OK;
+}
+
 int gcs_icmp_checksum_dev(gcs_ctx* ctx, const uint8_t* d_buf, uint64_t buf_bytes,
                           const uint64_t* d_off, const uint16_t* d_len, uint32_t n,
                           uint16_t* d_out, void* stream)

@@ -484,10 +484,12 @@ __device__ __forceinline__ uint4 patch_lo(uint4 v, int k, u32 lo16)
 // (the check fields always lie in chunks 1..5); `active` = false for padding
 // groups, which take part in the cross-lane steps but write nothing.
 // EXT adds the ICMP fold (GCS_VF_ICMP / GCS_CF_ICMP) and RSS steering: the
-// tuple words are gathered from the lanes holding them (held_hw).
+// tuple words are gathered from the lanes holding them (held_hw).  `wlim` =
+// bytes writable from f: a whole-chunk write-back never goes past it (a frame
+// ending at a buffer end that is not 16 B-aligned gets halfword stores).
 template <int G, int U, bool COMPUTE, int WM, bool EXT = false>
 __device__ __forceinline__ void epilogue(const Hdr& h, Acc a, uint8_t* __restrict__ f, u32 len,
-                                         bool desc_ok, int sub, u32 flags,
+                                         int64_t wlim, bool desc_ok, int sub, u32 flags,
                                          uint8_t* __restrict__ out_code,
                                          uint32_t* __restrict__ out_csum, bool active,
                                          const uint4 (&v)[U], const XFrame& xf = XFrame{})
@@ -614,6 +616,15 @@ __device__ __forceinline__ void epilogue(const Hdr& h, Acc a, uint8_t* __restric
                                          (wicmp && (c >> 2) == (cicmp >> 2)));
                 if (!take)
                     continue;
+                if (16 * c + 16 > wlim) {                    // chunk crosses the buffer end
+                    if (has_ip)
+                        *reinterpret_cast<uint16_t*>(f + 24) = (uint16_t)ipc;
+                    if (has_tcp)
+                        *reinterpret_cast<uint16_t*>(f + ts + 16) = (uint16_t)l4c;
+                    if (has_icmp)
+                        *reinterpret_cast<uint16_t*>(f + ts + 2) = (uint16_t)l4c;
+                    continue;
+                }
                 uint4 w = v[j];
                 if (has_ip)
                     w.z = (w.z & 0xFFFF0000u) | ipc;                 // bytes 24..25
@@ -695,7 +706,7 @@ __device__ __forceinline__ void frame_body(const uint4 (&v)[U], uint8_t* __restr
                 accum_chunk<COMPUTE>(w[j], 16 * (base + j * G + sub), ts, te, a);
         }
     }
-    epilogue<G, U, COMPUTE, WM, EXT>(h, a, wf, len, desc_ok, sub, flags, out_code, out_csum,
+    epilogue<G, U, COMPUTE, WM, EXT>(h, a, wf, len, avail, desc_ok, sub, flags, out_code, out_csum,
                                      active, v, xf);
 }
 

@@ -33,6 +33,10 @@ hipError_t launch_classify_fixed(uint8_t* frames, uint64_t stride, uint32_t fram
 hipError_t launch_classify_desc(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
                                 const uint16_t* len, uint32_t n, uint8_t* verdict,
                                 uint32_t flags, const Ext& ext, hipStream_t s);
+hipError_t launch_copy_fill(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
+                            const uint16_t* len, const uint8_t* src, uint64_t src_bytes,
+                            const uint64_t* src_off, uint32_t n, uint8_t* status,
+                            uint32_t* csums, uint32_t flags, hipStream_t s);
 hipError_t launch_icmp_fn(const uint8_t* buf, uint64_t buf_bytes, const uint64_t* off,
                           const uint16_t* len, uint32_t n, uint16_t* out, hipStream_t s);
 hipError_t launch_rss_fn(const uint32_t* sip, const uint32_t* dip, const uint16_t* sp,

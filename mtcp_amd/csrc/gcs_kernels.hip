@@ -132,7 +132,7 @@ __device__ __forceinline__ void small_frame(uint8_t* __restrict__ frames, uint64
             accum_chunk<COMPUTE>(v[c], 16 * c, ts, te, a);
     }
     // one-lane "group": epilogue<1, 4> finishes the frame (no reduction steps)
-    epilogue<1, 4, COMPUTE, kWM, EXT>(h, a, f, frame_len, true, 0, flags,
+    epilogue<1, 4, COMPUTE, kWM, EXT>(h, a, f, frame_len, (int64_t)stride, true, 0, flags,
                                       out_code ? out_code + i : nullptr,
                                       out_csum ? out_csum + i : nullptr, true, v,
                                       EXT ? small_xframe(ext, i, nib) : XFrame{});
@@ -294,6 +294,147 @@ k_desc_mixed_x(uint8_t* __restrict__ frames, uint64_t frames_bytes,
 {
     desc_mixed<COMPUTE, XCD, OCC, true>(frames, frames_bytes, off, lens, n, out_code, out_csum,
                                         flags, ext);
+}
+
+// ---------------------------------------------------------------------------
+// TX payload copy + fill (SendTCPPacket, tcp_out.c:316-333:
+// memcpy of the payload behind the TCP header, then TCPCalcChecksum over
+// header + payload, then IPOutput's ip_fast_csum, ip_out.c:172).  One pass:
+// the payload is read once from the source, folded while in registers and
+// written once into the frame; only the header chunks are read from the frame.
+// A frame is copied when its headers describe a complete TCP segment (the
+// conditions under which the fill returns GCS_TX_OK); any other frame gets the
+// plain fill.  Payload bytes [hl, te) of the frame come from src + pay_off[i]
+// (any alignment: unaligned 16 B loads), hl = 14 + 4*ihl + 4*doff, te = 14 +
+// tot_len; bytes past te are left as they are.
+
+typedef u32x4 u32x4_u __attribute__((aligned(1)));
+
+__device__ __forceinline__ uint4 ldg16u(const uint8_t* p)
+{
+    const u32x4 r = *reinterpret_cast<const u32x4_u*>(p);
+    return make_uint4(r.x, r.y, r.z, r.w);
+}
+
+__device__ __forceinline__ u32 chunk_byte(const uint4& v, int k)
+{
+    return (pick(v, k >> 2) >> (8 * (k & 3))) & 0xFFu;
+}
+
+template <int G, int U>
+__global__ void __launch_bounds__(kBlock)
+k_copy_fill(uint8_t* __restrict__ frames, uint64_t frames_bytes,
+            const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens,
+            const uint8_t* __restrict__ src, uint64_t src_bytes,
+            const uint64_t* __restrict__ src_off, u32 n, uint8_t* __restrict__ out_code,
+            uint32_t* __restrict__ out_csum, u32 flags)
+{
+    static_assert(G >= 16, "the first G chunks must hold the longest header (134 B)");
+    constexpr int FPB = kBlock / G;
+    const int sub = threadIdx.x & (G - 1);
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);
+    const uint64_t i = (uint64_t)blk * FPB + threadIdx.x / G;
+    if (i >= n)
+        return;
+    const uint64_t o = off[i];
+    const u32 len = lens[i];
+    const bool ok = (o & 15) == 0 && o <= frames_bytes && len <= frames_bytes - o;
+    uint8_t* f = frames + (ok ? o : 0);
+    const int64_t avail = ok ? (int64_t)(frames_bytes - o) : 0;
+    const int nchunks = ok ? (int)((len + 15) >> 4) : 0;
+    const uint4 z = make_uint4(0, 0, 0, 0);
+
+    // headers: frame chunk `sub` of the first G chunks
+    const uint4 hv = sub < nchunks ? load_chunk<true, false>(f + 16 * sub, avail - 16 * sub) : z;
+    Hdr h;
+    h.d3 = group_bcast<G, 0>(hv.w);
+    h.d4 = group_bcast<G, 1>(hv.x);
+    h.d5 = group_bcast<G, 1>(hv.y);
+    const int ihl = (int)((h.d3 >> 16) & 15u);
+    const int ts = 14 + 4 * ihl;
+    const int tot = (int)bswap16(h.d4 & 0xFFFFu);
+    const int te = 14 + tot;
+    const int pd = ts + 12;                            // doff << 4 | res
+    const u32 db = group_sum<G>(sub == (pd >> 4) ? chunk_byte(hv, pd & 15) : 0u);
+    const int doff = (int)(db >> 4);
+    const int hl = ts + 4 * doff;
+    const bool copy = ok && len >= 34 && (h.d3 & 0xFFFFu) == 0x0008u && ihl >= 5 &&
+                      (h.d5 >> 24) == 6 && doff >= 5 && tot >= 4 * (ihl + doff) &&
+                      te <= (int)len;
+    const uint64_t plen = copy ? (uint64_t)(te - hl) : 0;
+    const uint64_t po = copy ? src_off[i] : 0;
+    if (copy && !(po <= src_bytes && plen <= src_bytes - po)) {   // group-uniform
+        if (sub == 0) {
+            if (out_code)
+                out_code[i] = GCS_TX_BAD_DESC;
+            if (out_csum)
+                out_csum[i] = 0;
+        }
+        return;
+    }
+    const uint8_t* ps = src + po;                      // frame byte p <- ps[p - hl]
+
+    Acc a = {0u, 0u, 0u};
+    uint4 first[U];
+    for (int base = 0; base < nchunks; base += G * U) {   // group-uniform
+        uint4 v[U];
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            const int c = base + j * G + sub;
+            const int cb = 16 * c;
+            uint4 x = z;
+            if (c < nchunks) {
+                const bool frame_bytes = !copy || cb < hl || cb + 16 > te;
+                uint4 fr = z;
+                if (base == 0 && j == 0)
+                    fr = hv;
+                else if (frame_bytes)
+                    fr = load_chunk<true, false>(f + cb, avail - cb);
+                if (!copy || cb + 16 <= hl || cb >= te) {
+                    x = fr;                                  // header / past the segment
+                } else if (cb >= hl && cb + 16 <= te) {
+                    x = ldg16u(ps + (cb - hl));              // payload
+                } else {                                     // straddles hl or te
+                    u32 w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+                    for (int k = 0; k < 16; k++) {
+                        const int p = cb + k;
+                        const u32 b = (p >= hl && p < te) ? (u32)ps[p - hl] : chunk_byte(fr, k);
+                        w[k >> 2] |= b << (8 * (k & 3));
+                    }
+                    x = make_uint4(w[0], w[1], w[2], w[3]);
+                }
+            }
+            v[j] = x;
+        }
+#pragma unroll
+        for (int j = 0; j < U; j++)
+            accum_chunk<true>(v[j], 16 * (base + j * G + sub), ts, te, a);
+        if (copy) {
+            // chunks 8.. go out now; the first line (with the check fields) in the epilogue
+#pragma unroll
+            for (int j = 0; j < U; j++) {
+                const int c = base + j * G + sub;
+                const int cb = 16 * c;
+                if (c < 8 || c >= nchunks || cb >= te)
+                    continue;
+                if (cb + 16 <= avail) {
+                    stg16<WM_SECTOR>(f + cb, v[j]);
+                } else {                                     // the buffer ends inside it
+                    for (int k = 0; k < 16 && cb + k < te; k++)
+                        f[cb + k] = (uint8_t)chunk_byte(v[j], k);
+                }
+            }
+        }
+        if (base == 0) {
+#pragma unroll
+            for (int j = 0; j < U; j++)
+                first[j] = v[j];
+        }
+    }
+    epilogue<G, U, true, WM_LINE_SC1>(h, a, f, len, avail, ok, sub, flags & ~GCS_CF_NO_INPLACE,
+                                      out_code ? out_code + i : nullptr,
+                                      out_csum ? out_csum + i : nullptr, true, first);
 }
 
 // TCPCalcChecksum(buf + off[i], len[i], saddr[i], daddr[i]), G lanes per item;
@@ -521,6 +662,17 @@ hipError_t launch_rss_fn(const uint32_t* sip, const uint32_t* dip, const uint16_
 {
     hipLaunchKernelGGL(k_rss_fn, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, sip, dip,
                        sp, dp, n, ext);
+    return hipGetLastError();
+}
+
+hipError_t launch_copy_fill(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
+                            const uint16_t* len, const uint8_t* src, uint64_t src_bytes,
+                            const uint64_t* src_off, u32 n, uint8_t* status, uint32_t* csums,
+                            u32 flags, hipStream_t s)
+{
+    constexpr int G = 32, U = 3, FPB = kBlock / G;
+    hipLaunchKernelGGL((k_copy_fill<G, U>), dim3((n + FPB - 1) / FPB), dim3(kBlock), 0, s, frames,
+                       frames_bytes, off, len, src, src_bytes, src_off, n, status, csums, flags);
     return hipGetLastError();
 }
 

@@ -77,6 +77,8 @@ def lib() -> C.CDLL:
             "gcs_verify_ptrs": (i, [vp, vp, vp, u32, vp, u32]),
             "gcs_compute_ptrs": (i, [vp, vp, vp, u32, vp, vp]),
             "gcs_icmp_checksum_dev": (i, [vp, vp, u64, vp, vp, u32, vp, vp]),
+            "gcs_compute_copy_dev": (i, [vp, vp, u64, vp, vp, vp, u64, vp, u32, vp, vp, u32,
+                                         vp]),
             "gcs_ctx_set_rss": (i, [vp, vp, u32, u32, i]),
             "gcs_classify_fixed_dev": (i, [vp, vp, u64, u32, u32, vp, vp, vp, u32, vp]),
             "gcs_classify_dev": (i, [vp, vp, u64, vp, vp, u32, vp, vp, vp, u32, vp]),
@@ -236,6 +238,18 @@ class Context:
             self._need(a, w * n, "array")
         check(self.L.gcs_ip_checksum_dev(self.h, _daddr(buf), bb, _daddr(off), _daddr(ihl), n,
                                          _daddr(out), stream), "ip_checksum")
+
+    def compute_copy(self, frames, off, lens, src, src_off, n, status=None, csums=None,
+                     flags=0, stream=None, frames_bytes=None, src_bytes=None):
+        fb = _nbytes(frames) if frames_bytes is None else frames_bytes
+        sb = _nbytes(src) if src_bytes is None else src_bytes
+        self._need(frames, fb, "frames")
+        self._need(src, sb, "src")
+        for a, w in ((off, 8), (lens, 2), (src_off, 8), (status, 1), (csums, 4)):
+            self._need(a, w * n, "array")
+        check(self.L.gcs_compute_copy_dev(self.h, _daddr(frames), fb, _daddr(off), _daddr(lens),
+                                          _daddr(src), sb, _daddr(src_off), n, _daddr(status),
+                                          _daddr(csums), flags, stream), "compute_copy")
 
     def icmp_checksum(self, buf, off, lens, n, out, stream=None, buf_bytes=None):
         bb = _nbytes(buf) if buf_bytes is None else buf_bytes

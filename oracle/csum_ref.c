@@ -295,6 +295,53 @@ int ref_tx_fill_f(uint8_t *f, uint32_t len, uint32_t *csums, uint32_t flags)
 	return REF_TX_OK;
 }
 
+/* tcp_out.c:316-321 memcpy's the payload behind header + options, then
+ * :323-333 folds; IPOutput's fold follows (ip_out.c:172). */
+int ref_tx_copy_fill(uint8_t *f, uint32_t len, const uint8_t *src, uint64_t src_avail,
+                     uint32_t *csums)
+{
+	if (len >= 34 && ld16(f + 12) == 0x0008) {
+		uint32_t ihl = f[14] & 0x0Fu, ts = 14 + 4 * ihl;
+		uint32_t tot = bswap16((uint16_t)ld16(f + 16));
+		if (ihl >= 5 && f[23] == 6 && ts + 12 < len) {
+			uint32_t doff = f[ts + 12] >> 4, hl = ts + 4 * doff;
+			if (doff >= 5 && tot >= 4 * (ihl + doff) && 14 + tot <= len) {
+				uint32_t plen = 14 + tot - hl;
+				if (!src || plen > src_avail) {
+					if (csums)
+						*csums = 0;
+					return REF_TX_BAD_DESC;
+				}
+				memcpy(f + hl, src, plen);
+			}
+		}
+	}
+	return ref_tx_fill(f, len, csums);
+}
+
+void ref_compute_copy_batch(uint8_t *buf, uint64_t buf_bytes, const uint64_t *off,
+                            const uint16_t *len, uint32_t n, const uint8_t *src,
+                            uint64_t src_bytes, const uint64_t *src_off, uint8_t *status,
+                            uint32_t *csums)
+{
+	uint32_t i;
+	for (i = 0; i < n; i++) {
+		int s;
+		uint64_t so = src_off[i];
+		if (!((off[i] & 15) == 0 && off[i] <= buf_bytes && len[i] <= buf_bytes - off[i])) {
+			s = REF_TX_BAD_DESC;
+			if (csums)
+				csums[i] = 0;
+		} else {
+			s = ref_tx_copy_fill(buf + off[i], len[i], so <= src_bytes ? src + so : NULL,
+			                     so <= src_bytes ? src_bytes - so : 0,
+			                     csums ? &csums[i] : NULL);
+		}
+		if (status)
+			status[i] = (uint8_t)s;
+	}
+}
+
 static int desc_ok(uint64_t buf_bytes, uint64_t off, uint32_t len)
 {
 	return (off & 15) == 0 && off <= buf_bytes && len <= buf_bytes - off;

@@ -16,6 +16,7 @@
  *                          tcp_in.c:1208-1241            (RX verify order)
  *   ref_tx_fill            mtcp/src/ip_out.c:143-173, tcp_out.c:244,323-333
  *                          (TX: check fields zero when folded, then stored)
+ *   ref_tx_copy_fill       mtcp/src/tcp_out.c:316-333    (payload memcpy + fill)
  *   ref_icmp_checksum      mtcp/src/icmp.c:18-42         (ICMPChecksum, static)
  *   ref_rss_hash/_core     mtcp/src/rss.c:13-41,44-86,97-115 (BuildKeyCache,
  *                          GetRSSHash, GetRSSCPUCore)
@@ -89,6 +90,21 @@ int ref_rx_verdict(uint8_t *frame, uint32_t len, uint32_t flags);
  * ICMP message, tot_len - ihl*4 bytes); csums then holds ip | icmp << 16. */
 int ref_tx_fill(uint8_t *frame, uint32_t len, uint32_t *csums);
 int ref_tx_fill_f(uint8_t *frame, uint32_t len, uint32_t *csums, uint32_t flags);
+
+/* TX payload copy + fill (SendTCPPacket, tcp_out.c:316-333): when the frame's
+ * headers describe a complete TCP segment (IPv4, ihl >= 5, TCP, doff >= 5,
+ * tot_len >= (ihl+doff)*4, 14 + tot_len <= len), its payload -- bytes
+ * [hl, 14 + tot_len), hl = 14 + ihl*4 + doff*4 -- is copied from src (which
+ * must hold that many bytes and not be NULL -- NULL is a source offset past
+ * the source buffer -- else REF_TX_BAD_DESC and nothing is written);
+ * then ref_tx_fill.  The batch takes per-frame source offsets into one
+ * source buffer of src_bytes. */
+int ref_tx_copy_fill(uint8_t *frame, uint32_t len, const uint8_t *src, uint64_t src_avail,
+                     uint32_t *csums);
+void ref_compute_copy_batch(uint8_t *buf, uint64_t buf_bytes, const uint64_t *off,
+                            const uint16_t *len, uint32_t n, const uint8_t *src,
+                            uint64_t src_bytes, const uint64_t *src_off, uint8_t *status,
+                            uint32_t *csums);
 
 /* ICMPChecksum(buf, len): LE 16-bit words, an odd final byte added as the
  * low byte of a zero-high-byte word, two-step fold, ~.  The C leaves the high

@@ -73,6 +73,9 @@ class Oracle:
         L.ref_tx_fill_f.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]
         L.ref_compute_batch_f.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
                                           C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint32]
+        L.ref_compute_copy_batch.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
+                                             C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p,
+                                             C.c_void_p, C.c_void_p]
         L.ref_rss_hash.restype = C.c_uint32
         L.ref_rss_hash.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint16, C.c_uint16]
         L.ref_rss_core.restype = C.c_int
@@ -136,6 +139,17 @@ class Oracle:
         self.L.ref_classify_fixed(_p(buf), stride, frame_len, n, _p(vd), _p(h), _p(q), flags,
                                   _p(k), num_queues, endian_check)
         return vd, h, q
+
+    def compute_copy_batch(self, buf, off, lens, src, src_off):
+        n = len(off)
+        st = np.zeros(n, dtype=np.uint8)
+        cs = np.zeros(n, dtype=np.uint32)
+        self.L.ref_compute_copy_batch(_p(buf), buf.nbytes,
+                                      _p(np.ascontiguousarray(off, np.uint64)),
+                                      _p(np.ascontiguousarray(lens, np.uint16)), n, _p(src),
+                                      src.nbytes, _p(np.ascontiguousarray(src_off, np.uint64)),
+                                      _p(st), _p(cs))
+        return st, cs
 
     def icmp_checksum_batch(self, buf, off, lens):
         n = len(off)

@@ -124,3 +124,31 @@ def test_icmp_frames_rx_tx(both, payload):
     for i in range(n):
         assert O.L.ref_rx_verdict(b1.ctypes.data + i * stride, L, 2) == \
             R.rx_verdict_f_at(b1, i * stride, L, 2)
+
+
+def test_copy_fill_is_memcpy_then_reference_fill(both):
+    """tcp_out.c:316-333: the oracle's fused copy + fill equals the payload
+    memcpy followed by the reference's own fill, frame by frame."""
+    O, R = both
+    rng = np.random.default_rng(12)
+    n = 1500
+    buf, off, lens = synth.packed_frames(synth.imix_lengths(n, seed=13), seed=14)
+    for i in np.nonzero(rng.random(n) < 0.1)[0]:
+        buf[int(off[i]) + 23] = 1                          # not TCP: plain fill
+    src = rng.integers(0, 256, size=3_000_000, dtype=np.uint8)
+    so = rng.integers(0, len(src) - 1600, size=n).astype(np.uint64)
+    a = buf.copy()
+    st, cs = O.compute_copy_batch(a, off, lens, src, so)
+    b = buf.copy()
+    for i in range(n):
+        o, L = int(off[i]), int(lens[i])
+        ihl = int(b[o + 14]) & 15
+        ts = 14 + 4 * ihl
+        if int(b[o + 23]) == 6:
+            hl = ts + 4 * (int(b[o + ts + 12]) >> 4)
+            tot = (int(b[o + 16]) << 8) | int(b[o + 17])
+            pl = 14 + tot - hl
+            b[o + hl:o + hl + pl] = src[int(so[i]):int(so[i]) + pl]
+        s, c = R.tx_fill_at(b, o, L)
+        assert (s, c) == (st[i], cs[i])
+    np.testing.assert_array_equal(a, b)
