@@ -23,6 +23,8 @@
  *                         (mtcp/src/rss.c:44-115), fused into the RX verify.
  *   gcs_compute_copy_dev  SendTCPPacket's payload memcpy + both TX folds
  *                         (tcp_out.c:316-333, ip_out.c:172) in one pass.
+ *   gcs_gro_dev           software LRO: in-order segment merge with refilled checks
+ *                         (the NIC LRO of ENABLELRO builds, dpdk_module.c:855-881).
  *
  * The io_module_func plugin that sits on top of this ABI (the drop-in under
  * mtcp/src, io_module.h:60-72) is declared in gpucsum_io_module.h.
@@ -198,6 +200,28 @@ int gcs_compute_copy_dev(gcs_ctx *ctx, uint8_t *d_frames, uint64_t frames_bytes,
                          const uint8_t *d_src, uint64_t src_bytes,
                          const uint64_t *d_src_off, uint32_t n, uint8_t *d_status,
                          uint32_t *d_csums, uint32_t flags, void *stream);
+
+/* ---- software LRO: receive-side segment merge ----------------------------
+ * What a NIC's LRO does for mTCP's ENABLELRO builds (dpdk_module.c:44-48,
+ * 855-881; tcp_ring_buffer.c:15-21), on the GPU, after the RX verify.  Over
+ * windows of `window` (1..256) consecutive descriptors, runs of in-order
+ * ACCEPT segments of one flow become one frame: the head's headers with
+ * tot_len updated and PSH if any member had it, the payloads in order, IP and
+ * TCP checks refilled -- a frame mTCP's own RX checks accept.  The merge rules
+ * (Linux GRO's) are listed in oracle/csum_ref.h (ref_gro_batch); a run never
+ * exceeds max_len bytes (<= 65535; mTCP's LRO buffers are 16384, dpdk_module.c:45).
+ * d_verdict: the frames' GCS_V_* verdicts (gcs_verify_dev / gcs_classify_dev).
+ * Output frames of a window are packed from the window's first input offset,
+ * 16 B-aligned, into d_out (out_bytes; nothing past it is written): inputs must
+ * be packed in increasing offset order, and out_bytes >= in_bytes keeps every
+ * frame whole.  Per input frame i: d_head[i] = index of its run's head;
+ * d_out_off[i] = the run's output offset; d_out_len[i] = the run's length for
+ * a head, 0 for a merged member (and for a bad descriptor). */
+int gcs_gro_dev(gcs_ctx *ctx, const uint8_t *d_in, uint64_t in_bytes,
+                const uint64_t *d_off, const uint16_t *d_len, const uint8_t *d_verdict,
+                uint32_t n, uint32_t window, uint32_t max_len, uint8_t *d_out,
+                uint64_t out_bytes, uint64_t *d_out_off, uint16_t *d_out_len,
+                uint32_t *d_head, void *stream);
 
 /* ---- RSS steering (rss.c) ----------------------------------------------
  * gcs_ctx_set_rss: the Toeplitz key (key_len >= 16; only the first 16 bytes

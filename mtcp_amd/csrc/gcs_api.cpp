@@ -753,6 +753,23 @@ int gcs_compute_copy_dev(gcs_ctx* ctx, uint8_t* d_frames, uint64_t frames_bytes,
     return GCS_OK;
 }
 
+int gcs_gro_dev(gcs_ctx* ctx, const uint8_t* d_in, uint64_t in_bytes, const uint64_t* d_off,
+                const uint16_t* d_len, const uint8_t* d_verdict, uint32_t n, uint32_t window,
+                uint32_t max_len, uint8_t* d_out, uint64_t out_bytes, uint64_t* d_out_off,
+                uint16_t* d_out_len, uint32_t* d_head, void* stream)
+{
+    if (!ctx || window == 0 || window > 256 || max_len > 65535 ||
+        (n && (!d_in || !d_off || !d_len || !d_verdict || !d_out || !d_out_off || !d_out_len ||
+               !d_head)))
+        return GCS_EINVAL;
+    if (n == 0)
+        return GCS_OK;
+    DeviceGuard g(ctx->device);
+    HIP_TRY(gcs::launch_gro(d_in, in_bytes, d_off, d_len, d_verdict, n, window, max_len, d_out,
+                            out_bytes, d_out_off, d_out_len, d_head, pick_stream(ctx, stream)));
+    return GCS_OK;
+}
+
 int gcs_icmp_checksum_dev(gcs_ctx* ctx, const uint8_t* d_buf, uint64_t buf_bytes,
                           const uint64_t* d_off, const uint16_t* d_len, uint32_t n,
                           uint16_t* d_out, void* stream)

@@ -37,6 +37,10 @@ hipError_t launch_copy_fill(uint8_t* frames, uint64_t frames_bytes, const uint64
                             const uint16_t* len, const uint8_t* src, uint64_t src_bytes,
                             const uint64_t* src_off, uint32_t n, uint8_t* status,
                             uint32_t* csums, uint32_t flags, hipStream_t s);
+hipError_t launch_gro(const uint8_t* in, uint64_t in_bytes, const uint64_t* off,
+                      const uint16_t* len, const uint8_t* verdict, uint32_t n, uint32_t window,
+                      uint32_t max_len, uint8_t* out, uint64_t out_bytes, uint64_t* out_off,
+                      uint16_t* out_len, uint32_t* head, hipStream_t s);
 hipError_t launch_icmp_fn(const uint8_t* buf, uint64_t buf_bytes, const uint64_t* off,
                           const uint16_t* len, uint32_t n, uint16_t* out, hipStream_t s);
 hipError_t launch_rss_fn(const uint32_t* sip, const uint32_t* dip, const uint16_t* sp,

@@ -437,6 +437,267 @@ k_copy_fill(uint8_t* __restrict__ frames, uint64_t frames_bytes,
                                       out_csum ? out_csum + i : nullptr, true, first);
 }
 
+// ---------------------------------------------------------------------------
+// Software LRO (the merge a NIC's LRO does for mTCP's
+// ENABLELRO builds, dpdk_module.c:855-881).  Rules: oracle/csum_ref.h
+// ref_gro_batch.  One block per window of <= kGroW frames:
+//   A  thread t parses frame t's first 96 B into LDS;
+//   B  thread t decides whether frame t continues frame t-1;
+//   C  thread 0 walks the window once to form runs (length limit), offsets;
+//   D  each wave builds whole runs: a single frame is copied as it is, a
+//      longer run is assembled destination-chunk by destination-chunk (head
+//      headers with tot_len / PSH patched, then the members' payloads through
+//      unaligned 16 B loads), folded on the way (accum_chunk) and written,
+//      with the checks filled by the TX epilogue -- the merged frame is read
+//      once and written once.
+
+constexpr int kGroW = 256;      // frames per window (one per thread)
+constexpr int kGroHdr = 96;     // header bytes kept per frame (14 + 20 + 60 + 2)
+
+__device__ __forceinline__ u32 lds_be16(const uint8_t* p) { return ((u32)p[0] << 8) | p[1]; }
+__device__ __forceinline__ u32 lds_be32(const uint8_t* p)
+{
+    return ((u32)p[0] << 24) | ((u32)p[1] << 16) | ((u32)p[2] << 8) | p[3];
+}
+
+// gro_continues of oracle/csum_ref.c over two frames' header bytes
+__device__ bool gro_cont(const uint8_t* p, const uint8_t* c, int pp, int pc)
+{
+    if (pp <= 0 || pc <= 0)
+        return false;
+    if (p[15] != c[15] || lds_be16(p + 20) != lds_be16(c + 20) || (lds_be16(p + 20) & 0x3FFFu) ||
+        p[22] != c[22])
+        return false;
+    for (int k = 26; k < 34; k++)
+        if (p[k] != c[k])
+            return false;
+    const u32 idp = lds_be16(p + 18), idc = lds_be16(c + 18);
+    if (idc != idp && idc != ((idp + 1) & 0xFFFFu))
+        return false;
+    for (int k = 34; k < 38; k++)
+        if (p[k] != c[k])
+            return false;
+    for (int k = 42; k < 46; k++)
+        if (p[k] != c[k])
+            return false;
+    if (c[46] != p[46] || (p[46] & 0x0F) || lds_be16(p + 48) != lds_be16(c + 48) ||
+        lds_be16(p + 52) || lds_be16(c + 52))
+        return false;
+    if (p[47] != 0x10 || (c[47] != 0x10 && c[47] != 0x18))
+        return false;
+    const int hl = 34 + 4 * (p[46] >> 4);
+    for (int k = 54; k < hl; k++)
+        if (p[k] != c[k])
+            return false;
+    return lds_be32(c + 38) == lds_be32(p + 38) + (u32)pp;
+}
+
+template <int U>
+__global__ void __launch_bounds__(kBlock)
+k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restrict__ off,
+      const uint16_t* __restrict__ lens, const uint8_t* __restrict__ verdict, u32 n, u32 window,
+      u32 max_len, uint8_t* __restrict__ out, uint64_t out_bytes, uint64_t* __restrict__ out_off,
+      uint16_t* __restrict__ out_len, uint32_t* __restrict__ head)
+{
+    static_assert(kBlock == kGroW, "one frame per thread");
+    constexpr int G = 64;
+    __shared__ uint8_t hdr[kGroW][kGroHdr];
+    __shared__ int pay[kGroW];         // TCP payload bytes of a mergeable frame, else -1
+    __shared__ uint8_t cont[kGroW];
+    __shared__ uint8_t dok[kGroW];     // descriptor inside the input buffer
+    __shared__ uint32_t pref[kGroW];   // payload offset of a member within its run
+    __shared__ uint16_t rhead[kGroW];  // run head (window index) of each frame
+    __shared__ uint16_t run_t[kGroW];  // runs: head index, member count, length, offset
+    __shared__ uint16_t run_n[kGroW];
+    __shared__ uint32_t run_len[kGroW];
+    __shared__ uint64_t run_off[kGroW];
+    __shared__ int nruns;
+
+    const int t = threadIdx.x;
+    const uint64_t w0 = (uint64_t)blockIdx.x * window;
+    const int cnt = (int)min<uint64_t>(window, n - w0);
+    const uint4 z = make_uint4(0, 0, 0, 0);
+
+    // A: parse
+    if (t < cnt) {
+        const uint64_t o = off[w0 + t];
+        const u32 L = lens[w0 + t];
+        const bool ok = (o & 15) == 0 && o <= in_bytes && L <= in_bytes - o;
+        const bool acc = ok && verdict[w0 + t] == GCS_V_ACCEPT;
+        dok[t] = ok;
+#pragma unroll
+        for (int c = 0; c < kGroHdr / 16; c++) {
+            const uint4 v = acc ? load_chunk<true, false>(in + o + 16 * c,
+                                                          (int64_t)(in_bytes - o) - 16 * c)
+                                : z;
+            uint32_t* d = reinterpret_cast<uint32_t*>(&hdr[t][16 * c]);
+            d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+        }
+        const uint8_t* h = hdr[t];
+        int p = -1;
+        if (acc && (h[14] & 0x0F) == 5)
+            p = (int)lds_be16(h + 16) - 20 - 4 * (h[46] >> 4);
+        pay[t] = p;
+    }
+    __syncthreads();
+    // B: continuation
+    if (t < cnt)
+        cont[t] = t > 0 && gro_cont(hdr[t - 1], hdr[t], pay[t - 1], pay[t]);
+    __syncthreads();
+    // C: runs (one thread walks the window)
+    if (t == 0) {
+        uint64_t o = cnt ? off[w0] : 0;
+        int r = -1, cur = 0;
+        u32 mlen = 0;
+        bool mergeable = false;
+        for (int k = 0; k < cnt; k++) {
+            if (k > 0 && mergeable && cont[k] && mlen + (u32)pay[k] <= max_len) {
+                pref[k] = mlen - (34 + 4 * (hdr[cur][46] >> 4));
+                mlen += (u32)pay[k];
+                rhead[k] = (uint16_t)cur;
+                run_n[r]++;
+                run_len[r] = mlen;
+                continue;
+            }
+            if (r >= 0)
+                o += (run_len[r] + 15u) & ~15u;
+            r++;
+            cur = k;
+            mergeable = pay[k] > 0;
+            mlen = mergeable ? 34 + 4 * (hdr[k][46] >> 4) + (u32)pay[k]
+                             : (dok[k] ? (u32)lens[w0 + k] : 0u);      // a bad descriptor: nothing
+            pref[k] = 0;
+            rhead[k] = (uint16_t)k;
+            run_t[r] = (uint16_t)k;
+            run_n[r] = 1;
+            run_len[r] = mlen;
+            run_off[r] = o;
+        }
+        nruns = r + 1;
+    }
+    __syncthreads();
+    if (t < cnt) {
+        const int hk = rhead[t];
+        head[w0 + t] = (uint32_t)(w0 + hk);
+        // the run's offset: the head's entry (runs are listed in head order)
+        int lo = 0, hi = nruns - 1;
+        while (lo < hi) {                              // last run with run_t <= hk
+            const int mid = (lo + hi + 1) >> 1;
+            if (run_t[mid] <= hk) lo = mid; else hi = mid - 1;
+        }
+        out_off[w0 + t] = run_off[lo];
+        out_len[w0 + t] = hk == t ? (uint16_t)run_len[lo] : (uint16_t)0;
+    }
+
+    // D: build the runs, one wave per run
+    const int wave = t >> 6, sub = t & 63, nwaves = kBlock / 64;
+    for (int r = wave; r < nruns; r += nwaves) {       // wave-uniform
+        const int k0 = run_t[r], nm = run_n[r];
+        const u32 mlen = run_len[r];
+        const uint64_t oo = run_off[r];
+        uint8_t* m = out + oo;
+        const int64_t wlim = oo <= out_bytes ? (int64_t)(out_bytes - oo) : 0;
+        const uint64_t io = off[w0 + k0];
+        const int nchunks = (int)((mlen + 15) >> 4);
+        if (nm == 1) {                                 // as it is
+            const int64_t avail = (int64_t)(in_bytes - io);
+            for (int c = sub; c < nchunks; c += G) {
+                const uint4 v = load_chunk<true, false>(in + io + 16 * c, avail - 16 * c);
+                if (16 * c + 16 <= wlim) {
+                    stg16<WM_SECTOR>(m + 16 * c, v);
+                } else {
+                    for (int k = 0; k < 16 && 16 * c + k < (int)mlen && 16 * c + k < wlim; k++)
+                        m[16 * c + k] = (uint8_t)chunk_byte(v, k);
+                }
+            }
+            continue;
+        }
+        const uint8_t* hh = hdr[k0];
+        const int hl = 34 + 4 * (hh[46] >> 4);
+        uint8_t psh = 0;
+        for (int k = k0; k < k0 + nm; k++)
+            psh |= hdr[k][47] & 0x08;
+        const int ts = 34, te = (int)mlen;
+        Acc a = {0u, 0u, 0u};
+        uint4 first[U];
+        for (int base = 0; base < nchunks; base += G * U) {
+            uint4 v[U];
+#pragma unroll
+            for (int j = 0; j < U; j++) {
+                const int c = base + j * G + sub;
+                const int cb = 16 * c;
+                uint4 x = z;
+                if (c < nchunks) {
+                    // payload member holding merged byte cb (binary search on pref)
+                    int sg = k0;
+                    if (cb >= hl) {
+                        int lo2 = k0, hi2 = k0 + nm - 1;
+                        const u32 q = (u32)(cb - hl);
+                        while (lo2 < hi2) {
+                            const int mid = (lo2 + hi2 + 1) >> 1;
+                            if (pref[mid] <= q) lo2 = mid; else hi2 = mid - 1;
+                        }
+                        sg = lo2;
+                    }
+                    const u32 q = (u32)(cb - hl);
+                    if (cb >= hl && cb + 16 <= te && q + 16 <= pref[sg] + (u32)pay[sg]) {
+                        x = ldg16u(in + off[w0 + sg] + hl + (q - pref[sg]));
+                    } else {
+                        u32 w[4] = {0u, 0u, 0u, 0u};
+                        int s2 = sg;
+                        for (int k = 0; k < 16; k++) {
+                            const int p = cb + k;
+                            u32 b = 0;
+                            if (p < hl) {
+                                b = p < kGroHdr ? hh[p] : 0u;
+                            } else if (p < te) {
+                                const u32 qq = (u32)(p - hl);
+                                while (qq >= pref[s2] + (u32)pay[s2])
+                                    s2++;
+                                b = in[off[w0 + s2] + hl + (qq - pref[s2])];
+                            }
+                            w[k >> 2] |= b << (8 * (k & 3));
+                        }
+                        x = make_uint4(w[0], w[1], w[2], w[3]);
+                    }
+                    if (c == 1)                                // tot_len (bytes 16-17)
+                        x.x = (x.x & 0xFFFF0000u) | bswap16((mlen - 14) & 0xFFFFu);
+                    if (c == 2)                                // flags (byte 47): PSH of any member
+                        x.w |= (u32)psh << 24;
+                }
+                v[j] = x;
+            }
+#pragma unroll
+            for (int j = 0; j < U; j++)
+                accum_chunk<true>(v[j], 16 * (base + j * G + sub), ts, te, a);
+#pragma unroll
+            for (int j = 0; j < U; j++) {
+                const int c = base + j * G + sub;
+                const int cb = 16 * c;
+                if (c < 8 || c >= nchunks)
+                    continue;
+                if (cb + 16 <= wlim) {
+                    stg16<WM_SECTOR>(m + cb, v[j]);
+                } else {
+                    for (int k = 0; k < 16 && cb + k < te && cb + k < wlim; k++)
+                        m[cb + k] = (uint8_t)chunk_byte(v[j], k);
+                }
+            }
+            if (base == 0) {
+#pragma unroll
+                for (int j = 0; j < U; j++)
+                    first[j] = v[j];
+            }
+        }
+        Hdr h;
+        h.d3 = group_bcast<G, 0>(first[0].w);
+        h.d4 = group_bcast<G, 1>(first[0].x);
+        h.d5 = group_bcast<G, 1>(first[0].y);
+        epilogue<G, U, true, WM_LINE_SC1>(h, a, m, mlen, wlim, true, sub, 0u, nullptr, nullptr,
+                                          true, first);
+    }
+}
+
 // TCPCalcChecksum(buf + off[i], len[i], saddr[i], daddr[i]), G lanes per item;
 // PSEUDO = false: ICMPChecksum(buf + off[i], len[i]) (icmp.c:18-42), the same
 // word loop and odd-byte rule without the pseudo header.
@@ -673,6 +934,17 @@ hipError_t launch_copy_fill(uint8_t* frames, uint64_t frames_bytes, const uint64
     constexpr int G = 32, U = 3, FPB = kBlock / G;
     hipLaunchKernelGGL((k_copy_fill<G, U>), dim3((n + FPB - 1) / FPB), dim3(kBlock), 0, s, frames,
                        frames_bytes, off, len, src, src_bytes, src_off, n, status, csums, flags);
+    return hipGetLastError();
+}
+
+hipError_t launch_gro(const uint8_t* in, uint64_t in_bytes, const uint64_t* off,
+                      const uint16_t* len, const uint8_t* verdict, u32 n, u32 window,
+                      u32 max_len, uint8_t* out, uint64_t out_bytes, uint64_t* out_off,
+                      uint16_t* out_len, uint32_t* head, hipStream_t s)
+{
+    hipLaunchKernelGGL((k_gro<2>), dim3((n + window - 1) / window), dim3(kBlock), 0, s, in,
+                       in_bytes, off, len, verdict, n, window, max_len, out, out_bytes, out_off,
+                       out_len, head);
     return hipGetLastError();
 }
 

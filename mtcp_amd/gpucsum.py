@@ -77,6 +77,8 @@ def lib() -> C.CDLL:
             "gcs_verify_ptrs": (i, [vp, vp, vp, u32, vp, u32]),
             "gcs_compute_ptrs": (i, [vp, vp, vp, u32, vp, vp]),
             "gcs_icmp_checksum_dev": (i, [vp, vp, u64, vp, vp, u32, vp, vp]),
+            "gcs_gro_dev": (i, [vp, vp, u64, vp, vp, vp, u32, u32, u32, vp, u64, vp, vp, vp,
+                                vp]),
             "gcs_compute_copy_dev": (i, [vp, vp, u64, vp, vp, vp, u64, vp, u32, vp, vp, u32,
                                          vp]),
             "gcs_ctx_set_rss": (i, [vp, vp, u32, u32, i]),
@@ -250,6 +252,18 @@ class Context:
         check(self.L.gcs_compute_copy_dev(self.h, _daddr(frames), fb, _daddr(off), _daddr(lens),
                                           _daddr(src), sb, _daddr(src_off), n, _daddr(status),
                                           _daddr(csums), flags, stream), "compute_copy")
+
+    def gro(self, frames, off, lens, verdict, n, window, max_len, out, out_off, out_len, head,
+            stream=None, in_bytes=None, out_bytes=None):
+        ib = _nbytes(frames) if in_bytes is None else in_bytes
+        ob = _nbytes(out) if out_bytes is None else out_bytes
+        self._need(frames, ib, "frames")
+        self._need(out, ob, "out")
+        for a, w in ((off, 8), (lens, 2), (verdict, 1), (out_off, 8), (out_len, 2), (head, 4)):
+            self._need(a, w * n, "array")
+        check(self.L.gcs_gro_dev(self.h, _daddr(frames), ib, _daddr(off), _daddr(lens),
+                                 _daddr(verdict), n, window, max_len, _daddr(out), ob,
+                                 _daddr(out_off), _daddr(out_len), _daddr(head), stream), "gro")
 
     def icmp_checksum(self, buf, off, lens, n, out, stream=None, buf_bytes=None):
         bb = _nbytes(buf) if buf_bytes is None else buf_bytes

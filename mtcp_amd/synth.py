@@ -201,3 +201,55 @@ def to_icmp(buf: np.ndarray, off: np.ndarray, lengths: np.ndarray, which: np.nda
         ts = o + ETH_LEN + 4 * ihl
         buf[o + 23] = 1
         buf[ts], buf[ts + 1] = 8, 0
+
+
+def tcp_streams(n: int, n_flows: int = 8, run_mean: float = 6.0, payload_max: int = 1448,
+                seed: int = DEFAULT_SEED) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """A received burst of ``n`` TCP data segments from ``n_flows`` flows, in
+    bursts of consecutive in-order segments per flow (geometric run lengths of
+    mean ``run_mean``), the way an LRO / GRO engine sees them.  Each flow has
+    fixed addresses, ports, ack, window and timestamp option; sequence numbers
+    and IP ids continue from segment to segment.  The last segment of a run
+    sometimes carries PSH.  Packed like ``packed_frames``; check fields 0."""
+    rng = np.random.default_rng(seed)
+    flows = []
+    for _ in range(n_flows):
+        flows.append(dict(sip=rng.integers(0, 256, 4, dtype=np.uint8),
+                          dip=rng.integers(0, 256, 4, dtype=np.uint8),
+                          sp=int(rng.integers(1024, 65536)), dp=int(rng.integers(1, 1024)),
+                          seq=int(rng.integers(0, 1 << 32)), ack=int(rng.integers(0, 1 << 32)),
+                          win=int(rng.integers(1, 65536)), ipid=int(rng.integers(0, 65536)),
+                          ts=rng.integers(0, 256, 8, dtype=np.uint8)))
+    segs = []
+    while len(segs) < n:
+        fl = flows[int(rng.integers(0, n_flows))]
+        run = min(int(rng.geometric(1.0 / run_mean)), n - len(segs))
+        for k in range(run):
+            pl = payload_max if rng.random() < 0.7 else int(rng.integers(1, payload_max + 1))
+            psh = k == run - 1 and rng.random() < 0.3
+            segs.append((fl, pl, psh, fl["seq"], fl["ipid"]))
+            fl["seq"] = (fl["seq"] + pl) & 0xFFFFFFFF
+            fl["ipid"] = (fl["ipid"] + 1) & 0xFFFF
+    lens = np.array([14 + 20 + 32 + s[1] for s in segs], dtype=np.uint16)
+    off, total = packed_offsets(lens)
+    buf = rng.integers(0, 256, size=total + 64, dtype=np.uint8)
+    for i, (fl, pl, psh, seq, ipid) in enumerate(segs):
+        o = int(off[i])
+        f = buf[o:o + int(lens[i])]
+        f[12], f[13], f[14], f[15] = 0x08, 0x00, 0x45, 0
+        tot = int(lens[i]) - 14
+        f[16], f[17] = tot >> 8, tot & 0xFF
+        f[18], f[19] = ipid >> 8, ipid & 0xFF
+        f[20], f[21], f[22], f[23] = 0x40, 0, 64, 6
+        f[24] = f[25] = 0
+        f[26:30] = fl["sip"]
+        f[30:34] = fl["dip"]
+        f[34], f[35], f[36], f[37] = fl["sp"] >> 8, fl["sp"] & 0xFF, fl["dp"] >> 8, fl["dp"] & 0xFF
+        f[38:42] = np.frombuffer(seq.to_bytes(4, "big"), dtype=np.uint8)
+        f[42:46] = np.frombuffer(fl["ack"].to_bytes(4, "big"), dtype=np.uint8)
+        f[46], f[47] = 8 << 4, 0x18 if psh else 0x10
+        f[48], f[49] = fl["win"] >> 8, fl["win"] & 0xFF
+        f[50] = f[51] = f[52] = f[53] = 0
+        f[54], f[55], f[56], f[57] = 1, 1, 8, 10
+        f[58:66] = fl["ts"]
+    return buf, off, lens

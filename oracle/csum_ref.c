@@ -8,6 +8,7 @@
 #include "csum_ref.h"
 
 #include <pthread.h>
+#include <stdlib.h>
 #include <string.h>
 
 /* Little-endian loads from any alignment (the reference dereferences
@@ -339,6 +340,113 @@ void ref_compute_copy_batch(uint8_t *buf, uint64_t buf_bytes, const uint64_t *of
 		}
 		if (status)
 			status[i] = (uint8_t)s;
+	}
+}
+
+/* ---- software LRO (see csum_ref.h) --------------------------------------- */
+
+static uint32_t be16(const uint8_t *p) { return ((uint32_t)p[0] << 8) | p[1]; }
+static uint32_t be32(const uint8_t *p)
+{
+	return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+/* TCP payload bytes of an ACCEPT frame with ihl == 5, else -1 */
+static int gro_payload(const uint8_t *f)
+{
+	uint32_t doff = f[46] >> 4, tot = be16(f + 16);
+	if ((f[14] & 0x0F) != 5)
+		return -1;
+	return (int)tot - 20 - 4 * (int)doff;
+}
+
+static int gro_continues(const uint8_t *p, const uint8_t *c)
+{
+	int pp = gro_payload(p), pc = gro_payload(c);
+	uint32_t doff = p[46] >> 4, k;
+	if (pp <= 0 || pc <= 0)
+		return 0;
+	if (p[15] != c[15] || be16(p + 20) != be16(c + 20) || (be16(p + 20) & 0x3FFF) ||
+	    p[22] != c[22] || memcmp(p + 26, c + 26, 8))
+		return 0;
+	if (be16(c + 18) != be16(p + 18) && be16(c + 18) != ((be16(p + 18) + 1) & 0xFFFF))
+		return 0;
+	if (memcmp(p + 34, c + 34, 4) || memcmp(p + 42, c + 42, 4) || c[46] != p[46] ||
+	    (p[46] & 0x0F) || be16(p + 48) != be16(c + 48) || be16(p + 52) || be16(c + 52))
+		return 0;
+	if (p[47] != 0x10 || (c[47] != 0x10 && c[47] != 0x18))
+		return 0;
+	for (k = 54; k < 34 + 4 * doff; k++)
+		if (p[k] != c[k])
+			return 0;
+	return be32(c + 38) == be32(p + 38) + (uint32_t)pp;
+}
+
+void ref_gro_batch(const uint8_t *buf, uint64_t buf_bytes, const uint64_t *off,
+                   const uint16_t *len, const uint8_t *verdict, uint32_t n,
+                   uint32_t window, uint32_t max_len, uint8_t *out, uint64_t out_bytes,
+                   uint64_t *out_off, uint16_t *out_len, uint32_t *head)
+{
+	uint32_t w0, i;
+	if (window == 0)
+		window = 1;
+	for (w0 = 0; w0 < n; w0 += window) {
+		uint32_t w1 = w0 + window < n ? w0 + window : n;
+		uint64_t o = off[w0];
+		i = w0;
+		while (i < w1) {
+			/* run [i, j) */
+			const uint8_t *h = buf + off[i];
+			uint32_t j = i + 1, mlen;
+			if (verdict[i] == REF_V_ACCEPT && (off[i] & 15) == 0 && off[i] <= buf_bytes &&
+			    len[i] <= buf_bytes - off[i] && gro_payload(h) > 0) {
+				uint32_t hl = 34 + 4 * (h[46] >> 4);
+				mlen = hl + (uint32_t)gro_payload(h);
+				while (j < w1 && verdict[j] == REF_V_ACCEPT && (off[j] & 15) == 0 &&
+				       off[j] <= buf_bytes && len[j] <= buf_bytes - off[j] &&
+				       gro_continues(buf + off[j - 1], buf + off[j]) &&
+				       mlen + (uint32_t)gro_payload(buf + off[j]) <= max_len) {
+					mlen += (uint32_t)gro_payload(buf + off[j]);
+					j++;
+				}
+			}
+			head[i] = i;
+			out_off[i] = o;
+			if (j == i + 1) {
+				/* a single frame: copied as it is (a bad descriptor: nothing) */
+				int ok = (off[i] & 15) == 0 && off[i] <= buf_bytes &&
+				         len[i] <= buf_bytes - off[i];
+				out_len[i] = ok ? len[i] : 0;
+				if (ok && o < out_bytes)
+					memcpy(out + o, h, o + len[i] <= out_bytes ? len[i] : out_bytes - o);
+			} else {
+				uint32_t hl = 34 + 4 * (h[46] >> 4), k, pos = hl, psh = 0;
+				uint8_t *m = (uint8_t *)malloc(mlen);
+				out_len[i] = (uint16_t)mlen;
+				memcpy(m, h, hl);
+				for (k = i; k < j; k++) {
+					const uint8_t *f = buf + off[k];
+					uint32_t pl = (uint32_t)gro_payload(f);
+					memcpy(m + pos, f + hl, pl);
+					pos += pl;
+					psh |= f[47] & 0x08;
+					if (k > i) {
+						head[k] = i;
+						out_off[k] = o;
+						out_len[k] = 0;
+					}
+				}
+				m[16] = (uint8_t)((mlen - 14) >> 8);
+				m[17] = (uint8_t)(mlen - 14);
+				m[47] |= (uint8_t)psh;
+				ref_tx_fill(m, mlen, NULL);
+				if (o < out_bytes)
+					memcpy(out + o, m, o + mlen <= out_bytes ? mlen : out_bytes - o);
+				free(m);
+			}
+			o += (out_len[i] + 15u) & ~15ull;
+			i = j;
+		}
 	}
 }
 

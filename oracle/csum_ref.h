@@ -17,6 +17,7 @@
  *   ref_tx_fill            mtcp/src/ip_out.c:143-173, tcp_out.c:244,323-333
  *                          (TX: check fields zero when folded, then stored)
  *   ref_tx_copy_fill       mtcp/src/tcp_out.c:316-333    (payload memcpy + fill)
+ *   ref_gro_batch          software LRO merge (rules: this project's, see below)
  *   ref_icmp_checksum      mtcp/src/icmp.c:18-42         (ICMPChecksum, static)
  *   ref_rss_hash/_core     mtcp/src/rss.c:13-41,44-86,97-115 (BuildKeyCache,
  *                          GetRSSHash, GetRSSCPUCore)
@@ -105,6 +106,33 @@ void ref_compute_copy_batch(uint8_t *buf, uint64_t buf_bytes, const uint64_t *of
                             const uint16_t *len, uint32_t n, const uint8_t *src,
                             uint64_t src_bytes, const uint64_t *src_off, uint8_t *status,
                             uint32_t *csums);
+
+/* Receive-side segment merge ("software LRO"): the job a
+ * NIC's LRO does for mTCP's ENABLELRO builds (dpdk_module.c:44-48, 855-881;
+ * tcp_ring_buffer.c:15-21), done on the host-independent frame batch.  The
+ * reference has no software merge, so the RULES are this project's (they are
+ * Linux GRO's tcp4_gro_receive conditions); what is pinned to the reference is
+ * that every merged frame passes its own RX checks (refx_rx_verdict) and
+ * carries exactly the concatenated payloads.
+ *
+ * Frames are taken in windows of `window` consecutive descriptors (a burst);
+ * inside a window, frame c continues frame p = c-1 when both are ACCEPT (the
+ * given verdicts), both have ihl == 5, equal tos / frag_off (no MF, offset 0)
+ * / ttl / saddr / daddr, c's IP id is p's or p's + 1, equal ports / ack /
+ * doff / window / TCP options, zero urgent pointers and reserved bits, p's
+ * flags are exactly ACK and c's ACK or ACK|PSH, both carry payload, and
+ * seq(c) == seq(p) + payload(p); and the run stays <= max_len bytes.
+ * A run of one frame is copied as it is; a longer run becomes one frame: the
+ * head's headers with tot_len = the merged length - 14 and PSH if any member
+ * has it, the members' payloads in order, and both checks refilled.  Output
+ * frames of a window are packed from that window's first input offset, each
+ * at a 16 B-aligned offset (inputs must be packed in increasing order, as a
+ * PSIO chunk or a staging area is).  head[i] = the run head of frame i;
+ * out_off / out_len are set for heads (out_len = 0 for merged members). */
+void ref_gro_batch(const uint8_t *buf, uint64_t buf_bytes, const uint64_t *off,
+                   const uint16_t *len, const uint8_t *verdict, uint32_t n,
+                   uint32_t window, uint32_t max_len, uint8_t *out, uint64_t out_bytes,
+                   uint64_t *out_off, uint16_t *out_len, uint32_t *head);
 
 /* ICMPChecksum(buf, len): LE 16-bit words, an odd final byte added as the
  * low byte of a zero-high-byte word, two-step fold, ~.  The C leaves the high

@@ -76,6 +76,9 @@ class Oracle:
         L.ref_compute_copy_batch.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
                                              C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p,
                                              C.c_void_p, C.c_void_p]
+        L.ref_gro_batch.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p,
+                                    C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64,
+                                    C.c_void_p, C.c_void_p, C.c_void_p]
         L.ref_rss_hash.restype = C.c_uint32
         L.ref_rss_hash.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint16, C.c_uint16]
         L.ref_rss_core.restype = C.c_int
@@ -150,6 +153,19 @@ class Oracle:
                                       src.nbytes, _p(np.ascontiguousarray(src_off, np.uint64)),
                                       _p(st), _p(cs))
         return st, cs
+
+    def gro_batch(self, buf, off, lens, verdict, window, max_len, out_bytes=None):
+        """-> (out buffer, out_off, out_len, head)"""
+        n = len(off)
+        out = np.zeros(buf.nbytes if out_bytes is None else out_bytes, dtype=np.uint8)
+        oo = np.zeros(n, dtype=np.uint64)
+        ol = np.zeros(n, dtype=np.uint16)
+        hd = np.zeros(n, dtype=np.uint32)
+        self.L.ref_gro_batch(_p(buf), buf.nbytes, _p(np.ascontiguousarray(off, np.uint64)),
+                             _p(np.ascontiguousarray(lens, np.uint16)),
+                             _p(np.ascontiguousarray(verdict, np.uint8)), n, window, max_len,
+                             _p(out), out.nbytes, _p(oo), _p(ol), _p(hd))
+        return out, oo, ol, hd
 
     def icmp_checksum_batch(self, buf, off, lens):
         n = len(off)

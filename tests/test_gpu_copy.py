@@ -127,7 +127,9 @@ def test_copy_fill_payload_edges(torch_dev, ctx, O, payload, doff):
 def test_copy_fill_bad_source_and_buffer_end(torch_dev, ctx, O):
     t = torch_dev
     n = 300
-    buf, off, lens, src, src_off = segments(n, 77)
+    lens = synth.imix_lengths(n, seed=77)
+    lens[-1] = 1501                                    # ends the buffer off a 16 B boundary
+    buf, off, lens, src, src_off = segments(n, 77, lens=lens)
     src_off[::7] = len(src) - 3                        # payload would run past the source
     src_off[1::13] = len(src) + 5                      # offset past the source
     # the last frame ends exactly at frames_bytes, which is not 16 B-aligned

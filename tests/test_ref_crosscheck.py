@@ -152,3 +152,16 @@ def test_copy_fill_is_memcpy_then_reference_fill(both):
         s, c = R.tx_fill_at(b, o, L)
         assert (s, c) == (st[i], cs[i])
     np.testing.assert_array_equal(a, b)
+
+
+def test_lro_merged_frames_pass_reference_rx(both):
+    """Software LRO: every merged frame passes the reference's own RX checks."""
+    O, R = both
+    buf, off, lens = synth.tcp_streams(4000, seed=21)
+    O.compute_batch(buf, off, lens)
+    vd = O.verify_batch(buf.copy(), off, lens)
+    out, oo, ol, hd = O.gro_batch(buf, off, lens, vd, 64, 16384)
+    heads = np.nonzero(hd == np.arange(len(off)))[0]
+    assert len(heads) < len(off) // 3
+    for h in heads:
+        assert R.rx_verdict_at(out, int(oo[h]), int(ol[h])) == 0

@@ -408,6 +408,94 @@ int copy_main(uint64_t n, int rounds)
     return 0;
 }
 
+// Software LRO: 1500 B segments of 16 flows arriving in
+// runs of 8 in-order segments per flow; merge windows of 64 frames.
+__global__ void k_stream_hdr(uint8_t* buf, uint64_t n, uint64_t stride, uint32_t L)
+{
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint8_t* f = buf + i * stride;
+    const uint32_t fl = (uint32_t)((i / 8) % 16), sgi = (uint32_t)((i / 128) * 8 + i % 8);
+    const uint32_t tot = L - 14, pl = L - 66, seq = fl * 1000003u + sgi * pl, id = sgi & 0xFFFF;
+    f[12] = 8; f[13] = 0; f[14] = 0x45; f[15] = 0; f[16] = tot >> 8; f[17] = tot & 255;
+    f[18] = id >> 8; f[19] = id & 255;
+    f[20] = 0x40; f[21] = 0; f[22] = 64; f[23] = 6; f[24] = f[25] = 0;
+    f[26] = 10; f[27] = 0; f[28] = 0; f[29] = (uint8_t)fl; f[30] = 10; f[31] = 0; f[32] = 1; f[33] = 1;
+    f[34] = 0x80; f[35] = (uint8_t)fl; f[36] = 0; f[37] = 80;
+    f[38] = seq >> 24; f[39] = seq >> 16; f[40] = seq >> 8; f[41] = seq;
+    f[42] = 1; f[43] = 2; f[44] = 3; f[45] = 4; f[46] = 8 << 4; f[47] = 0x10;
+    f[48] = 0x10; f[49] = 0; f[50] = f[51] = f[52] = f[53] = 0;
+    f[54] = 1; f[55] = 1; f[56] = 8; f[57] = 10;
+    for (int k = 58; k < 66; k++) f[k] = (uint8_t)(fl + k);
+}
+
+int lro_main(uint64_t n, int rounds)
+{
+    const uint32_t L = 1500;
+    const uint64_t stride = 1536;
+    uint8_t *in, *out, *vd;
+    uint64_t *off, *soff, *oo;
+    uint16_t *lens, *ol;
+    uint32_t* hd;
+    CK(hipMalloc(&in, n * stride));
+    CK(hipMalloc(&out, n * stride));
+    CK(hipMalloc(&vd, n));
+    CK(hipMalloc(&off, 8 * n));
+    CK(hipMalloc(&soff, 8 * n));
+    CK(hipMalloc(&oo, 8 * n));
+    CK(hipMalloc(&lens, 2 * n));
+    CK(hipMalloc(&ol, 2 * n));
+    CK(hipMalloc(&hd, 4 * n));
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    hipLaunchKernelGGL(k_init, dim3(4096), dim3(256), 0, s, in, n, stride, L);
+    hipLaunchKernelGGL(k_stream_hdr, dim3((n + 255) / 256), dim3(256), 0, s, in, n, stride, L);
+    hipLaunchKernelGGL(k_seq_off, dim3((n + 255) / 256), dim3(256), 0, s, off, soff, lens, n,
+                       stride, L, 0u);
+    CK(launch_compute_desc(in, n * stride, off, lens, (u32)n, nullptr, nullptr, 0u, s));
+    CK(launch_verify_desc(in, n * stride, off, lens, (u32)n, vd, 0u, s));
+    CK(hipStreamSynchronize(s));
+    std::printf("LRO: n %llu x %u B segments, 16 flows in runs of 8, windows of 64\n",
+                (unsigned long long)n, L);
+    const double bytes = 2.0 * n * L;                   // read each frame, write it merged
+    std::vector<Variant> vs;
+    vs.push_back({"gro (launch_gro, window 64, max 16384)", bytes, [&](hipStream_t st) {
+        CK(launch_gro(in, n * stride, off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol,
+                      hd, st));
+    }});
+    vs.push_back({"verify (launch_verify_desc) for scale", (double)n * (L + 1), [&](hipStream_t st) {
+        CK(launch_verify_desc(in, n * stride, off, lens, (u32)n, vd, 0u, st));
+    }});
+    vs.push_back({"D2D copy of the batch for scale", 2.0 * n * stride, [&](hipStream_t st) {
+        CK(hipMemcpyAsync(out, in, n * stride, hipMemcpyDeviceToDevice, st));
+    }});
+    run_variants(vs, s, rounds);
+    CK(launch_gro(in, n * stride, off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd,
+                  s));
+    std::vector<uint16_t> hl(n);
+    std::vector<uint64_t> ho(n);
+    CK(hipMemcpy(hl.data(), ol, 2 * n, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(ho.data(), oo, 8 * n, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> mo;
+    std::vector<uint16_t> ml;
+    for (uint64_t i = 0; i < n; i++)
+        if (hl[i]) { mo.push_back(ho[i]); ml.push_back(hl[i]); }
+    uint64_t *dmo;
+    uint16_t* dml;
+    CK(hipMalloc(&dmo, 8 * mo.size()));
+    CK(hipMalloc(&dml, 2 * ml.size()));
+    CK(hipMemcpy(dmo, mo.data(), 8 * mo.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(dml, ml.data(), 2 * ml.size(), hipMemcpyHostToDevice));
+    CK(launch_verify_desc(out, n * stride, dmo, dml, (u32)mo.size(), vd, 0u, s));
+    std::vector<uint8_t> hv(mo.size());
+    CK(hipMemcpy(hv.data(), vd, mo.size(), hipMemcpyDeviceToHost));
+    size_t bad = 0;
+    for (auto b : hv) bad += b != 0;
+    std::printf("merged frames %zu (mean %.2f segments), failing verify: %zu (expect 0)\n",
+                mo.size(), (double)n / mo.size(), bad);
+    return 0;
+}
+
 void run_variants(std::vector<Variant>& vs, hipStream_t s, int rounds)
 {
     hipEvent_t e0, e1;
@@ -445,6 +533,9 @@ int main(int argc, char** argv)
     if (argc > 1 && std::string(argv[1]) == "copy")
         return copy_main(argc > 2 ? std::strtoull(argv[2], nullptr, 10) : (1u << 20),
                          argc > 3 ? std::atoi(argv[3]) : 15);
+    if (argc > 1 && std::string(argv[1]) == "lro")
+        return lro_main(argc > 2 ? std::strtoull(argv[2], nullptr, 10) : (1u << 20),
+                        argc > 3 ? std::atoi(argv[3]) : 15);
     if (argc > 1 && std::string(argv[1]) == "ext")
         return ext_main(argc > 2 ? std::atoi(argv[2]) : 1500,
                         argc > 3 ? std::strtoull(argv[3], nullptr, 10) : (1u << 20),
