@@ -321,6 +321,46 @@ __device__ __forceinline__ u32 chunk_byte(const uint4& v, int k)
     return (pick(v, k >> 2) >> (8 * (k & 3))) & 0xFFu;
 }
 
+// Chunk byte j of the result = byte j - k of v (0 below k), k in [0, 16].
+__device__ __forceinline__ uint4 bytes_up(uint4 v, int k)
+{
+    const uint64_t lo = v.x | ((uint64_t)v.y << 32), hi = v.z | ((uint64_t)v.w << 32);
+    const int sh = 8 * k;
+    uint64_t nlo, nhi;
+    if (sh == 0) {
+        nlo = lo;
+        nhi = hi;
+    } else if (sh < 64) {
+        nlo = lo << sh;
+        nhi = (hi << sh) | (lo >> (64 - sh));
+    } else if (sh < 128) {
+        nlo = 0;
+        nhi = lo << (sh - 64);
+    } else {
+        nlo = nhi = 0;
+    }
+    return make_uint4((u32)nlo, (u32)(nlo >> 32), (u32)nhi, (u32)(nhi >> 32));
+}
+
+// Bytes [a, b) of a chunk set, 0 <= a <= b <= 16.
+__device__ __forceinline__ uint4 byte_mask(int a, int b)
+{
+    return make_uint4(low_mask(b) & ~low_mask(a), low_mask(b - 4) & ~low_mask(a - 4),
+                      low_mask(b - 8) & ~low_mask(a - 8), low_mask(b - 12) & ~low_mask(a - 12));
+}
+
+// x where m is clear, y where it is set
+__device__ __forceinline__ uint4 blend(uint4 x, uint4 y, uint4 m)
+{
+    return make_uint4((x.x & ~m.x) | (y.x & m.x), (x.y & ~m.y) | (y.y & m.y),
+                      (x.z & ~m.z) | (y.z & m.z), (x.w & ~m.w) | (y.w & m.w));
+}
+
+// Chunk assembly plans (k_copy_fill, k_gro): which loads a destination chunk
+// needs and how they combine.  All loads of a batch are issued before any is
+// consumed, so a wave waits once per batch.
+enum { AS_ZERO = 0, AS_FRAME, AS_ONE, AS_UP, AS_TAIL, AS_TWO, AS_BYTES };
+
 template <int G, int U>
 __global__ void __launch_bounds__(kBlock)
 k_copy_fill(uint8_t* __restrict__ frames, uint64_t frames_bytes,
@@ -376,34 +416,64 @@ k_copy_fill(uint8_t* __restrict__ frames, uint64_t frames_bytes,
 
     Acc a = {0u, 0u, 0u};
     uint4 first[U];
+    // payload loads must stay inside the source buffer: `src_room` bytes from ps
+    const int64_t src_room = copy ? (int64_t)(src_bytes - po) : 0;
     for (int base = 0; base < nchunks; base += G * U) {   // group-uniform
-        uint4 v[U];
+        uint4 v[U], fr[U], pv[U];
+        int plan[U];
+        // 1: issue the loads of every chunk of the batch
 #pragma unroll
         for (int j = 0; j < U; j++) {
             const int c = base + j * G + sub;
             const int cb = 16 * c;
-            uint4 x = z;
+            int pl = AS_ZERO;
+            fr[j] = z;
+            pv[j] = z;
             if (c < nchunks) {
-                const bool frame_bytes = !copy || cb < hl || cb + 16 > te;
-                uint4 fr = z;
-                if (base == 0 && j == 0)
-                    fr = hv;
-                else if (frame_bytes)
-                    fr = load_chunk<true, false>(f + cb, avail - cb);
                 if (!copy || cb + 16 <= hl || cb >= te) {
-                    x = fr;                                  // header / past the segment
+                    pl = AS_FRAME;                           // header / past the segment
                 } else if (cb >= hl && cb + 16 <= te) {
-                    x = ldg16u(ps + (cb - hl));              // payload
-                } else {                                     // straddles hl or te
-                    u32 w[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-                    for (int k = 0; k < 16; k++) {
-                        const int p = cb + k;
-                        const u32 b = (p >= hl && p < te) ? (u32)ps[p - hl] : chunk_byte(fr, k);
-                        w[k >> 2] |= b << (8 * (k & 3));
-                    }
-                    x = make_uint4(w[0], w[1], w[2], w[3]);
+                    pl = AS_ONE;                             // payload only
+                    pv[j] = ldg16u(ps + (cb - hl));
+                } else if (cb < hl && cb + 16 <= te && src_room >= 16) {
+                    pl = AS_UP;                              // headers, then the payload start
+                    pv[j] = ldg16u(ps);
+                } else if (cb >= hl && src_room >= (int64_t)(cb - hl) + 16) {
+                    pl = AS_TAIL;                            // the payload end, then frame bytes
+                    pv[j] = ldg16u(ps + (cb - hl));
+                } else {
+                    pl = AS_BYTES;                           // tiny payload / source end
                 }
+                if (pl != AS_ONE) {
+                    if (base == 0 && j == 0)
+                        fr[j] = hv;
+                    else
+                        fr[j] = load_chunk<true, false>(f + cb, avail - cb);
+                }
+            }
+            plan[j] = pl;
+        }
+        // 2: assemble
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            const int cb = 16 * (base + j * G + sub);
+            uint4 x = z;
+            switch (plan[j]) {
+            case AS_FRAME: x = fr[j]; break;
+            case AS_ONE: x = pv[j]; break;
+            case AS_UP: x = blend(fr[j], bytes_up(pv[j], hl - cb), byte_mask(hl - cb, 16)); break;
+            case AS_TAIL: x = blend(fr[j], pv[j], byte_mask(0, te - cb)); break;
+            case AS_BYTES: {
+                u32 w[4] = {0u, 0u, 0u, 0u};
+                for (int k = 0; k < 16; k++) {
+                    const int p = cb + k;
+                    const u32 b = (p >= hl && p < te) ? (u32)ps[p - hl] : chunk_byte(fr[j], k);
+                    w[k >> 2] |= b << (8 * (k & 3));
+                }
+                x = make_uint4(w[0], w[1], w[2], w[3]);
+                break;
+            }
+            default: break;
             }
             v[j] = x;
         }
@@ -501,7 +571,7 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
 {
     static_assert(kBlock == kGroW, "one frame per thread");
     constexpr int G = 64;
-    __shared__ uint8_t hdr[kGroW][kGroHdr];
+    __shared__ __attribute__((aligned(16))) uint8_t hdr[kGroW][kGroHdr];
     __shared__ int pay[kGroW];         // TCP payload bytes of a mergeable frame, else -1
     __shared__ uint8_t cont[kGroW];
     __shared__ uint8_t dok[kGroW];     // descriptor inside the input buffer
@@ -620,51 +690,104 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
         const int ts = 34, te = (int)mlen;
         Acc a = {0u, 0u, 0u};
         uint4 first[U];
+        const uint8_t* in_end = in + in_bytes;
         for (int base = 0; base < nchunks; base += G * U) {
-            uint4 v[U];
+            uint4 v[U], pa[U], pb[U];
+            int plan[U], cut[U];
+            // 1: issue the loads of every chunk of the batch
+#pragma unroll
+            for (int j = 0; j < U; j++) {
+                const int c = base + j * G + sub;
+                const int cb = 16 * c;
+                int pl = AS_ZERO, ct = 0, sg = k0;
+                pa[j] = z;
+                pb[j] = z;
+                if (c < nchunks && cb + 16 <= hl) {
+                    pl = AS_FRAME;                                 // head's headers (LDS)
+                } else if (c < nchunks && cb < hl) {
+                    const uint8_t* p0 = in + off[w0 + k0] + hl;
+                    ct = hl - cb;                                  // header bytes in the chunk
+                    if (cb + 16 <= te && pay[k0] >= 16 - ct && p0 + 16 <= in_end) {
+                        pl = AS_UP;
+                        pa[j] = ldg16u(p0);
+                    } else {
+                        pl = AS_BYTES;
+                    }
+                } else if (c < nchunks) {
+                    const u32 q = (u32)(cb - hl);                  // merged payload offset
+                    int lo2 = k0, hi2 = k0 + nm - 1;
+                    while (lo2 < hi2) {
+                        const int mid = (lo2 + hi2 + 1) >> 1;
+                        if (pref[mid] <= q) lo2 = mid; else hi2 = mid - 1;
+                    }
+                    sg = lo2;
+                    const int rem = (int)(pref[sg] + (u32)pay[sg] - q);   // bytes left in sg
+                    const int need = min(16, te - cb);
+                    const uint8_t* pq = in + off[w0 + sg] + hl + (q - pref[sg]);
+                    if (rem >= need && pq + 16 <= in_end) {
+                        pl = AS_ONE;                               // one member (masked at te)
+                        pa[j] = ldg16u(pq);
+                    } else if (sg + 1 < k0 + nm && pay[sg + 1] >= need - rem &&
+                               pq + 16 <= in_end && in + off[w0 + sg + 1] + hl + 16 <= in_end) {
+                        pl = AS_TWO;                               // the end of sg, then sg+1
+                        ct = rem;
+                        pa[j] = ldg16u(pq);
+                        pb[j] = ldg16u(in + off[w0 + sg + 1] + hl);
+                    } else {
+                        pl = AS_BYTES;
+                    }
+                }
+                plan[j] = pl;
+                cut[j] = ct;
+            }
+            // 2: assemble
 #pragma unroll
             for (int j = 0; j < U; j++) {
                 const int c = base + j * G + sub;
                 const int cb = 16 * c;
                 uint4 x = z;
-                if (c < nchunks) {
-                    // payload member holding merged byte cb (binary search on pref)
-                    int sg = k0;
-                    if (cb >= hl) {
-                        int lo2 = k0, hi2 = k0 + nm - 1;
-                        const u32 q = (u32)(cb - hl);
-                        while (lo2 < hi2) {
-                            const int mid = (lo2 + hi2 + 1) >> 1;
-                            if (pref[mid] <= q) lo2 = mid; else hi2 = mid - 1;
+                switch (plan[j]) {
+                case AS_FRAME:
+                    x = *reinterpret_cast<const uint4*>(&hh[cb]);
+                    break;
+                case AS_UP:
+                    x = blend(*reinterpret_cast<const uint4*>(&hh[cb]), bytes_up(pa[j], cut[j]),
+                              byte_mask(cut[j], 16));
+                    break;
+                case AS_ONE:
+                    x = pa[j];
+                    break;
+                case AS_TWO:
+                    x = blend(pa[j], bytes_up(pb[j], cut[j]), byte_mask(cut[j], 16));
+                    break;
+                case AS_BYTES: {
+                    u32 w[4] = {0u, 0u, 0u, 0u};
+                    int s2 = k0;
+                    for (int k = 0; k < 16; k++) {
+                        const int p = cb + k;
+                        u32 b = 0;
+                        if (p < hl) {
+                            b = hh[p];
+                        } else if (p < te) {
+                            const u32 qq = (u32)(p - hl);
+                            while (qq >= pref[s2] + (u32)pay[s2])
+                                s2++;
+                            b = in[off[w0 + s2] + hl + (qq - pref[s2])];
                         }
-                        sg = lo2;
+                        w[k >> 2] |= b << (8 * (k & 3));
                     }
-                    const u32 q = (u32)(cb - hl);
-                    if (cb >= hl && cb + 16 <= te && q + 16 <= pref[sg] + (u32)pay[sg]) {
-                        x = ldg16u(in + off[w0 + sg] + hl + (q - pref[sg]));
-                    } else {
-                        u32 w[4] = {0u, 0u, 0u, 0u};
-                        int s2 = sg;
-                        for (int k = 0; k < 16; k++) {
-                            const int p = cb + k;
-                            u32 b = 0;
-                            if (p < hl) {
-                                b = p < kGroHdr ? hh[p] : 0u;
-                            } else if (p < te) {
-                                const u32 qq = (u32)(p - hl);
-                                while (qq >= pref[s2] + (u32)pay[s2])
-                                    s2++;
-                                b = in[off[w0 + s2] + hl + (qq - pref[s2])];
-                            }
-                            w[k >> 2] |= b << (8 * (k & 3));
-                        }
-                        x = make_uint4(w[0], w[1], w[2], w[3]);
-                    }
-                    if (c == 1)                                // tot_len (bytes 16-17)
-                        x.x = (x.x & 0xFFFF0000u) | bswap16((mlen - 14) & 0xFFFFu);
-                    if (c == 2)                                // flags (byte 47): PSH of any member
-                        x.w |= (u32)psh << 24;
+                    x = make_uint4(w[0], w[1], w[2], w[3]);
+                    break;
                 }
+                default:
+                    break;
+                }
+                if (c < nchunks && cb + 16 > te)                    // nothing past the frame
+                    x = blend(z, x, byte_mask(0, te - cb));
+                if (c == 1)                                        // tot_len (bytes 16-17)
+                    x.x = (x.x & 0xFFFF0000u) | bswap16((mlen - 14) & 0xFFFFu);
+                if (c == 2)                                        // flags (byte 47): PSH of any member
+                    x.w |= (u32)psh << 24;
                 v[j] = x;
             }
 #pragma unroll
