@@ -51,7 +51,7 @@ def parse():
                         "the HBM/GPU clocks take ~10 ms of load to reach steady state "
                         "(DESIGN.md §5); reported in the JSON line")
     p.add_argument("--no-extras", action="store_true",
-                   help="skip the 64 B (C1) and PCIe-inclusive side measurements")
+                   help="skip the side measurements (C1, C3, SURVEY 8f rows, PCIe-inclusive)")
     return p.parse_args()
 
 
@@ -222,6 +222,107 @@ def c1_small_frames(ctx, torch, steps=20):
             "hbm_gbs_algorithmic": n * (L + 1) / (ms * 1e-3) / 1e9}
 
 
+def _launch_ms(torch, fn, reps=10, warm=3):
+    """Mean HIP-event time of `fn()` launched back to back on the current stream."""
+    for _ in range(warm):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def c3_imix(ctx, torch, n=4 << 20):
+    """C3 side measurement: 4M IMIX frames (64/576/1500 at 7:4:1, pslib 64 B
+    packing), descriptor batch in HBM, TX fill and RX verify per launch."""
+    from mtcp_amd import synth
+    lens = synth.imix_lengths(n, seed=0x494D)
+    buf, off, ln, total = synth.packed_frames_device(lens, seed=0x494D)
+    stream = torch.cuda.current_stream().cuda_stream
+    ctx.compute(buf, off, ln, n, stream=stream)
+    v = torch.empty(n, dtype=torch.uint8, device="cuda")
+    vms = _launch_ms(torch, lambda: ctx.verify(buf, off, ln, n, v, stream=stream))
+    cms = _launch_ms(torch, lambda: ctx.compute(buf, off, ln, n, stream=stream))
+    assert int((v != 0).sum()) == 0
+    nbytes = int(lens.astype(np.int64).sum())
+    return {"workload": f"C3: {n} IMIX frames (mean {nbytes / n:.1f} B), {total / 1e9:.2f} GB "
+                        "packed at 64 B, descriptor batch",
+            "verify_ms": vms, "compute_ms": cms,
+            "verify_gpkt_per_s": n / vms / 1e6, "compute_gpkt_per_s": n / cms / 1e6,
+            "verify_hbm_gbs_algorithmic": (nbytes + n * 11) / (vms * 1e-3) / 1e9,
+            "compute_hbm_gbs_algorithmic": (nbytes + n * 14) / (cms * 1e-3) / 1e9}
+
+
+def rows_8f(ctx, torch, n=1 << 20, L=1500):
+    """SURVEY §8f rows 2-4 on C2-shaped data (1M x 1500 B), per launch:
+    ICMP flag on TCP traffic, classify (verify + RSS), TX payload copy + fill,
+    software LRO.  Each checked for its expected outcome."""
+    from mtcp_amd import synth
+    stream = torch.cuda.current_stream().cuda_stream
+    buf, stride = synth.fixed_frames_device(n, L, seed=0x8F)
+    ctx.compute_fixed(buf, stride, L, n, stream=stream)
+    v = torch.empty(n, dtype=torch.uint8, device="cuda")
+    out = {}
+    ms = _launch_ms(torch, lambda: ctx.verify_fixed(buf, stride, L, n, v, stream=stream))
+    out["verify_ms"] = ms
+    ms = _launch_ms(torch, lambda: ctx.verify_fixed(buf, stride, L, n, v,
+                                                    flags=gpucsum_K()["GCS_VF_ICMP"],
+                                                    stream=stream))
+    out["verify_icmp_flag_ms"] = ms
+    h = torch.empty(n, dtype=torch.int32, device="cuda")
+    q = torch.empty(n, dtype=torch.int16, device="cuda")
+    ctx.set_rss(None, 16, 0)
+    ms = _launch_ms(torch, lambda: ctx.classify_fixed(buf, stride, L, n, v, h, q, stream=stream))
+    ctx.set_rss(None, 1, 0)
+    assert int((v != 0).sum()) == 0 and int((q < 0).sum()) == 0 and int((q >= 16).sum()) == 0
+    out["classify_ms"] = ms
+    out["classify_gpkt_per_s"] = n / ms / 1e6
+    # copy + fill: payloads from a contiguous send buffer into the frames
+    pl = L - 66
+    src = torch.randint(0, 256, (n * pl + 64,), dtype=torch.uint8, device="cuda")
+    off = torch.arange(n, device="cuda", dtype=torch.int64) * stride
+    src_off = torch.arange(n, device="cuda", dtype=torch.int64) * pl
+    lens = torch.full((n,), L, dtype=torch.int16, device="cuda")
+    st = torch.empty(n, dtype=torch.uint8, device="cuda")
+    ms = _launch_ms(torch, lambda: ctx.compute_copy(buf, off, lens, src, src_off, n, st,
+                                                    stream=stream))
+    assert int((st != 0).sum()) == 0
+    ctx.verify_fixed(buf, stride, L, n, v, stream=stream)
+    torch.cuda.synchronize()
+    assert int((v != 0).sum()) == 0
+    out["copy_fill_ms"] = ms
+    out["copy_fill_gbs_algorithmic"] = n * (pl + 66 + L) / (ms * 1e-3) / 1e9
+    del src, buf
+    # software LRO: 16 flows in runs of 8, windows of 64
+    sb, stride = synth.tcp_streams_device(n, L)
+    off = torch.arange(n, device="cuda", dtype=torch.int64) * stride
+    ctx.compute(sb, off, lens, n, stream=stream)
+    ctx.verify(sb, off, lens, n, v, stream=stream)
+    o = torch.empty_like(sb)
+    oo = torch.empty(n, dtype=torch.int64, device="cuda")
+    ol = torch.empty(n, dtype=torch.int16, device="cuda")
+    hd = torch.empty(n, dtype=torch.int32, device="cuda")
+    ms = _launch_ms(torch, lambda: ctx.gro(sb, off, lens, v, n, 64, 16384, o, oo, ol, hd,
+                                           stream=stream))
+    heads = int((ol != 0).sum())
+    assert heads == n // 8
+    out["lro_ms"] = ms
+    out["lro_merged_frames"] = heads
+    out["lro_gbs_algorithmic"] = 2 * n * L / (ms * 1e-3) / 1e9
+    out["workload"] = (f"{n} x {L} B frames; RSS 16 queues; copy+fill {pl} B payloads from a "
+                       "contiguous send buffer; LRO 16 flows in runs of 8, windows of 64")
+    return out
+
+
+def gpucsum_K():
+    from mtcp_amd import gpucsum
+    return gpucsum.K
+
+
 def pcie_inclusive(gcs, torch, frame_len=1500, n=1 << 20):
     """Host-resident frames through the host entry points: gcs_verify (H2D of
     the frames, kernel, D2H of 1 B verdicts) and gcs_compute (H2D, kernel, D2H
@@ -338,6 +439,10 @@ def main():
             del tx, rx
             torch.cuda.empty_cache()
             line["c1_64B"] = c1_small_frames(ctx, torch)
+            line["c3_imix"] = c3_imix(ctx, torch)
+            torch.cuda.empty_cache()
+            line["rows_8f"] = rows_8f(ctx, torch)
+            torch.cuda.empty_cache()
             line["pcie_inclusive"] = pcie_inclusive(gpucsum, torch)
     ctx.close()
     if rank == 0:

@@ -253,3 +253,73 @@ def tcp_streams(n: int, n_flows: int = 8, run_mean: float = 6.0, payload_max: in
         f[54], f[55], f[56], f[57] = 1, 1, 8, 10
         f[58:66] = fl["ts"]
     return buf, off, lens
+
+
+def packed_frames_device(lengths: np.ndarray, seed: int = DEFAULT_SEED, device: str = "cuda"):
+    """``packed_frames`` generated in HBM with torch (C3 IMIX at 4M frames):
+    returns (uint8 buffer, off[int64 tensor], len[int16 tensor], total bytes).
+    Headers as ``fixed_frames_device`` per length (doff 5 below 66 B, else 8);
+    check fields 0."""
+    import torch
+
+    lengths = np.asarray(lengths, dtype=np.uint16)
+    assert (lengths >= 54).all()
+    off_np, total = packed_offsets(lengths)
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    buf = torch.randint(0, 256, (total + 64,), dtype=torch.uint8, device=device, generator=g)
+    off = torch.from_numpy(off_np.astype(np.int64)).to(device)
+    L = torch.from_numpy(lengths.astype(np.int64)).to(device)
+    tot = L - ETH_LEN
+    big = L >= 66
+    cols = {12: 0x08, 13: 0x00, 14: 0x45, 15: 0, 20: 0x40, 21: 0, 22: 64, 23: 6, 24: 0, 25: 0,
+            47: 0x10, 50: 0, 51: 0, 52: 0, 53: 0}
+    for c, v in cols.items():
+        buf[off + c] = v
+    buf[off + 16] = (tot >> 8).to(torch.uint8)
+    buf[off + 17] = (tot & 0xFF).to(torch.uint8)
+    buf[off + 46] = torch.where(big, 8 << 4, 5 << 4).to(torch.uint8)
+    ob = off[big]
+    for c, v in ((54, 1), (55, 1), (56, 8), (57, 10)):
+        buf[ob + c] = v
+    return buf, off, torch.from_numpy(lengths.view(np.int16)).to(device), total
+
+
+def tcp_streams_device(n: int, frame_len: int = 1500, flows: int = 16, run: int = 8,
+                       device: str = "cuda"):
+    """An LRO workload in HBM: ``n`` data segments of ``frame_len`` bytes (66 B
+    of headers with NOP,NOP,TS) at stride ``stride_for(frame_len)``, from
+    ``flows`` flows arriving in runs of ``run`` in-order segments each (frame
+    i: flow (i // run) % flows).  Sequence numbers and IP ids continue per
+    flow.  Returns (buffer, stride); check fields 0."""
+    import torch
+
+    stride = stride_for(frame_len)
+    buf = torch.randint(0, 256, (n * stride,), dtype=torch.uint8, device=device)
+    b = buf.view(n, stride)
+    i = torch.arange(n, device=device, dtype=torch.int64)
+    fl = (i // run) % flows
+    sgi = (i // (run * flows)) * run + i % run
+    pl = frame_len - 66
+    seq = (fl * 1000003 + sgi * pl) & 0xFFFFFFFF
+    ipid = sgi & 0xFFFF
+    tot = frame_len - ETH_LEN
+
+    def put(col, val):
+        b[:, col] = (val if torch.is_tensor(val) else torch.full_like(i, val)).to(torch.uint8)
+
+    for c, v in {12: 8, 13: 0, 14: 0x45, 15: 0, 16: tot >> 8, 17: tot & 0xFF, 20: 0x40, 21: 0,
+                 22: 64, 23: 6, 24: 0, 25: 0, 26: 10, 27: 0, 28: 0, 30: 10, 31: 0, 32: 1, 33: 1,
+                 34: 0x80, 36: 0, 37: 80, 42: 1, 43: 2, 44: 3, 45: 4, 46: 8 << 4, 47: 0x10,
+                 48: 0x10, 49: 0, 50: 0, 51: 0, 52: 0, 53: 0, 54: 1, 55: 1, 56: 8,
+                 57: 10}.items():
+        put(c, v)
+    put(18, ipid >> 8)
+    put(19, ipid & 0xFF)
+    put(29, fl)
+    put(35, fl)
+    for k in range(4):
+        put(38 + k, (seq >> (24 - 8 * k)) & 0xFF)
+    for k in range(58, 66):
+        put(k, fl + k)
+    return buf, stride
