@@ -45,43 +45,75 @@ __device__ __forceinline__ XFrame xframe(const Ext& x, uint64_t i)
                   x.queue ? x.queue + i : nullptr, x.nq, x.nq_magic, x.endian, nullptr};
 }
 
-template <int G, int U, bool COMPUTE, bool LOOP, bool NT, int WM, bool XCD, bool EXT>
+// K > 1: each group takes K frames, FPB apart (so every load instruction of a
+// wave still reads one contiguous range), and issues the loads of all K before
+// folding any: small frames give a lane only U*16 bytes each, too few bytes in
+// flight per wave to cover HBM latency.
+template <int G, int U, bool COMPUTE, bool LOOP, bool NT, int WM, bool XCD, bool EXT, int K = 1>
 __device__ __forceinline__ void fixed_frame(uint8_t* __restrict__ frames, uint64_t stride,
                                             u32 frame_len, u32 n, uint8_t* __restrict__ out_code,
                                             uint32_t* __restrict__ out_csum, u32 flags,
                                             const Ext& ext)
 {
-    constexpr int FPB = kBlock / G;                    // frames per block
+    constexpr int FPB = kBlock / G;                    // frames per block and batch
     const int sub = threadIdx.x & (G - 1);
     const uint32_t blk = XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint64_t i = (uint64_t)blk * FPB + threadIdx.x / G;
-    if (i >= n)
+    const uint64_t i0 = (uint64_t)blk * FPB * K + threadIdx.x / G;
+    if (i0 >= n)
         return;                                        // whole group leaves together
-    do_frame<G, U, COMPUTE, LOOP, false, NT, WM, EXT>(frames + i * stride, frame_len,
-                                                      (int64_t)stride, true, sub, flags,
-                                                      out_code ? out_code + i : nullptr,
-                                                      out_csum ? out_csum + i : nullptr, true,
-                                                      EXT ? xframe(ext, i) : XFrame{});
+    if constexpr (K == 1) {
+        do_frame<G, U, COMPUTE, LOOP, false, NT, WM, EXT>(frames + i0 * stride, frame_len,
+                                                          (int64_t)stride, true, sub, flags,
+                                                          out_code ? out_code + i0 : nullptr,
+                                                          out_csum ? out_csum + i0 : nullptr,
+                                                          true, EXT ? xframe(ext, i0) : XFrame{});
+    } else {
+        static_assert(!LOOP, "K > 1 is for frames that fit one batch");
+        const int nch = (int)((frame_len + 15) >> 4);
+        uint4 v[K][U];
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const uint64_t i = i0 + (uint64_t)k * FPB;
+            if (i < n) {
+                load_first<G, U, false, NT>(frames + i * stride, nch, (int64_t)stride, sub, v[k]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < U; j++)
+                    v[k][j] = make_uint4(0, 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const uint64_t i = i0 + (uint64_t)k * FPB;
+            if (i >= n)
+                break;                                 // group-uniform, and so are later k
+            uint8_t* f = frames + i * stride;
+            frame_body<G, U, COMPUTE, false, false, NT, WM, EXT>(
+                v[k], f, f, frame_len, (int64_t)stride, true, sub, flags,
+                out_code ? out_code + i : nullptr, out_csum ? out_csum + i : nullptr, true,
+                EXT ? xframe(ext, i) : XFrame{});
+        }
+    }
 }
 
-template <int G, int U, bool COMPUTE, bool LOOP, bool NT, int WM, bool XCD = false>
+template <int G, int U, bool COMPUTE, bool LOOP, bool NT, int WM, bool XCD = false, int K = 1>
 __global__ void __launch_bounds__(kBlock)
 k_fixed(uint8_t* __restrict__ frames, uint64_t stride, u32 frame_len, u32 n,
         uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags)
 {
-    fixed_frame<G, U, COMPUTE, LOOP, NT, WM, XCD, false>(frames, stride, frame_len, n, out_code,
-                                                         out_csum, flags, Ext{});
+    fixed_frame<G, U, COMPUTE, LOOP, NT, WM, XCD, false, K>(frames, stride, frame_len, n,
+                                                            out_code, out_csum, flags, Ext{});
 }
 
 // k_fixed with the extensions (ICMP fold, RSS steering): a separate
 // instantiation so the plain path carries none of their registers.
-template <int G, int U, bool COMPUTE, bool LOOP, bool NT, int WM, bool XCD>
+template <int G, int U, bool COMPUTE, bool LOOP, bool NT, int WM, bool XCD, int K = 1>
 __global__ void __launch_bounds__(kBlock)
 k_fixed_x(uint8_t* __restrict__ frames, uint64_t stride, u32 frame_len, u32 n,
           uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags, Ext ext)
 {
-    fixed_frame<G, U, COMPUTE, LOOP, NT, WM, XCD, true>(frames, stride, frame_len, n, out_code,
-                                                        out_csum, flags, ext);
+    fixed_frame<G, U, COMPUTE, LOOP, NT, WM, XCD, true, K>(frames, stride, frame_len, n, out_code,
+                                                           out_csum, flags, ext);
 }
 
 // Small frames (<= 64 B, C1): ONE LANE PER FRAME.  A lane loads its frame's
@@ -179,16 +211,30 @@ k_desc(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __re
 }
 
 // Mixed-size descriptor batch (IMIX, plugin bursts): a block takes 256
-// consecutive frames, sorts them into three LDS lists by size, and runs each
-// list on a group size that fits it: <= 64 B on 4 lanes (1 chunk per lane),
-// <= 768 B on 16 lanes (3 chunks per lane), larger on 32 lanes (3 chunks per
-// lane, then further batches).  Each list is walked by a block-uniform loop
-// so every cross-lane step sees its whole group.  Verdicts / statuses / checks
-// are staged in LDS and leave as one coalesced store per block.
-template <int G, int U, bool COMPUTE, bool LOOP, bool EXT>
+// consecutive frames, keeps their validated descriptors in LDS, sorts them
+// into three LDS lists by size, and runs each list on a group shape that fits
+// it (DescShape: class 0 = frames <= 16*G0*U0 B on G0 lanes x U0 chunks, class
+// 1 <= 16*G1*U1 B on G1 x U1, class 2 the rest on G2 x U2 with further
+// batches; WM = the TX write-back mode).  Each list is walked by a
+// block-uniform loop so every cross-lane step sees its whole group.
+// Verdicts / statuses / checks are staged in LDS and leave as one coalesced
+// store per block.  Keeping the descriptors in LDS saves each list iteration
+// a dependent global load before its frame loads: 4M IMIX frames, verify
+// 316 -> 269 us, fill 407 -> 364 us.  Wider shapes (U = 6 or 9 per lane)
+// spill at 6 waves per SIMD and lose (kbench imix).
+template <int G0_, int U0_, int G1_, int U1_, int G2_, int U2_, int WM_ = kWM>
+struct DescShape {
+    static constexpr int G0 = G0_, U0 = U0_, G1 = G1_, U1 = U1_, G2 = G2_, U2 = U2_, WM = WM_;
+    static constexpr int T0 = 16 * G0 * U0, T1 = 16 * G1 * U1;
+};
+
+// The shipped shapes (A/B in tools/kbench.hip imix).
+template <bool COMPUTE>
+using DescShip = DescShape<4, 1, 16, 3, 32, 3>;
+
+template <int G, int U, bool COMPUTE, bool LOOP, bool EXT, int WM>
 __device__ __forceinline__ void desc_class(uint8_t* __restrict__ frames, uint64_t frames_bytes,
-                                           const uint64_t* __restrict__ off,
-                                           const uint16_t* __restrict__ lens, uint64_t f0,
+                                           const uint64_t* soff, const uint16_t* slen,
                                            const uint16_t* list, int count, u32 flags,
                                            uint8_t* codes, uint32_t* csums, const Ext& ext,
                                            uint32_t* hashes, uint16_t* queues)
@@ -199,22 +245,22 @@ __device__ __forceinline__ void desc_class(uint8_t* __restrict__ frames, uint64_
         const int k = base + g;
         const bool active = k < count;
         const int t = active ? list[k] : list[0];      // list[0] exists: count > 0
-        const uint64_t o = off[f0 + t];
-        const u32 len = lens[f0 + t];
+        const uint64_t o = soff[t];                    // LDS: no dependent global load
+        const u32 len = slen[t];
         uint8_t* f = frames + o;                       // descriptor validated in phase 0
         const XFrame xf =
             EXT ? XFrame{{ext.key[0], ext.key[1], ext.key[2], ext.key[3]},
                          hashes ? hashes + t : nullptr, queues ? queues + t : nullptr, ext.nq,
                          ext.nq_magic, ext.endian, nullptr}
                 : XFrame{};
-        do_frame<G, U, COMPUTE, LOOP, true, kNT, kWM, EXT>(f, len, (int64_t)(frames_bytes - o),
+        do_frame<G, U, COMPUTE, LOOP, true, kNT, WM, EXT>(f, len, (int64_t)(frames_bytes - o),
                                                            true, sub, flags, codes + t,
                                                            COMPUTE ? csums + t : nullptr, active,
                                                            xf);
     }
 }
 
-template <bool COMPUTE, bool XCD, int OCC, bool EXT>
+template <class S, bool COMPUTE, bool XCD, bool EXT>
 __device__ __forceinline__ void desc_mixed(uint8_t* __restrict__ frames, uint64_t frames_bytes,
                                            const uint64_t* __restrict__ off,
                                            const uint16_t* __restrict__ lens, u32 n,
@@ -222,6 +268,8 @@ __device__ __forceinline__ void desc_mixed(uint8_t* __restrict__ frames, uint64_
                                            uint32_t* __restrict__ out_csum, u32 flags,
                                            const Ext& ext)
 {
+    __shared__ uint64_t soff[kBlock];
+    __shared__ uint16_t slen[kBlock];
     __shared__ uint16_t list[3][kBlock];
     __shared__ int cnt[3];
     __shared__ uint8_t codes[kBlock];
@@ -249,7 +297,9 @@ __device__ __forceinline__ void desc_mixed(uint8_t* __restrict__ frames, uint64_
                 queues[t] = 0xFFFF;
             }
         } else {
-            const int c = len <= 64 ? 0 : (len <= 768 ? 1 : 2);
+            soff[t] = o;
+            slen[t] = (uint16_t)len;
+            const int c = len <= (u32)S::T0 ? 0 : (len <= (u32)S::T1 ? 1 : 2);
             list[c][atomicAdd(&cnt[c], 1)] = (uint16_t)t;
         }
     }
@@ -257,9 +307,9 @@ __device__ __forceinline__ void desc_mixed(uint8_t* __restrict__ frames, uint64_
     const int n0 = cnt[0], n1 = cnt[1], n2 = cnt[2];
     uint32_t* hl = EXT && !COMPUTE ? hashes : nullptr;
     uint16_t* ql = EXT && !COMPUTE ? queues : nullptr;
-    if (n0) desc_class<4, 1, COMPUTE, false, EXT>(frames, frames_bytes, off, lens, f0, list[0], n0, flags, codes, csums, ext, hl, ql);
-    if (n1) desc_class<16, 3, COMPUTE, false, EXT>(frames, frames_bytes, off, lens, f0, list[1], n1, flags, codes, csums, ext, hl, ql);
-    if (n2) desc_class<32, 3, COMPUTE, true, EXT>(frames, frames_bytes, off, lens, f0, list[2], n2, flags, codes, csums, ext, hl, ql);
+    if (n0) desc_class<S::G0, S::U0, COMPUTE, false, EXT, S::WM>(frames, frames_bytes, soff, slen, list[0], n0, flags, codes, csums, ext, hl, ql);
+    if (n1) desc_class<S::G1, S::U1, COMPUTE, false, EXT, S::WM>(frames, frames_bytes, soff, slen, list[1], n1, flags, codes, csums, ext, hl, ql);
+    if (n2) desc_class<S::G2, S::U2, COMPUTE, true, EXT, S::WM>(frames, frames_bytes, soff, slen, list[2], n2, flags, codes, csums, ext, hl, ql);
     __syncthreads();
     if (i < n) {
         if (out_code)
@@ -275,25 +325,25 @@ __device__ __forceinline__ void desc_mixed(uint8_t* __restrict__ frames, uint64_
     }
 }
 
-template <bool COMPUTE, bool XCD, int OCC = 1>
+template <class S, bool COMPUTE, bool XCD, int OCC = 1>
 __global__ void __launch_bounds__(kBlock, OCC)
 k_desc_mixed(uint8_t* __restrict__ frames, uint64_t frames_bytes,
              const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens, u32 n,
              uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags)
 {
-    desc_mixed<COMPUTE, XCD, OCC, false>(frames, frames_bytes, off, lens, n, out_code, out_csum,
-                                         flags, Ext{});
+    desc_mixed<S, COMPUTE, XCD, false>(frames, frames_bytes, off, lens, n, out_code, out_csum,
+                                       flags, Ext{});
 }
 
-template <bool COMPUTE, bool XCD, int OCC = 1>
+template <class S, bool COMPUTE, bool XCD, int OCC = 1>
 __global__ void __launch_bounds__(kBlock, OCC)
 k_desc_mixed_x(uint8_t* __restrict__ frames, uint64_t frames_bytes,
                const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens, u32 n,
                uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags,
                Ext ext)
 {
-    desc_mixed<COMPUTE, XCD, OCC, true>(frames, frames_bytes, off, lens, n, out_code, out_csum,
-                                        flags, ext);
+    desc_mixed<S, COMPUTE, XCD, true>(frames, frames_bytes, off, lens, n, out_code, out_csum,
+                                      flags, ext);
 }
 
 // ---------------------------------------------------------------------------
@@ -916,19 +966,19 @@ k_ip_fn(const uint8_t* __restrict__ buf, uint64_t buf_bytes, const uint64_t* __r
 // ---------------------------------------------------------------------------
 // launchers (called from gcs_api.cpp)
 
-template <int G, int U, bool COMPUTE, bool LOOP, bool EXT>
+template <int G, int U, bool COMPUTE, bool LOOP, bool EXT, int K = 1>
 static hipError_t launch_fixed(uint8_t* frames, uint64_t stride, u32 frame_len, u32 n,
                                uint8_t* code, uint32_t* csum, u32 flags, const Ext& ext,
                                hipStream_t s)
 {
-    constexpr int FPB = kBlock / G;
+    constexpr int FPB = kBlock / G * K;                // frames per block
     dim3 grid((n + FPB - 1) / FPB);
     if (EXT)
-        hipLaunchKernelGGL((k_fixed_x<G, U, COMPUTE, LOOP, kNT, kWM, kXCD>), grid, dim3(kBlock), 0,
-                           s, frames, stride, frame_len, n, code, csum, flags, ext);
+        hipLaunchKernelGGL((k_fixed_x<G, U, COMPUTE, LOOP, kNT, kWM, kXCD, K>), grid, dim3(kBlock),
+                           0, s, frames, stride, frame_len, n, code, csum, flags, ext);
     else
-        hipLaunchKernelGGL((k_fixed<G, U, COMPUTE, LOOP, kNT, kWM, kXCD>), grid, dim3(kBlock), 0,
-                           s, frames, stride, frame_len, n, code, csum, flags);
+        hipLaunchKernelGGL((k_fixed<G, U, COMPUTE, LOOP, kNT, kWM, kXCD, K>), grid, dim3(kBlock),
+                           0, s, frames, stride, frame_len, n, code, csum, flags);
     return hipGetLastError();
 }
 
@@ -940,20 +990,25 @@ static hipError_t dispatch_fixed(uint8_t* frames, uint64_t stride, u32 frame_len
 {
     const u32 chunks = (frame_len + 15) / 16;
     if (chunks <= 4) {
-        // <= 64 B.  RX: one lane per frame (1M x 64 B: 16.7 us vs 19.8 us with 4 lanes
-        // per frame).  TX keeps 4 lanes per frame: their sector write-back is one
-        // coalesced 1 KiB store per wave, where one lane per frame scatters 64
-        // sectors per store instruction (74 us).
+        // <= 64 B.  TX: 4 lanes per frame, whose sector write-back is one coalesced
+        // 1 KiB store per wave, where one lane per frame scatters 64 sectors per
+        // store instruction (74 us per 1M frames vs 21.8 us); more frames per group
+        // only adds to the write tail (K = 2: 22.4 us, 8M frames 151 -> 161 us).
         if (COMPUTE)
             return launch_fixed<4, 1, COMPUTE, false, EXT>(frames, stride, frame_len, n, code,
                                                            csum, flags, ext, s);
-        const dim3 grid((n + kBlock - 1) / kBlock);
-        if (EXT)
-            hipLaunchKernelGGL((k_small_x<COMPUTE, kNT, kXCD>), grid, dim3(kBlock), 0, s, frames,
-                               stride, frame_len, n, code, csum, flags, ext);
-        else
-            hipLaunchKernelGGL((k_small<COMPUTE, kNT, kXCD>), grid, dim3(kBlock), 0, s, frames,
-                               stride, frame_len, n, code, csum, flags);
+        // Plain RX: 4 lanes per frame, 2 frames per group with both loads issued
+        // first.  8M x 64 B: 128 -> 95 us against one lane per frame, whose
+        // 64-B-strided loads fall behind once the batch leaves the Infinity
+        // Cache; 1M: 16.8 vs 16.6 us.
+        if (!EXT)
+            return launch_fixed<4, 1, COMPUTE, false, EXT, 2>(frames, stride, frame_len, n, code,
+                                                              csum, flags, ext, s);
+        // RX with the extensions: one lane per frame (k_small_x), whose RSS hash
+        // is 24 lookups in LDS nibble tables instead of a 4-lane bit split.
+        hipLaunchKernelGGL((k_small_x<COMPUTE, kNT, kXCD>), dim3((n + kBlock - 1) / kBlock),
+                           dim3(kBlock), 0, s, frames, stride, frame_len, n, code, csum, flags,
+                           ext);
         return hipGetLastError();
     }
     if (chunks <= 8)   return launch_fixed<8, 1, COMPUTE, false, EXT>(frames, stride, frame_len, n, code, csum, flags, ext, s);
@@ -997,12 +1052,13 @@ static hipError_t launch_desc(uint8_t* frames, uint64_t frames_bytes, const uint
                               const uint16_t* len, u32 n, uint8_t* code, uint32_t* csums,
                               u32 flags, bool ext_on, const Ext& ext, hipStream_t s)
 {
+    using S = DescShip<COMPUTE>;
     const dim3 grid((n + kBlock - 1) / kBlock);
     if (ext_on)
-        hipLaunchKernelGGL((k_desc_mixed_x<COMPUTE, kXCD, kDescOcc>), grid, dim3(kBlock), 0, s,
+        hipLaunchKernelGGL((k_desc_mixed_x<S, COMPUTE, kXCD, kDescOcc>), grid, dim3(kBlock), 0, s,
                            frames, frames_bytes, off, len, n, code, csums, flags, ext);
     else
-        hipLaunchKernelGGL((k_desc_mixed<COMPUTE, kXCD, kDescOcc>), grid, dim3(kBlock), 0, s,
+        hipLaunchKernelGGL((k_desc_mixed<S, COMPUTE, kXCD, kDescOcc>), grid, dim3(kBlock), 0, s,
                            frames, frames_bytes, off, len, n, code, csums, flags);
     return hipGetLastError();
 }

@@ -143,6 +143,21 @@ def device_count() -> int:
     return c.value if rc == 0 else 0
 
 
+def _torch_ordered(stream, *bufs):
+    """Stream ordering for stream=None launches.  They run on the context's
+    own (non-blocking) HIP stream, which does not wait for torch's stream: a
+    torch.zeros() / copy still in flight there would race the kernel.  So
+    when a torch CUDA tensor is passed without an explicit stream, wait for
+    torch's current stream first.  (bench.py passes torch's stream instead.)"""
+    if stream is not None:
+        return
+    for b in bufs:
+        if getattr(b, "is_cuda", False):
+            import torch
+            torch.cuda.current_stream().synchronize()
+            return
+
+
 class Context:
     """One gcs_ctx: a HIP device + stream (+ pinned staging for host batches)."""
 
@@ -190,6 +205,7 @@ class Context:
             raise GcsError(f"{what}: buffer of {_nbytes(buf)} B < required {nbytes} B")
 
     def verify_fixed(self, frames, stride, frame_len, n, verdict, flags=0, stream=None):
+        _torch_ordered(stream, frames, verdict)
         self._need(frames, n * stride, "frames")
         self._need(verdict, n, "verdict")
         check(self.L.gcs_verify_fixed_dev(self.h, _daddr(frames), stride, frame_len, n,
@@ -197,6 +213,7 @@ class Context:
 
     def compute_fixed(self, frames, stride, frame_len, n, status=None, csums=None, flags=0,
                       stream=None):
+        _torch_ordered(stream, frames, status, csums)
         self._need(frames, n * stride, "frames")
         self._need(status, n, "status")
         self._need(csums, 4 * n, "csums")
@@ -205,6 +222,7 @@ class Context:
               "compute_fixed")
 
     def verify(self, frames, off, lens, n, verdict, flags=0, stream=None, frames_bytes=None):
+        _torch_ordered(stream, frames, off, lens, verdict)
         fb = _nbytes(frames) if frames_bytes is None else frames_bytes
         self._need(frames, fb, "frames")
         self._need(off, 8 * n, "off")
@@ -215,6 +233,7 @@ class Context:
 
     def compute(self, frames, off, lens, n, status=None, csums=None, flags=0, stream=None,
                 frames_bytes=None):
+        _torch_ordered(stream, frames, off, lens, status, csums)
         fb = _nbytes(frames) if frames_bytes is None else frames_bytes
         self._need(frames, fb, "frames")
         self._need(off, 8 * n, "off")
@@ -225,6 +244,7 @@ class Context:
                                      _daddr(status), _daddr(csums), flags, stream), "compute")
 
     def tcp_checksum(self, buf, off, lens, saddr, daddr, n, out, stream=None, buf_bytes=None):
+        _torch_ordered(stream, buf, off, lens, saddr, daddr, out)
         bb = _nbytes(buf) if buf_bytes is None else buf_bytes
         self._need(buf, bb, "buf")
         for a, w in ((off, 8), (lens, 2), (saddr, 4), (daddr, 4), (out, 2)):
@@ -234,6 +254,7 @@ class Context:
               "tcp_checksum")
 
     def ip_checksum(self, buf, off, ihl, n, out, stream=None, buf_bytes=None):
+        _torch_ordered(stream, buf, off, ihl, out)
         bb = _nbytes(buf) if buf_bytes is None else buf_bytes
         self._need(buf, bb, "buf")
         for a, w in ((off, 8), (ihl, 1), (out, 2)):
@@ -243,6 +264,7 @@ class Context:
 
     def compute_copy(self, frames, off, lens, src, src_off, n, status=None, csums=None,
                      flags=0, stream=None, frames_bytes=None, src_bytes=None):
+        _torch_ordered(stream, frames, off, lens, src, src_off, status, csums)
         fb = _nbytes(frames) if frames_bytes is None else frames_bytes
         sb = _nbytes(src) if src_bytes is None else src_bytes
         self._need(frames, fb, "frames")
@@ -255,6 +277,7 @@ class Context:
 
     def gro(self, frames, off, lens, verdict, n, window, max_len, out, out_off, out_len, head,
             stream=None, in_bytes=None, out_bytes=None):
+        _torch_ordered(stream, frames, off, lens, verdict, out, out_off, out_len, head)
         ib = _nbytes(frames) if in_bytes is None else in_bytes
         ob = _nbytes(out) if out_bytes is None else out_bytes
         self._need(frames, ib, "frames")
@@ -266,6 +289,7 @@ class Context:
                                  _daddr(out_off), _daddr(out_len), _daddr(head), stream), "gro")
 
     def icmp_checksum(self, buf, off, lens, n, out, stream=None, buf_bytes=None):
+        _torch_ordered(stream, buf, off, lens, out)
         bb = _nbytes(buf) if buf_bytes is None else buf_bytes
         self._need(buf, bb, "buf")
         for a, w in ((off, 8), (lens, 2), (out, 2)):
@@ -281,6 +305,7 @@ class Context:
 
     def classify_fixed(self, frames, stride, frame_len, n, verdict, hash=None, queue=None,
                        flags=0, stream=None):
+        _torch_ordered(stream, frames, verdict, hash, queue)
         self._need(frames, n * stride, "frames")
         self._need(verdict, n, "verdict")
         self._need(hash, 4 * n, "hash")
@@ -291,6 +316,7 @@ class Context:
 
     def classify(self, frames, off, lens, n, verdict, hash=None, queue=None, flags=0,
                  stream=None, frames_bytes=None):
+        _torch_ordered(stream, frames, off, lens, verdict, hash, queue)
         fb = _nbytes(frames) if frames_bytes is None else frames_bytes
         self._need(frames, fb, "frames")
         self._need(off, 8 * n, "off")
@@ -303,6 +329,7 @@ class Context:
                                       stream), "classify")
 
     def rss(self, sip, dip, sp, dp, n, hash=None, queue=None, stream=None):
+        _torch_ordered(stream, sip, dip, sp, dp, hash, queue)
         for a, w in ((sip, 4), (dip, 4), (sp, 2), (dp, 2), (hash, 4), (queue, 2)):
             self._need(a, w * n, "array")
         check(self.L.gcs_rss_dev(self.h, _daddr(sip), _daddr(dip), _daddr(sp), _daddr(dp), n,

@@ -141,14 +141,26 @@ int imix_main(uint64_t n, int rounds)
         hipLaunchKernelGGL((k_desc<16, 2, true, true, WM_SECTOR_SC1>), dim3((n + 15) / 16),
                            dim3(256), 0, st, tx, total, doff, dlen, (u32)n, nullptr, nullptr, 0u);
     }});
-#define MIXED(C_, OCC_, TAG)                                                               \
-    vs.push_back({std::string(C_ ? "compute" : "verify ") + " k_desc_mixed occ " + TAG,     \
+#define MIXED(C_, OCC_, TAG, ...)                                                          \
+    vs.push_back({std::string(C_ ? "compute" : "verify ") + " mixed occ " + TAG,            \
                   C_ ? cb : vb, [&](hipStream_t st) {                                      \
-        hipLaunchKernelGGL((k_desc_mixed<C_, true, OCC_>), dim3((n + 255) / 256), dim3(256), \
-                           0, st, C_ ? tx : rx, total, doff, dlen, (u32)n,                  \
-                           C_ ? nullptr : v1, nullptr, 0u);                                 \
+        hipLaunchKernelGGL((k_desc_mixed<DescShape<__VA_ARGS__>, C_, true, OCC_>),          \
+                           dim3((n + 255) / 256), dim3(256), 0, st, C_ ? tx : rx, total,     \
+                           doff, dlen, (u32)n, C_ ? nullptr : v1, nullptr,                  \
+                           std::string(TAG).find("no write") != std::string::npos           \
+                               ? (u32)GCS_CF_NO_INPLACE : 0u);                              \
     }});
-    MIXED(false, 6, "6") MIXED(false, 8, "8") MIXED(true, 6, "6") MIXED(true, 8, "8")
+    // shapes (round 1: <4,1|16,3|32,3> wins; U = 6 / 9 spill at 6 waves, 270 -> 360-780 us)
+    MIXED(false, 6, "6 <4,1|16,3|32,3>", 4, 1, 16, 3, 32, 3)
+    MIXED(false, 6, "6 <4,1|8,3|32,3>", 4, 1, 8, 3, 32, 3)
+    MIXED(false, 6, "6 <4,1|16,2|32,3>", 4, 1, 16, 2, 32, 3)
+    MIXED(true, 6, "6 <4,1|16,3|32,3>", 4, 1, 16, 3, 32, 3)
+    // TX write-back modes
+    MIXED(true, 6, "6 <4,1|16,3|32,3> 16B chunks sc1", 4, 1, 16, 3, 32, 3, WM_CHUNK_SC1)
+    MIXED(true, 6, "6 <4,1|16,3|32,3> 2B stores", 4, 1, 16, 3, 32, 3, WM_HALFWORD)
+    MIXED(true, 6, "6 <4,1|16,3|32,3> 64B sector plain", 4, 1, 16, 3, 32, 3, WM_SECTOR)
+    MIXED(true, 6, "6 <4,1|16,3|32,3> 128B line sc1", 4, 1, 16, 3, 32, 3, WM_LINE_SC1)
+    MIXED(true, 6, "6 <4,1|16,3|32,3> no write-back", 4, 1, 16, 3, 32, 3)
     vs.push_back({"verify  desc (launch_verify_desc)", vb, [&](hipStream_t st) {
         CK(launch_verify_desc(rx, total, doff, dlen, (u32)n, v1, 0u, st));
     }});
@@ -674,6 +686,24 @@ int main(int argc, char** argv)
         vs.push_back({"compute dispatch_fixed (k_small)", cbytes, [&](hipStream_t st) {
             CK(launch_compute_fixed(tx, stride, L, (u32)n, nullptr, nullptr, 0u, st));
         }});
+        // K frames per group, all loads issued first
+#define KV(G_, K_, C_)                                                                         \
+        vs.push_back({std::string(C_ ? "compute" : "verify ") + " k_fixed<" #G_ ",1> K=" #K_,  \
+                      C_ ? cbytes : vbytes, [&](hipStream_t st) {                              \
+            hipLaunchKernelGGL((k_fixed<G_, 1, C_, false, true, WM_SECTOR_SC1, true, K_>),     \
+                               dim3((n + 256 / G_ * K_ - 1) / (256 / G_ * K_)), dim3(256), 0,  \
+                               st, C_ ? tx : rx, stride, L, (u32)n, C_ ? nullptr : v2,         \
+                               nullptr, 0u);                                                   \
+        }});
+        KV(4, 2, false) KV(4, 4, false) KV(4, 8, false)
+        KV(4, 2, true)
+#define KW(WM_, TAG)                                                                           \
+        vs.push_back({std::string("compute k_fixed<4,1> ") + TAG, cbytes, [&](hipStream_t st) { \
+            hipLaunchKernelGGL((k_fixed<4, 1, true, false, true, WM_, true>), dim3((n + 63) / 64), \
+                               dim3(256), 0, st, tx, stride, L, (u32)n, nullptr, nullptr, 0u); \
+        }});
+        KW(WM_CHUNK_SC1, "16B chunks sc1") KW(WM_HALFWORD, "2B stores") KW(WM_SECTOR, "64B plain")
+        KW(WM_CHUNK, "16B chunks plain")
     } else {
         vs.push_back({"verify  dispatch_fixed", vbytes, [&](hipStream_t st) {
             CK(launch_verify_fixed(rx, stride, L, (u32)n, v1, 0u, st));
