@@ -183,10 +183,11 @@ int imix_main(uint64_t n, int rounds)
 
 // K frames per group, software-pipelined: the loads of frame k+1 are issued
 // before frame k is reduced and written back, so a wave's store tail overlaps
-// its next loads.  OOP: the 64 B write-back goes to scratch + 64*i (a
+// its next loads.  OOP = 1: the 64 B write-back goes to scratch + 64*i (a
 // contiguous stream) instead of the frame, to separate the cost of scattered
-// DRAM writes from the cost of the store tail.
-template <int G, int U, int K, bool COMPUTE, int WM, bool OOP>
+// DRAM writes from the cost of the store tail; OOP = 2: to scratch + 64*(i %
+// 4096), 256 KiB that stay in L2 (plain stores) -- no DRAM writes at all.
+template <int G, int U, int K, bool COMPUTE, int WM, int OOP>
 __global__ void __launch_bounds__(256)
 k_multi(uint8_t* __restrict__ frames, uint64_t stride, u32 len, u32 n,
         uint8_t* __restrict__ out_code, uint8_t* __restrict__ scratch)
@@ -210,7 +211,7 @@ k_multi(uint8_t* __restrict__ frames, uint64_t stride, u32 len, u32 n,
             load_first<G, U, false, true>(frames + (i + FPB) * stride, nch, 1 << 30, sub, w);
         uint8_t* f = frames + i * stride;
         frame_body<G, U, COMPUTE, false, false, true, WM>(
-            v, f, OOP ? scratch + 64 * i : f, len, 1 << 30, true, sub, 0u,
+            v, f, OOP == 0 ? f : scratch + 64 * (OOP == 1 ? i : (i & 4095)), len, 1 << 30, true, sub, 0u,
             COMPUTE ? nullptr : out_code + i, nullptr, true);
         if (more) {
 #pragma unroll
@@ -253,6 +254,16 @@ int tx_main(uint64_t n, int rounds)
                            C_ ? tx : rx, stride, L, (u32)n, C_ ? nullptr : v1, nullptr, FL_); \
     }});
     TXV(32, 3, false, WM_SECTOR_SC1, 0u, "")
+#define TXN(G_, U_, C_, WM_, FL_, TAG)                                                        \
+    vs.push_back({std::string(C_ ? "compute" : "verify ") + " <" #G_ "," #U_ "> linear " + TAG, \
+                  C_ ? cbytes : vbytes, [&](hipStream_t st) {                                 \
+        hipLaunchKernelGGL((k_fixed<G_, U_, C_, false, true, WM_, false>),                    \
+                           dim3((n + 256 / G_ - 1) / (256 / G_)), dim3(256), 0, st,           \
+                           C_ ? tx : rx, stride, L, (u32)n, C_ ? nullptr : v1, nullptr, FL_); \
+    }});
+    TXN(32, 3, false, WM_SECTOR_SC1, 0u, "")
+    TXN(32, 3, true, WM_SECTOR_SC1, (u32)GCS_CF_NO_INPLACE, "pure fold (no write-back)")
+    TXN(32, 3, true, WM_SECTOR_SC1, 0u, "64B sector sc1")
     TXV(16, 6, false, WM_SECTOR_SC1, 0u, "")
     TXV(64, 2, false, WM_SECTOR_SC1, 0u, "")
     TXV(8, 12, false, WM_SECTOR_SC1, 0u, "")
@@ -275,6 +286,8 @@ int tx_main(uint64_t n, int rounds)
     }});
     MULTI(1, true, WM_SECTOR_SC1, true, "64B sector sc1 to a contiguous scratch")
     MULTI(1, true, WM_SECTOR, true, "64B sector plain to a contiguous scratch")
+    MULTI(1, true, WM_SECTOR, 2, "64B sector plain to 256 KiB of L2-resident scratch")
+    MULTI(1, true, WM_SECTOR_SC1, 2, "64B sector sc1 to 256 KiB of scratch")
     MULTI(2, true, WM_SECTOR_SC1, false, "64B sector sc1, pipelined")
     MULTI(4, true, WM_SECTOR_SC1, false, "64B sector sc1, pipelined")
     MULTI(2, false, WM_SECTOR_SC1, false, "pipelined")
@@ -516,6 +529,24 @@ void run_variants(std::vector<Variant>& vs, hipStream_t s, int rounds)
     for (auto& v : vs)
         for (int w = 0; w < 3; w++) v.run(s);
     CK(hipStreamSynchronize(s));
+    // KB_BLOCKED=1: each variant's rounds back to back (after 3 untimed runs of
+    // it), instead of interleaved -- no variant then runs behind another's
+    // dirty lines or write-back.
+    if (std::getenv("KB_BLOCKED")) {
+        for (auto& v : vs) {
+            for (int w = 0; w < 3; w++) v.run(s);
+            for (int r = 0; r < rounds; r++) {
+                CK(hipEventRecord(e0, s));
+                v.run(s);
+                CK(hipEventRecord(e1, s));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                v.ms.push_back(ms);
+            }
+        }
+        rounds = 0;
+    }
     for (int r = 0; r < rounds; r++) {
         for (auto& v : vs) {
             CK(hipEventRecord(e0, s));
@@ -729,6 +760,24 @@ int main(int argc, char** argv)
     for (auto& v : vs)
         for (int w = 0; w < 3; w++) v.run(s);
     CK(hipStreamSynchronize(s));
+    // KB_BLOCKED=1: each variant's rounds back to back (after 3 untimed runs of
+    // it), instead of interleaved -- no variant then runs behind another's
+    // dirty lines or write-back.
+    if (std::getenv("KB_BLOCKED")) {
+        for (auto& v : vs) {
+            for (int w = 0; w < 3; w++) v.run(s);
+            for (int r = 0; r < rounds; r++) {
+                CK(hipEventRecord(e0, s));
+                v.run(s);
+                CK(hipEventRecord(e1, s));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                v.ms.push_back(ms);
+            }
+        }
+        rounds = 0;
+    }
     for (int r = 0; r < rounds; r++) {
         for (auto& v : vs) {
             CK(hipEventRecord(e0, s));
