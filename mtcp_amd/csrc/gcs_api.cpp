@@ -44,6 +44,12 @@ int hip_fail(hipError_t e, const char* what)
 
 constexpr int kSlots = 2;
 constexpr uint64_t kSlotAlign = 64;   // pslib packing, io_engine/lib/pslib.c:146
+// Host batches staged in at most this many bytes run in direct mode (the
+// kernel reads pinned staging over PCIe; run_host_batch).  Per-call latency,
+// DMA copies vs direct (tools/burst_lat.py): 64 x 1500 B verify
+// 42 -> 21 us, 256 x 1500 B 87 -> 29 us, 1024 x 1500 B 136 -> 96 us.  The env
+// variable GCS_DIRECT_MAX_BYTES overrides it (0 disables direct mode).
+constexpr uint64_t kDirectMaxBytes = 2u << 20;
 
 struct Slot {
     hipStream_t stream = nullptr;
@@ -62,6 +68,15 @@ struct Slot {
     uint32_t* d_hash = nullptr;
     uint16_t* h_queue = nullptr;
     uint16_t* d_queue = nullptr;
+    // device views of the pinned buffers (direct mode: the kernel reads the
+    // staged frames and writes its results over PCIe, no DMA copies)
+    uint8_t* m_frames = nullptr;
+    uint64_t* m_off = nullptr;
+    uint16_t* m_len = nullptr;
+    uint8_t* m_code = nullptr;
+    uint32_t* m_csum = nullptr;
+    uint32_t* m_hash = nullptr;
+    uint16_t* m_queue = nullptr;
     // bookkeeping of the chunk in flight
     bool busy = false;
     uint32_t first = 0, count = 0;
@@ -178,6 +193,8 @@ struct gcs_ctx {
     uint32_t rss_nq = 1, rss_magic = 0, rss_endian = 0;
     uint32_t max_frames = 0;   // per slot
     uint64_t max_bytes = 0;    // per slot
+    uint64_t direct_max = 0;   // host batches up to this many staged bytes: direct mode
+    bool direct_spread = true; // direct mode on k_desc (8 frames per block), not k_desc_mixed
     Slot slot[kSlots];
     std::unique_ptr<GatherPool> pool;
 
@@ -259,6 +276,13 @@ int alloc_slot(Slot& s, uint32_t frames, uint64_t bytes)
     HIP_TRY(hipHostMalloc((void**)&s.h_queue, frames * sizeof(uint16_t), hipHostMallocDefault));
     HIP_TRY(hipMalloc((void**)&s.d_hash, frames * sizeof(uint32_t)));
     HIP_TRY(hipMalloc((void**)&s.d_queue, frames * sizeof(uint16_t)));
+    HIP_TRY(hipHostGetDevicePointer((void**)&s.m_frames, s.h_frames, 0));
+    HIP_TRY(hipHostGetDevicePointer((void**)&s.m_off, s.h_off, 0));
+    HIP_TRY(hipHostGetDevicePointer((void**)&s.m_len, s.h_len, 0));
+    HIP_TRY(hipHostGetDevicePointer((void**)&s.m_code, s.h_code, 0));
+    HIP_TRY(hipHostGetDevicePointer((void**)&s.m_csum, s.h_csum, 0));
+    HIP_TRY(hipHostGetDevicePointer((void**)&s.m_hash, s.h_hash, 0));
+    HIP_TRY(hipHostGetDevicePointer((void**)&s.m_queue, s.h_queue, 0));
     return GCS_OK;
 }
 
@@ -438,32 +462,57 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
         }
         s.first = next;
         s.count = cnt;
-        HIP_TRY(hipMemcpyAsync(s.d_frames, h2d_src, used, hipMemcpyHostToDevice, s.stream));
-        HIP_TRY(hipMemcpyAsync(s.d_off, s.h_off, cnt * sizeof(uint64_t), hipMemcpyHostToDevice,
-                               s.stream));
-        HIP_TRY(hipMemcpyAsync(s.d_len, s.h_len, cnt * sizeof(uint16_t), hipMemcpyHostToDevice,
-                               s.stream));
-        if (compute) {
-            HIP_TRY(gcs::launch_compute_desc(s.d_frames, used, s.d_off, s.d_len, cnt, s.d_code,
-                                             s.d_csum, GCS_CF_NO_INPLACE, s.stream));
-            HIP_TRY(hipMemcpyAsync(s.h_csum, s.d_csum, cnt * sizeof(uint32_t),
-                                   hipMemcpyDeviceToHost, s.stream));
+        // Direct mode: a small batch staged whole in one gather (an mTCP burst is
+        // <= 64 frames, dpdk_module.c:76).  The kernel reads the pinned staging
+        // and writes its results over PCIe: one launch instead of three H2D
+        // copies + the kernel + one or three D2H copies, each with its own
+        // submission latency.
+        const bool direct = h2d_src == s.h_frames && next == 0 && cnt == n &&
+                            used <= ctx->direct_max;
+        uint8_t* frames_d = direct ? s.m_frames : s.d_frames;
+        uint64_t* off_d = direct ? s.m_off : s.d_off;
+        uint16_t* len_d = direct ? s.m_len : s.d_len;
+        uint8_t* code_d = direct ? s.m_code : s.d_code;
+        uint32_t* csum_d = direct ? s.m_csum : s.d_csum;
+        uint32_t* hash_d = direct ? s.m_hash : s.d_hash;
+        uint16_t* queue_d = direct ? s.m_queue : s.d_queue;
+        if (!direct) {
+            HIP_TRY(hipMemcpyAsync(s.d_frames, h2d_src, used, hipMemcpyHostToDevice, s.stream));
+            HIP_TRY(hipMemcpyAsync(s.d_off, s.h_off, cnt * sizeof(uint64_t),
+                                   hipMemcpyHostToDevice, s.stream));
+            HIP_TRY(hipMemcpyAsync(s.d_len, s.h_len, cnt * sizeof(uint16_t),
+                                   hipMemcpyHostToDevice, s.stream));
+        }
+        const bool spread = direct && ctx->direct_spread && !(flags & GCS_VF_ICMP);
+        if (compute && spread) {
+            HIP_TRY(gcs::launch_compute_desc_spread(frames_d, used, off_d, len_d, cnt, code_d,
+                                                    csum_d, GCS_CF_NO_INPLACE, s.stream));
+        } else if (compute) {
+            HIP_TRY(gcs::launch_compute_desc(frames_d, used, off_d, len_d, cnt, code_d, csum_d,
+                                             GCS_CF_NO_INPLACE, s.stream));
+            if (!direct)
+                HIP_TRY(hipMemcpyAsync(s.h_csum, s.d_csum, cnt * sizeof(uint32_t),
+                                       hipMemcpyDeviceToHost, s.stream));
         } else if (classify) {
-            HIP_TRY(gcs::launch_classify_desc(s.d_frames, used, s.d_off, s.d_len, cnt, s.d_code,
+            HIP_TRY(gcs::launch_classify_desc(frames_d, used, off_d, len_d, cnt, code_d,
                                               flags & GCS_VF_ICMP,
-                                              rss_ext(ctx, s.d_hash, s.d_queue), s.stream));
-            if (hash)
+                                              rss_ext(ctx, hash_d, queue_d), s.stream));
+            if (hash && !direct)
                 HIP_TRY(hipMemcpyAsync(s.h_hash, s.d_hash, cnt * sizeof(uint32_t),
                                        hipMemcpyDeviceToHost, s.stream));
-            if (queue)
+            if (queue && !direct)
                 HIP_TRY(hipMemcpyAsync(s.h_queue, s.d_queue, cnt * sizeof(uint16_t),
                                        hipMemcpyDeviceToHost, s.stream));
+        } else if (spread) {
+            HIP_TRY(gcs::launch_verify_desc_spread(frames_d, used, off_d, len_d, cnt, code_d,
+                                                   flags & GCS_VF_ICMP, s.stream));
         } else {
             // the tcp_in.c:1237 side effect is applied on the host copy below
-            HIP_TRY(gcs::launch_verify_desc(s.d_frames, used, s.d_off, s.d_len, cnt, s.d_code,
+            HIP_TRY(gcs::launch_verify_desc(frames_d, used, off_d, len_d, cnt, code_d,
                                             flags & GCS_VF_ICMP, s.stream));
         }
-        HIP_TRY(hipMemcpyAsync(s.h_code, s.d_code, cnt, hipMemcpyDeviceToHost, s.stream));
+        if (!direct)
+            HIP_TRY(hipMemcpyAsync(s.h_code, s.d_code, cnt, hipMemcpyDeviceToHost, s.stream));
         HIP_TRY(hipEventRecord(s.done, s.stream));
         s.busy = true;
         next += cnt;
@@ -543,6 +592,11 @@ int gcs_ctx_create(gcs_ctx** out, int device, uint32_t max_frames, uint64_t max_
         return hip_fail(e, "hipStreamCreateWithFlags");
     }
     set_rss_params(ctx, kDefaultRssKey, 1, 0);
+    ctx->direct_max = kDirectMaxBytes;
+    if (const char* e = std::getenv("GCS_DIRECT_MAX_BYTES"))
+        ctx->direct_max = std::strtoull(e, nullptr, 10);
+    if (const char* e = std::getenv("GCS_DIRECT_SPREAD"))
+        ctx->direct_spread = std::atoi(e) != 0;
     if (max_frames && max_bytes) {
         // split the requested staging between the two slots
         ctx->max_frames = std::max<uint32_t>(1, max_frames / kSlots + 1);

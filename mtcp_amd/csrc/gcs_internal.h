@@ -27,6 +27,12 @@ hipError_t launch_verify_desc(uint8_t* frames, uint64_t frames_bytes, const uint
 hipError_t launch_compute_desc(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
                                const uint16_t* len, uint32_t n, uint8_t* status, uint32_t* csums,
                                uint32_t flags, hipStream_t s);
+hipError_t launch_verify_desc_spread(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
+                                     const uint16_t* len, uint32_t n, uint8_t* verdict,
+                                     uint32_t flags, hipStream_t s);
+hipError_t launch_compute_desc_spread(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
+                                      const uint16_t* len, uint32_t n, uint8_t* status,
+                                      uint32_t* csums, uint32_t flags, hipStream_t s);
 hipError_t launch_classify_fixed(uint8_t* frames, uint64_t stride, uint32_t frame_len,
                                  uint32_t n, uint8_t* verdict, uint32_t flags, const Ext& ext,
                                  hipStream_t s);

@@ -1079,6 +1079,35 @@ hipError_t launch_compute_desc(uint8_t* frames, uint64_t frames_bytes, const uin
                              (flags & GCS_CF_ICMP) != 0, Ext{}, s);
 }
 
+// Descriptor batch spread thin: one frame per 32-lane group (8 frames per
+// block), so a small batch read over PCIe from pinned host memory (direct
+// mode, gcs_api.cpp) is pulled by many CUs at once instead of one block.
+template <bool COMPUTE>
+static hipError_t launch_desc_spread(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
+                                     const uint16_t* len, u32 n, uint8_t* code, uint32_t* csums,
+                                     u32 flags, hipStream_t s)
+{
+    constexpr int G = 32, U = 3, FPB = kBlock / G;
+    hipLaunchKernelGGL((k_desc<G, U, COMPUTE, kNT, kWM>), dim3((n + FPB - 1) / FPB), dim3(kBlock),
+                       0, s, frames, frames_bytes, off, len, n, code, csums, flags);
+    return hipGetLastError();
+}
+
+hipError_t launch_verify_desc_spread(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
+                                     const uint16_t* len, u32 n, uint8_t* verdict, u32 flags,
+                                     hipStream_t s)
+{
+    return launch_desc_spread<false>(frames, frames_bytes, off, len, n, verdict, nullptr, flags,
+                                     s);
+}
+
+hipError_t launch_compute_desc_spread(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
+                                      const uint16_t* len, u32 n, uint8_t* status,
+                                      uint32_t* csums, u32 flags, hipStream_t s)
+{
+    return launch_desc_spread<true>(frames, frames_bytes, off, len, n, status, csums, flags, s);
+}
+
 hipError_t launch_classify_desc(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
                                 const uint16_t* len, u32 n, uint8_t* verdict, u32 flags,
                                 const Ext& ext, hipStream_t s)

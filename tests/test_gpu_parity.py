@@ -315,6 +315,37 @@ def test_host_batches_chunked(torch_dev, O):
         assert (rv[bad] != 0).all()
 
 
+@pytest.mark.parametrize("direct,spread", [(0, 1), (1 << 30, 0), (1 << 30, 1)])
+@pytest.mark.parametrize("n", [1, 64, 700])
+def test_host_bursts_direct_and_dma(torch_dev, O, monkeypatch, direct, spread, n):
+    """Small host batches (an mTCP burst) through both staging modes: DMA
+    copies, and direct mode (the kernel reads pinned staging over PCIe) on
+    the mixed and the spread descriptor kernel; jumbo frames included."""
+    monkeypatch.setenv("GCS_DIRECT_MAX_BYTES", str(direct))
+    monkeypatch.setenv("GCS_DIRECT_SPREAD", str(spread))
+    lens = synth.imix_lengths(n, seed=41 + n)
+    if n > 1:
+        lens[n // 2] = 9000
+    buf, off, lens = synth.packed_frames(lens, seed=42 + n)
+    with gpucsum.Context(0, max_frames=1024, max_bytes=4 << 20) as c:
+        b1 = buf.copy()
+        st, cs = c.compute_host(b1, off, lens)
+        ref = buf.copy()
+        rst, rcs = O.compute_batch(ref, off, lens)
+        np.testing.assert_array_equal(st, rst)
+        np.testing.assert_array_equal(cs, rcs)
+        np.testing.assert_array_equal(b1, ref)
+        bad = synth.corrupt(ref, off, lens, frac_log2=2, seed=7)
+        for flags in (1, 0):
+            b2 = ref.copy()
+            v = c.verify_host(b2, off, lens, flags=flags)
+            r2 = ref.copy()
+            rv = O.verify_batch(r2, off, lens, flags=flags)
+            np.testing.assert_array_equal(v, rv)
+            np.testing.assert_array_equal(b2, r2)
+        assert (rv[bad] != 0).all()
+
+
 @pytest.mark.parametrize("mode", ["pinned", "registered"])
 def test_host_batches_zero_copy(torch_dev, O, mode):
     """Pinned / registered host frames take the span (zero host copy) path."""
