@@ -563,7 +563,8 @@ k_copy_fill(uint8_t* __restrict__ frames, uint64_t frames_bytes,
 // ref_gro_batch.  One block per window of <= kGroW frames:
 //   A  thread t parses frame t's first 96 B into LDS;
 //   B  thread t decides whether frame t continues frame t-1;
-//   C  thread 0 walks the window once to form runs (length limit), offsets;
+//   C  each chain's first thread cuts its chain into runs (length limit);
+//      a block scan numbers the runs and gives their output offsets;
 //   D  each wave builds whole runs: a single frame is copied as it is, a
 //      longer run is assembled destination-chunk by destination-chunk (head
 //      headers with tot_len / PSH patched, then the members' payloads through
@@ -632,6 +633,11 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
     __shared__ uint32_t run_len[kGroW];
     __shared__ uint64_t run_off[kGroW];
     __shared__ int nruns;
+    __shared__ uint64_t soff[kGroW];   // the window's descriptors: no dependent global loads in D
+    __shared__ uint16_t rn_at[kGroW];  // per run head (window index): members, length, run index
+    __shared__ uint32_t rl_at[kGroW];
+    __shared__ uint16_t ridx[kGroW];
+    __shared__ uint32_t wsum[kBlock / 64][2];
 
     const int t = threadIdx.x;
     const uint64_t w0 = (uint64_t)blockIdx.x * window;
@@ -642,6 +648,7 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
     if (t < cnt) {
         const uint64_t o = off[w0 + t];
         const u32 L = lens[w0 + t];
+        soff[t] = o;
         const bool ok = (o & 15) == 0 && o <= in_bytes && L <= in_bytes - o;
         const bool acc = ok && verdict[w0 + t] == GCS_V_ACCEPT;
         dok[t] = ok;
@@ -664,49 +671,86 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
     if (t < cnt)
         cont[t] = t > 0 && gro_cont(hdr[t - 1], hdr[t], pay[t - 1], pay[t]);
     __syncthreads();
-    // C: runs (one thread walks the window)
-    if (t == 0) {
-        uint64_t o = cnt ? off[w0] : 0;
-        int r = -1, cur = 0;
-        u32 mlen = 0;
-        bool mergeable = false;
-        for (int k = 0; k < cnt; k++) {
-            if (k > 0 && mergeable && cont[k] && mlen + (u32)pay[k] <= max_len) {
+    // C: runs.  A chain is a maximal sequence of frames that each continue the
+    // previous one (cont); every frame of a chain is mergeable, so runs are
+    // chains cut greedily at max_len -- ref_gro_batch's walk, done by each
+    // chain's first thread over its own chain, in parallel.  Then one block
+    // scan gives every run its index and its 16 B-aligned output offset.
+    // (One thread walking the whole window took ~1/3 of the kernel.)
+    uint32_t rl = 0;                                   // this thread's run length if it heads one
+    bool rs = false;                                   // ... and whether it does
+    if (t < cnt && (t == 0 || !cont[t])) {
+        int cur = t;
+        u32 mlen = pay[t] > 0 ? 34 + 4 * (hdr[t][46] >> 4) + (u32)pay[t]
+                              : (dok[t] ? (u32)lens[w0 + t] : 0u);     // a bad descriptor: nothing
+        pref[t] = 0;
+        rhead[t] = (uint16_t)t;
+        rn_at[t] = 1;
+        for (int k = t + 1; k < cnt && cont[k]; k++) {
+            if (mlen + (u32)pay[k] <= max_len) {
                 pref[k] = mlen - (34 + 4 * (hdr[cur][46] >> 4));
                 mlen += (u32)pay[k];
                 rhead[k] = (uint16_t)cur;
-                run_n[r]++;
-                run_len[r] = mlen;
+                rn_at[cur]++;
                 continue;
             }
-            if (r >= 0)
-                o += (run_len[r] + 15u) & ~15u;
-            r++;
+            rl_at[cur] = mlen;                         // max_len cut: k heads a new run
             cur = k;
-            mergeable = pay[k] > 0;
-            mlen = mergeable ? 34 + 4 * (hdr[k][46] >> 4) + (u32)pay[k]
-                             : (dok[k] ? (u32)lens[w0 + k] : 0u);      // a bad descriptor: nothing
+            mlen = 34 + 4 * (hdr[k][46] >> 4) + (u32)pay[k];
             pref[k] = 0;
             rhead[k] = (uint16_t)k;
-            run_t[r] = (uint16_t)k;
-            run_n[r] = 1;
-            run_len[r] = mlen;
-            run_off[r] = o;
+            rn_at[k] = 1;
         }
-        nruns = r + 1;
+        rl_at[cur] = mlen;
+    }
+    __syncthreads();
+    if (t < cnt && rhead[t] == t) {
+        rs = true;
+        rl = rl_at[t];
+    }
+    // exclusive scans of (run starts, aligned run lengths) over the window
+    u32 xs = rs ? 1u : 0u, xl = rs ? (rl + 15u) & ~15u : 0u;
+    {
+        const int lane = t & 63, w = t >> 6;
+        u32 is = xs, il = xl;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const u32 os = __shfl_up(is, d, 64), ol = __shfl_up(il, d, 64);
+            if (lane >= d) {
+                is += os;
+                il += ol;
+            }
+        }
+        if (lane == 63) {
+            wsum[w][0] = is;
+            wsum[w][1] = il;
+        }
+        __syncthreads();
+        u32 bs = 0, bl = 0;
+        for (int q = 0; q < w; q++) {
+            bs += wsum[q][0];
+            bl += wsum[q][1];
+        }
+        xs = bs + is - xs;                             // exclusive
+        xl = bl + il - xl;
+        if (t == kBlock - 1)
+            nruns = (int)(bs + is);
+    }
+    const uint64_t o0 = cnt ? soff[0] : 0;
+    if (rs) {
+        run_t[xs] = (uint16_t)t;
+        run_n[xs] = (uint16_t)rn_at[t];
+        run_len[xs] = rl;
+        run_off[xs] = o0 + xl;
+        ridx[t] = (uint16_t)xs;
     }
     __syncthreads();
     if (t < cnt) {
         const int hk = rhead[t];
+        const int r = ridx[hk];
         head[w0 + t] = (uint32_t)(w0 + hk);
-        // the run's offset: the head's entry (runs are listed in head order)
-        int lo = 0, hi = nruns - 1;
-        while (lo < hi) {                              // last run with run_t <= hk
-            const int mid = (lo + hi + 1) >> 1;
-            if (run_t[mid] <= hk) lo = mid; else hi = mid - 1;
-        }
-        out_off[w0 + t] = run_off[lo];
-        out_len[w0 + t] = hk == t ? (uint16_t)run_len[lo] : (uint16_t)0;
+        out_off[w0 + t] = run_off[r];
+        out_len[w0 + t] = hk == t ? (uint16_t)run_len[r] : (uint16_t)0;
     }
 
     // D: build the runs, one wave per run
@@ -717,7 +761,7 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
         const uint64_t oo = run_off[r];
         uint8_t* m = out + oo;
         const int64_t wlim = oo <= out_bytes ? (int64_t)(out_bytes - oo) : 0;
-        const uint64_t io = off[w0 + k0];
+        const uint64_t io = soff[k0];
         const int nchunks = (int)((mlen + 15) >> 4);
         if (nm == 1) {                                 // as it is
             const int64_t avail = (int64_t)(in_bytes - io);
@@ -755,7 +799,7 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
                 if (c < nchunks && cb + 16 <= hl) {
                     pl = AS_FRAME;                                 // head's headers (LDS)
                 } else if (c < nchunks && cb < hl) {
-                    const uint8_t* p0 = in + off[w0 + k0] + hl;
+                    const uint8_t* p0 = in + soff[k0] + hl;
                     ct = hl - cb;                                  // header bytes in the chunk
                     if (cb + 16 <= te && pay[k0] >= 16 - ct && p0 + 16 <= in_end) {
                         pl = AS_UP;
@@ -773,16 +817,16 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
                     sg = lo2;
                     const int rem = (int)(pref[sg] + (u32)pay[sg] - q);   // bytes left in sg
                     const int need = min(16, te - cb);
-                    const uint8_t* pq = in + off[w0 + sg] + hl + (q - pref[sg]);
+                    const uint8_t* pq = in + soff[sg] + hl + (q - pref[sg]);
                     if (rem >= need && pq + 16 <= in_end) {
                         pl = AS_ONE;                               // one member (masked at te)
                         pa[j] = ldg16u(pq);
                     } else if (sg + 1 < k0 + nm && pay[sg + 1] >= need - rem &&
-                               pq + 16 <= in_end && in + off[w0 + sg + 1] + hl + 16 <= in_end) {
+                               pq + 16 <= in_end && in + soff[sg + 1] + hl + 16 <= in_end) {
                         pl = AS_TWO;                               // the end of sg, then sg+1
                         ct = rem;
                         pa[j] = ldg16u(pq);
-                        pb[j] = ldg16u(in + off[w0 + sg + 1] + hl);
+                        pb[j] = ldg16u(in + soff[sg + 1] + hl);
                     } else {
                         pl = AS_BYTES;
                     }
@@ -822,7 +866,7 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
                             const u32 qq = (u32)(p - hl);
                             while (qq >= pref[s2] + (u32)pay[s2])
                                 s2++;
-                            b = in[off[w0 + s2] + hl + (qq - pref[s2])];
+                            b = in[soff[s2] + hl + (qq - pref[s2])];
                         }
                         w[k >> 2] |= b << (8 * (k & 3));
                     }

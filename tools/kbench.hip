@@ -488,6 +488,12 @@ int lro_main(uint64_t n, int rounds)
         CK(launch_gro(in, n * stride, off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol,
                       hd, st));
     }});
+#define GROU(U_)                                                                             \
+    vs.push_back({"k_gro<" #U_ "> (window 64, max 16384)", bytes, [&](hipStream_t st) {          \
+        hipLaunchKernelGGL((k_gro<U_>), dim3((n + 63) / 64), dim3(256), 0, st, in, n * stride,   \
+                           off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd);    \
+    }});
+    GROU(2) GROU(3) GROU(4)
     vs.push_back({"verify (launch_verify_desc) for scale", (double)n * (L + 1), [&](hipStream_t st) {
         CK(launch_verify_desc(in, n * stride, off, lens, (u32)n, vd, 0u, st));
     }});
