@@ -428,6 +428,7 @@ k_copy_fill(uint8_t* __restrict__ frames, uint64_t frames_bytes,
         return;
     const uint64_t o = off[i];
     const u32 len = lens[i];
+    const uint64_t po_any = src_off[i];                // loaded with off[i], not after the headers
     const bool ok = (o & 15) == 0 && o <= frames_bytes && len <= frames_bytes - o;
     uint8_t* f = frames + (ok ? o : 0);
     const int64_t avail = ok ? (int64_t)(frames_bytes - o) : 0;
@@ -452,7 +453,7 @@ k_copy_fill(uint8_t* __restrict__ frames, uint64_t frames_bytes,
                       (h.d5 >> 24) == 6 && doff >= 5 && tot >= 4 * (ihl + doff) &&
                       te <= (int)len;
     const uint64_t plen = copy ? (uint64_t)(te - hl) : 0;
-    const uint64_t po = copy ? src_off[i] : 0;
+    const uint64_t po = copy ? po_any : 0;
     if (copy && !(po <= src_bytes && plen <= src_bytes - po)) {   // group-uniform
         if (sub == 0) {
             if (out_code)
