@@ -12,7 +12,7 @@ set -o pipefail
 ROUND=${1:-r01}
 OUT=gpurun_out/prof_$ROUND
 mkdir -p "$OUT"
-CMD="python bench.py --steps 10 --warmup 2 --cpu-seconds 0 --no-extras"
+CMD="python bench.py --steps 10 --warmup 2 --cpu-seconds 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \
     -- $CMD > "$OUT/trace.log" 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/fetch" -o run \
