@@ -411,6 +411,54 @@ __device__ __forceinline__ uint4 blend(uint4 x, uint4 y, uint4 m)
 // consumed, so a wave waits once per batch.
 enum { AS_ZERO = 0, AS_FRAME, AS_ONE, AS_UP, AS_TAIL, AS_TWO, AS_BYTES };
 
+// k_copy_fill: the plan and loads of one batch of destination chunks (base +
+// j*G + sub) for headers ending at hl and a segment ending at te; payload byte
+// p of the frame comes from ps[p - hl], with src_room readable bytes from ps.
+// Every source load stays inside [ps, ps + src_room): AS_ONE needs
+// cb - hl + 16 <= te - hl, which the caller has checked against src_room.
+// Frame chunks (headers, bytes past te, the plain fill) are loaded from f,
+// except batch 0's chunk `sub` < hv_lanes, already loaded as hv.
+template <int G, int U>
+__device__ __forceinline__ void cf_issue(int base, int sub, int nchunks, bool copy, int hl, int te,
+                                         const uint8_t* ps, int64_t src_room,
+                                         const uint8_t* f, int64_t avail, const uint4& hv,
+                                         int hv_lanes, uint4 (&fr)[U], uint4 (&pv)[U],
+                                         int (&plan)[U])
+{
+    const uint4 z = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+        const int c = base + j * G + sub;
+        const int cb = 16 * c;
+        int pl = AS_ZERO;
+        fr[j] = z;
+        pv[j] = z;
+        if (c < nchunks) {
+            if (!copy || cb + 16 <= hl || cb >= te) {
+                pl = AS_FRAME;                           // header / past the segment
+            } else if (cb >= hl && cb + 16 <= te) {
+                pl = AS_ONE;                             // payload only
+                pv[j] = ldg16u(ps + (cb - hl));
+            } else if (cb < hl && cb + 16 <= te && src_room >= 16) {
+                pl = AS_UP;                              // headers, then the payload start
+                pv[j] = ldg16u(ps);
+            } else if (cb >= hl && src_room >= (int64_t)(cb - hl) + 16) {
+                pl = AS_TAIL;                            // the payload end, then frame bytes
+                pv[j] = ldg16u(ps + (cb - hl));
+            } else {
+                pl = AS_BYTES;                           // tiny payload / source end
+            }
+            if (pl != AS_ONE) {
+                if (base == 0 && j == 0 && sub < hv_lanes)
+                    fr[j] = hv;
+                else
+                    fr[j] = load_chunk<true, false>(f + cb, avail - cb);
+            }
+        }
+        plan[j] = pl;
+    }
+}
+
 template <int G, int U>
 __global__ void __launch_bounds__(kBlock)
 k_copy_fill(uint8_t* __restrict__ frames, uint64_t frames_bytes,
@@ -420,6 +468,18 @@ k_copy_fill(uint8_t* __restrict__ frames, uint64_t frames_bytes,
             uint32_t* __restrict__ out_csum, u32 flags)
 {
     static_assert(G >= 16, "the first G chunks must hold the longest header (134 B)");
+    // Frame chunks read up front: 0..5, enough to parse (the doff byte of the
+    // longest IP header, ts + 12 <= 86, lies in chunk 5).  Further frame
+    // chunks are read only where the plan keeps frame bytes; the rest of the
+    // frame's old contents is overwritten by the payload, so reading it would
+    // waste ~0.45 GB per 1M x 1500 B frames (PMC: 2.2 GB read for 1.6 GB used).
+    constexpr int kHdrLanes = 6;
+    // Speculation: mTCP's data segments carry ihl 5 and doff 8 (ip_out.c:143,
+    // tcp_out.c:22-61 with timestamps), so headers end at 66 and tot_len covers
+    // the frame.  Batch 0's payload loads are issued for that layout together
+    // with the header loads, and re-issued only if the parsed headers differ:
+    // one memory round trip per frame instead of two.
+    constexpr int kSpecHl = 66;
     constexpr int FPB = kBlock / G;
     const int sub = threadIdx.x & (G - 1);
     const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);
@@ -435,8 +495,19 @@ k_copy_fill(uint8_t* __restrict__ frames, uint64_t frames_bytes,
     const int nchunks = ok ? (int)((len + 15) >> 4) : 0;
     const uint4 z = make_uint4(0, 0, 0, 0);
 
-    // headers: frame chunk `sub` of the first G chunks
-    const uint4 hv = sub < nchunks ? load_chunk<true, false>(f + 16 * sub, avail - 16 * sub) : z;
+    // headers: frame chunk `sub` < kHdrLanes
+    const uint4 hv = (sub < kHdrLanes && sub < nchunks)
+                         ? load_chunk<true, false>(f + 16 * sub, avail - 16 * sub)
+                         : z;
+    // speculative batch 0: the guessed source range lies inside the source
+    const int te_g = (int)len;
+    const bool copy_g = ok && te_g >= kSpecHl && po_any <= src_bytes &&
+                        (uint64_t)(te_g - kSpecHl) <= src_bytes - po_any;
+    uint4 fr[U], pv[U];
+    int plan[U];
+    cf_issue<G, U>(0, sub, nchunks, copy_g, kSpecHl, te_g, src + (copy_g ? po_any : 0),
+                   copy_g ? (int64_t)(src_bytes - po_any) : 0, f, avail, hv, kHdrLanes, fr, pv,
+                   plan);
     Hdr h;
     h.d3 = group_bcast<G, 0>(hv.w);
     h.d4 = group_bcast<G, 1>(hv.x);
@@ -464,46 +535,21 @@ k_copy_fill(uint8_t* __restrict__ frames, uint64_t frames_bytes,
         return;
     }
     const uint8_t* ps = src + po;                      // frame byte p <- ps[p - hl]
+    // payload loads must stay inside the source buffer: `src_room` bytes from ps
+    const int64_t src_room = copy ? (int64_t)(src_bytes - po) : 0;
+    // wrong guess (group-uniform): batch 0 again, for the parsed layout
+    if (copy != copy_g || (copy && (hl != kSpecHl || te != te_g)))
+        cf_issue<G, U>(0, sub, nchunks, copy, hl, te, ps, src_room, f, avail, hv, kHdrLanes, fr,
+                       pv, plan);
 
     Acc a = {0u, 0u, 0u};
     uint4 first[U];
-    // payload loads must stay inside the source buffer: `src_room` bytes from ps
-    const int64_t src_room = copy ? (int64_t)(src_bytes - po) : 0;
     for (int base = 0; base < nchunks; base += G * U) {   // group-uniform
-        uint4 v[U], fr[U], pv[U];
-        int plan[U];
-        // 1: issue the loads of every chunk of the batch
-#pragma unroll
-        for (int j = 0; j < U; j++) {
-            const int c = base + j * G + sub;
-            const int cb = 16 * c;
-            int pl = AS_ZERO;
-            fr[j] = z;
-            pv[j] = z;
-            if (c < nchunks) {
-                if (!copy || cb + 16 <= hl || cb >= te) {
-                    pl = AS_FRAME;                           // header / past the segment
-                } else if (cb >= hl && cb + 16 <= te) {
-                    pl = AS_ONE;                             // payload only
-                    pv[j] = ldg16u(ps + (cb - hl));
-                } else if (cb < hl && cb + 16 <= te && src_room >= 16) {
-                    pl = AS_UP;                              // headers, then the payload start
-                    pv[j] = ldg16u(ps);
-                } else if (cb >= hl && src_room >= (int64_t)(cb - hl) + 16) {
-                    pl = AS_TAIL;                            // the payload end, then frame bytes
-                    pv[j] = ldg16u(ps + (cb - hl));
-                } else {
-                    pl = AS_BYTES;                           // tiny payload / source end
-                }
-                if (pl != AS_ONE) {
-                    if (base == 0 && j == 0)
-                        fr[j] = hv;
-                    else
-                        fr[j] = load_chunk<true, false>(f + cb, avail - cb);
-                }
-            }
-            plan[j] = pl;
-        }
+        uint4 v[U];
+        // 1: issue the loads of every chunk of the batch (batch 0: above)
+        if (base > 0)
+            cf_issue<G, U>(base, sub, nchunks, copy, hl, te, ps, src_room, f, avail, hv,
+                           kHdrLanes, fr, pv, plan);
         // 2: assemble
 #pragma unroll
         for (int j = 0; j < U; j++) {
@@ -614,30 +660,33 @@ __device__ bool gro_cont(const uint8_t* p, const uint8_t* c, int pp, int pc)
     return lds_be32(c + 38) == lds_be32(p + 38) + (u32)pp;
 }
 
-template <int U>
+// W = the largest window the instantiation takes (LDS is sized by it): W = 64
+// needs ~9 KiB of LDS per block instead of ~36 KiB, so a CU holds twice the
+// blocks (8 instead of 4) and twice the run-building waves.
+template <int U, int W = kGroW>
 __global__ void __launch_bounds__(kBlock)
 k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restrict__ off,
       const uint16_t* __restrict__ lens, const uint8_t* __restrict__ verdict, u32 n, u32 window,
       u32 max_len, uint8_t* __restrict__ out, uint64_t out_bytes, uint64_t* __restrict__ out_off,
       uint16_t* __restrict__ out_len, uint32_t* __restrict__ head)
 {
-    static_assert(kBlock == kGroW, "one frame per thread");
+    static_assert(W <= kBlock, "one frame per thread");
     constexpr int G = 64;
-    __shared__ __attribute__((aligned(16))) uint8_t hdr[kGroW][kGroHdr];
-    __shared__ int pay[kGroW];         // TCP payload bytes of a mergeable frame, else -1
-    __shared__ uint8_t cont[kGroW];
-    __shared__ uint8_t dok[kGroW];     // descriptor inside the input buffer
-    __shared__ uint32_t pref[kGroW];   // payload offset of a member within its run
-    __shared__ uint16_t rhead[kGroW];  // run head (window index) of each frame
-    __shared__ uint16_t run_t[kGroW];  // runs: head index, member count, length, offset
-    __shared__ uint16_t run_n[kGroW];
-    __shared__ uint32_t run_len[kGroW];
-    __shared__ uint64_t run_off[kGroW];
+    __shared__ __attribute__((aligned(16))) uint8_t hdr[W][kGroHdr];
+    __shared__ int pay[W];         // TCP payload bytes of a mergeable frame, else -1
+    __shared__ uint8_t cont[W];
+    __shared__ uint8_t dok[W];     // descriptor inside the input buffer
+    __shared__ uint32_t pref[W];   // payload offset of a member within its run
+    __shared__ uint16_t rhead[W];  // run head (window index) of each frame
+    __shared__ uint16_t run_t[W];  // runs: head index, member count, length, offset
+    __shared__ uint16_t run_n[W];
+    __shared__ uint32_t run_len[W];
+    __shared__ uint64_t run_off[W];
     __shared__ int nruns;
-    __shared__ uint64_t soff[kGroW];   // the window's descriptors: no dependent global loads in D
-    __shared__ uint16_t rn_at[kGroW];  // per run head (window index): members, length, run index
-    __shared__ uint32_t rl_at[kGroW];
-    __shared__ uint16_t ridx[kGroW];
+    __shared__ uint64_t soff[W];   // the window's descriptors: no dependent global loads in D
+    __shared__ uint16_t rn_at[W];  // per run head (window index): members, length, run index
+    __shared__ uint32_t rl_at[W];
+    __shared__ uint16_t ridx[W];
     __shared__ uint32_t wsum[kBlock / 64][2];
 
     const int t = threadIdx.x;
@@ -1195,9 +1244,15 @@ hipError_t launch_gro(const uint8_t* in, uint64_t in_bytes, const uint64_t* off,
                       u32 max_len, uint8_t* out, uint64_t out_bytes, uint64_t* out_off,
                       uint16_t* out_len, uint32_t* head, hipStream_t s)
 {
-    hipLaunchKernelGGL((k_gro<2>), dim3((n + window - 1) / window), dim3(kBlock), 0, s, in,
-                       in_bytes, off, len, verdict, n, window, max_len, out, out_bytes, out_off,
-                       out_len, head);
+    // windows of <= 64 frames on the small-LDS instantiation (twice the blocks per CU)
+    if (window <= 64)
+        hipLaunchKernelGGL((k_gro<2, 64>), dim3((n + window - 1) / window), dim3(kBlock), 0, s, in,
+                           in_bytes, off, len, verdict, n, window, max_len, out, out_bytes,
+                           out_off, out_len, head);
+    else
+        hipLaunchKernelGGL((k_gro<2, kGroW>), dim3((n + window - 1) / window), dim3(kBlock), 0, s,
+                           in, in_bytes, off, len, verdict, n, window, max_len, out, out_bytes,
+                           out_off, out_len, head);
     return hipGetLastError();
 }
 

@@ -493,7 +493,13 @@ int lro_main(uint64_t n, int rounds)
         hipLaunchKernelGGL((k_gro<U_>), dim3((n + 63) / 64), dim3(256), 0, st, in, n * stride,   \
                            off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd);    \
     }});
-    GROU(2) GROU(3) GROU(4)
+    GROU(2) GROU(4)
+#define GROW(U_, W_)                                                                         \
+    vs.push_back({"k_gro<" #U_ "," #W_ "> (window 64, max 16384)", bytes, [&](hipStream_t st) {  \
+        hipLaunchKernelGGL((k_gro<U_, W_>), dim3((n + 63) / 64), dim3(256), 0, st, in, n * stride, \
+                           off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd);  \
+    }});
+    GROW(2, 64) GROW(4, 64)
     vs.push_back({"verify (launch_verify_desc) for scale", (double)n * (L + 1), [&](hipStream_t st) {
         CK(launch_verify_desc(in, n * stride, off, lens, (u32)n, vd, 0u, st));
     }});
