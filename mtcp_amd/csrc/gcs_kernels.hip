@@ -222,9 +222,13 @@ k_desc(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __re
 // a dependent global load before its frame loads: 4M IMIX frames, verify
 // 316 -> 269 us, fill 407 -> 364 us.  Wider shapes (U = 6 or 9 per lane)
 // spill at 6 waves per SIMD and lose (kbench imix).
-template <int G0_, int U0_, int G1_, int U1_, int G2_, int U2_, int WM_ = kWM>
+// F = descriptors per block (<= kBlock): fewer per block means more, shorter
+// blocks -- a smaller tail when large frames make every block long.
+template <int G0_, int U0_, int G1_, int U1_, int G2_, int U2_, int WM_ = kWM, int F_ = kBlock>
 struct DescShape {
     static constexpr int G0 = G0_, U0 = U0_, G1 = G1_, U1 = U1_, G2 = G2_, U2 = U2_, WM = WM_;
+    static constexpr int F = F_;
+    static_assert(F <= kBlock, "one descriptor per thread");
     static constexpr int T0 = 16 * G0 * U0, T1 = 16 * G1 * U1;
 };
 
@@ -268,23 +272,24 @@ __device__ __forceinline__ void desc_mixed(uint8_t* __restrict__ frames, uint64_
                                            uint32_t* __restrict__ out_csum, u32 flags,
                                            const Ext& ext)
 {
-    __shared__ uint64_t soff[kBlock];
-    __shared__ uint16_t slen[kBlock];
-    __shared__ uint16_t list[3][kBlock];
+    constexpr int F = S::F;
+    __shared__ uint64_t soff[F];
+    __shared__ uint16_t slen[F];
+    __shared__ uint16_t list[3][F];
     __shared__ int cnt[3];
-    __shared__ uint8_t codes[kBlock];
-    __shared__ uint32_t csums[COMPUTE ? kBlock : 1];
-    __shared__ uint32_t hashes[EXT && !COMPUTE ? kBlock : 1];
-    __shared__ uint16_t queues[EXT && !COMPUTE ? kBlock : 1];
+    __shared__ uint8_t codes[F];
+    __shared__ uint32_t csums[COMPUTE ? F : 1];
+    __shared__ uint32_t hashes[EXT && !COMPUTE ? F : 1];
+    __shared__ uint16_t queues[EXT && !COMPUTE ? F : 1];
     const uint32_t blk = XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint64_t f0 = (uint64_t)blk * kBlock;
+    const uint64_t f0 = (uint64_t)blk * F;
     const int t = threadIdx.x;
     if (t < 3)
         cnt[t] = 0;
     __syncthreads();
     // phase 0: validate and classify
     const uint64_t i = f0 + t;
-    if (i < n) {
+    if (t < F && i < n) {
         const uint64_t o = off[i];
         const u32 len = lens[i];
         const bool ok = (o & 15) == 0 && o <= frames_bytes && len <= frames_bytes - o;
@@ -311,7 +316,7 @@ __device__ __forceinline__ void desc_mixed(uint8_t* __restrict__ frames, uint64_
     if (n1) desc_class<S::G1, S::U1, COMPUTE, false, EXT, S::WM>(frames, frames_bytes, soff, slen, list[1], n1, flags, codes, csums, ext, hl, ql);
     if (n2) desc_class<S::G2, S::U2, COMPUTE, true, EXT, S::WM>(frames, frames_bytes, soff, slen, list[2], n2, flags, codes, csums, ext, hl, ql);
     __syncthreads();
-    if (i < n) {
+    if (t < F && i < n) {
         if (out_code)
             out_code[i] = codes[t];
         if (COMPUTE && out_csum)
@@ -1147,7 +1152,7 @@ static hipError_t launch_desc(uint8_t* frames, uint64_t frames_bytes, const uint
                               u32 flags, bool ext_on, const Ext& ext, hipStream_t s)
 {
     using S = DescShip<COMPUTE>;
-    const dim3 grid((n + kBlock - 1) / kBlock);
+    const dim3 grid((n + S::F - 1) / S::F);
     if (ext_on)
         hipLaunchKernelGGL((k_desc_mixed_x<S, COMPUTE, kXCD, kDescOcc>), grid, dim3(kBlock), 0, s,
                            frames, frames_bytes, off, len, n, code, csums, flags, ext);

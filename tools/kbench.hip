@@ -144,17 +144,20 @@ int imix_main(uint64_t n, int rounds)
 #define MIXED(C_, OCC_, TAG, ...)                                                          \
     vs.push_back({std::string(C_ ? "compute" : "verify ") + " mixed occ " + TAG,            \
                   C_ ? cb : vb, [&](hipStream_t st) {                                      \
-        hipLaunchKernelGGL((k_desc_mixed<DescShape<__VA_ARGS__>, C_, true, OCC_>),          \
-                           dim3((n + 255) / 256), dim3(256), 0, st, C_ ? tx : rx, total,     \
+        using S_ = DescShape<__VA_ARGS__>;                                                  \
+        hipLaunchKernelGGL((k_desc_mixed<S_, C_, true, OCC_>),                              \
+                           dim3((n + S_::F - 1) / S_::F), dim3(256), 0, st, C_ ? tx : rx, total, \
                            doff, dlen, (u32)n, C_ ? nullptr : v1, nullptr,                  \
                            std::string(TAG).find("no write") != std::string::npos           \
                                ? (u32)GCS_CF_NO_INPLACE : 0u);                              \
     }});
     // shapes (round 1: <4,1|16,3|32,3> wins; U = 6 / 9 spill at 6 waves, 270 -> 360-780 us)
     MIXED(false, 6, "6 <4,1|16,3|32,3>", 4, 1, 16, 3, 32, 3)
-    MIXED(false, 6, "6 <4,1|8,3|32,3>", 4, 1, 8, 3, 32, 3)
-    MIXED(false, 6, "6 <4,1|16,2|32,3>", 4, 1, 16, 2, 32, 3)
+    MIXED(false, 6, "6 <4,1|16,3|32,3> F=128", 4, 1, 16, 3, 32, 3, kWM, 128)
+    MIXED(false, 6, "6 <4,1|16,3|32,3> F=64", 4, 1, 16, 3, 32, 3, kWM, 64)
     MIXED(true, 6, "6 <4,1|16,3|32,3>", 4, 1, 16, 3, 32, 3)
+    MIXED(true, 6, "6 <4,1|16,3|32,3> F=128", 4, 1, 16, 3, 32, 3, kWM, 128)
+    MIXED(true, 6, "6 <4,1|16,3|32,3> F=64", 4, 1, 16, 3, 32, 3, kWM, 64)
     // TX write-back modes
     MIXED(true, 6, "6 <4,1|16,3|32,3> 16B chunks sc1", 4, 1, 16, 3, 32, 3, WM_CHUNK_SC1)
     MIXED(true, 6, "6 <4,1|16,3|32,3> 2B stores", 4, 1, 16, 3, 32, 3, WM_HALFWORD)
@@ -422,6 +425,21 @@ int copy_main(uint64_t n, int rounds)
     }});
     vs.push_back({"  fill alone (launch_compute_desc)", cbytes, [&](hipStream_t st_) {
         CK(launch_compute_desc(tx, n * stride, off, lens, (u32)n, st, nullptr, 0u, st_));
+    }});
+#define DFILL(F_)                                                                            \
+    vs.push_back({"  fill alone, desc_mixed F=" #F_, cbytes, [&](hipStream_t st_) {          \
+        using S_ = DescShape<4, 1, 16, 3, 32, 3, kWM, F_>;                                   \
+        hipLaunchKernelGGL((k_desc_mixed<S_, true, true, kDescOcc>), dim3((n + F_ - 1) / F_), \
+                           dim3(256), 0, st_, tx, n * stride, off, lens, (u32)n, st, nullptr, 0u); \
+    }});                                                                                     \
+    vs.push_back({"  verify, desc_mixed F=" #F_, (double)n * (L + 1), [&](hipStream_t st_) {  \
+        using S_ = DescShape<4, 1, 16, 3, 32, 3, kWM, F_>;                                   \
+        hipLaunchKernelGGL((k_desc_mixed<S_, false, true, kDescOcc>), dim3((n + F_ - 1) / F_), \
+                           dim3(256), 0, st_, tx, n * stride, off, lens, (u32)n, st, nullptr, 0u); \
+    }});
+    DFILL(256) DFILL(128) DFILL(64) DFILL(32)
+    vs.push_back({"  fill, fixed stride (launch_compute_fixed)", cbytes, [&](hipStream_t st_) {
+        CK(launch_compute_fixed(tx, stride, L, (u32)n, nullptr, nullptr, 0u, st_));
     }});
     run_variants(vs, s, rounds);
     std::vector<uint8_t> h(n);
