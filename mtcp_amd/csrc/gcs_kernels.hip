@@ -464,8 +464,8 @@ __device__ __forceinline__ void cf_issue(int base, int sub, int nchunks, bool co
     }
 }
 
-template <int G, int U>
-__global__ void __launch_bounds__(kBlock)
+template <int G, int U, int OCC = 1>
+__global__ void __launch_bounds__(kBlock, OCC)
 k_copy_fill(uint8_t* __restrict__ frames, uint64_t frames_bytes,
             const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens,
             const uint8_t* __restrict__ src, uint64_t src_bytes,
@@ -668,8 +668,8 @@ __device__ bool gro_cont(const uint8_t* p, const uint8_t* c, int pp, int pc)
 // W = the largest window the instantiation takes (LDS is sized by it): W = 64
 // needs ~9 KiB of LDS per block instead of ~36 KiB, so a CU holds twice the
 // blocks (8 instead of 4) and twice the run-building waves.
-template <int U, int W = kGroW>
-__global__ void __launch_bounds__(kBlock)
+template <int U, int W = kGroW, int OCC = 1>
+__global__ void __launch_bounds__(kBlock, OCC)
 k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restrict__ off,
       const uint16_t* __restrict__ lens, const uint8_t* __restrict__ verdict, u32 n, u32 window,
       u32 max_len, uint8_t* __restrict__ out, uint64_t out_bytes, uint64_t* __restrict__ out_off,
@@ -1249,9 +1249,11 @@ hipError_t launch_gro(const uint8_t* in, uint64_t in_bytes, const uint64_t* off,
                       u32 max_len, uint8_t* out, uint64_t out_bytes, uint64_t* out_off,
                       uint16_t* out_len, uint32_t* head, hipStream_t s)
 {
-    // windows of <= 64 frames on the small-LDS instantiation (twice the blocks per CU)
+    // windows of <= 64 frames on the small-LDS instantiation, 6 waves per SIMD
+    // (<= 80 VGPRs): 1M x 1500 B in runs of 8, 928 us (LDS-bound, 4 blocks per
+    // CU) -> 809 (89 VGPRs, 5 per SIMD) -> 772 us (tools/kbench lro)
     if (window <= 64)
-        hipLaunchKernelGGL((k_gro<2, 64>), dim3((n + window - 1) / window), dim3(kBlock), 0, s, in,
+        hipLaunchKernelGGL((k_gro<2, 64, 6>), dim3((n + window - 1) / window), dim3(kBlock), 0, s, in,
                            in_bytes, off, len, verdict, n, window, max_len, out, out_bytes,
                            out_off, out_len, head);
     else

@@ -153,11 +153,10 @@ int imix_main(uint64_t n, int rounds)
     }});
     // shapes (round 1: <4,1|16,3|32,3> wins; U = 6 / 9 spill at 6 waves, 270 -> 360-780 us)
     MIXED(false, 6, "6 <4,1|16,3|32,3>", 4, 1, 16, 3, 32, 3)
-    MIXED(false, 6, "6 <4,1|16,3|32,3> F=128", 4, 1, 16, 3, 32, 3, kWM, 128)
-    MIXED(false, 6, "6 <4,1|16,3|32,3> F=64", 4, 1, 16, 3, 32, 3, kWM, 64)
+
     MIXED(true, 6, "6 <4,1|16,3|32,3>", 4, 1, 16, 3, 32, 3)
-    MIXED(true, 6, "6 <4,1|16,3|32,3> F=128", 4, 1, 16, 3, 32, 3, kWM, 128)
-    MIXED(true, 6, "6 <4,1|16,3|32,3> F=64", 4, 1, 16, 3, 32, 3, kWM, 64)
+    MIXED(true, 5, "5 <4,1|16,3|32,3>", 4, 1, 16, 3, 32, 3)
+    MIXED(true, 8, "8 <4,1|16,3|32,3>", 4, 1, 16, 3, 32, 3)
     // TX write-back modes
     MIXED(true, 6, "6 <4,1|16,3|32,3> 16B chunks sc1", 4, 1, 16, 3, 32, 3, WM_CHUNK_SC1)
     MIXED(true, 6, "6 <4,1|16,3|32,3> 2B stores", 4, 1, 16, 3, 32, 3, WM_HALFWORD)
@@ -416,6 +415,12 @@ int copy_main(uint64_t n, int rounds)
         CK(launch_copy_fill(tx, n * stride, off, lens, src, n * plen + 64, soff, (u32)n, st,
                             nullptr, 0u, st_));
     }});
+#define CFO(O_)                                                                              \
+    vs.push_back({"fused copy + fill, occupancy " #O_, bytes, [&](hipStream_t st_) {          \
+        hipLaunchKernelGGL((k_copy_fill<32, 3, O_>), dim3((n + 7) / 8), dim3(256), 0, st_, tx,  \
+                           n * stride, off, lens, src, n * plen + 64, soff, (u32)n, st, nullptr, 0u); \
+    }});
+    CFO(6) CFO(8)
     vs.push_back({"hipMemcpy2DAsync payloads + fill", bytes, [&](hipStream_t st_) {
         CK(hipMemcpy2DAsync(tx + hl, stride, src, plen, plen, n, hipMemcpyDeviceToDevice, st_));
         CK(launch_compute_desc(tx, n * stride, off, lens, (u32)n, st, nullptr, 0u, st_));
@@ -517,7 +522,13 @@ int lro_main(uint64_t n, int rounds)
         hipLaunchKernelGGL((k_gro<U_, W_>), dim3((n + 63) / 64), dim3(256), 0, st, in, n * stride, \
                            off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd);  \
     }});
-    GROW(2, 64) GROW(4, 64)
+    GROW(2, 64)
+#define GROO(U_, W_, O_)                                                                     \
+    vs.push_back({"k_gro<" #U_ "," #W_ "," #O_ "> (window 64, max 16384)", bytes, [&](hipStream_t st) { \
+        hipLaunchKernelGGL((k_gro<U_, W_, O_>), dim3((n + 63) / 64), dim3(256), 0, st, in, n * stride, \
+                           off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd);  \
+    }});
+    GROO(2, 64, 6) GROO(2, 64, 8) GROO(1, 64, 8)
     vs.push_back({"verify (launch_verify_desc) for scale", (double)n * (L + 1), [&](hipStream_t st) {
         CK(launch_verify_desc(in, n * stride, off, lens, (u32)n, vd, 0u, st));
     }});
