@@ -277,6 +277,18 @@ int tx_main(uint64_t n, int rounds)
     TXV(16, 6, true, WM_SECTOR_SC1, 0u, "64B sector sc1")
     TXV(64, 2, true, WM_SECTOR_SC1, 0u, "64B sector sc1")
     TXV(8, 12, true, WM_SECTOR_SC1, 0u, "64B sector sc1")
+    // the bench step: TX fill of one batch, then RX verify of another
+#define STEPV(WM_, TAG)                                                                       \
+    vs.push_back({std::string("step TX+RX, TX write-back ") + TAG, cbytes + vbytes, [&](hipStream_t st) { \
+        hipLaunchKernelGGL((k_fixed<32, 3, true, false, true, WM_, true>), dim3((n + 7) / 8),   \
+                           dim3(256), 0, st, tx, stride, L, (u32)n, nullptr, nullptr, 0u);    \
+        hipLaunchKernelGGL((k_fixed<32, 3, false, false, true, WM_SECTOR_SC1, true>),          \
+                           dim3((n + 7) / 8), dim3(256), 0, st, rx, stride, L, (u32)n, v1,     \
+                           nullptr, 0u);                                                      \
+    }});
+    STEPV(WM_SECTOR_SC1, "64B sector sc1 (shipped)")
+    STEPV(WM_LINE_SC1, "128B line sc1")
+    STEPV(WM_SECTOR, "64B sector plain")
     uint8_t* scratch;
     CK(hipMalloc(&scratch, 64 * n));
 #define MULTI(K_, C_, WM_, OOP_, TAG)                                                         \
