@@ -50,6 +50,9 @@ def parse():
                    help="untimed seconds of the same kernels before the W warmup steps: "
                         "the HBM/GPU clocks take ~10 ms of load to reach steady state "
                         "(DESIGN.md §5); reported in the JSON line")
+    p.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                   help="process group for the timing barrier / max-over-ranks only (nccl = "
+                        "RCCL; gloo: rehearsing N>1 ranks on one GPU with GCS_BENCH_DEVICE)")
     p.add_argument("--no-extras", action="store_true",
                    help="skip the side measurements (C1, C3, SURVEY 8f rows, PCIe-inclusive)")
     return p.parse_args()
@@ -65,12 +68,17 @@ def dist_setup(args):
     import torch.distributed as dist
 
     world, rank, local = env_world()
+    # GCS_BENCH_DEVICE pins every rank to one device: a rehearsal of the N > 1
+    # path on a one-GPU box (with --dist-backend gloo; RCCL refuses two ranks
+    # on one GPU).  Unset, rank r uses GPU LOCAL_RANK as the driver runs it.
+    dev = int(os.environ.get("GCS_BENCH_DEVICE", local if world > 1 else 0))
+    torch.cuda.set_device(dev)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    return world, rank, local
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group("gloo")
+    return world, rank, dev
 
 
 def make_batches(ctx, n, frame_len, seed, torch):
@@ -442,7 +450,7 @@ def main():
     bad_seen = int((verdict != 0).sum())
     if bad_seen != nbad:
         raise SystemExit(f"rank {rank}: verify flagged {bad_seen} frames, {nbad} corrupted")
-    t = max_over_ranks(world, elapsed)
+    t = max_over_ranks(world, elapsed, device="cuda" if args.dist_backend == "nccl" else "cpu")
 
     rate = aggregate_rate(2 * n, world, args.steps, t)   # TX fills + RX verifies, all ranks
     value = rate / 1e9
