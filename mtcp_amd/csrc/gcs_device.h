@@ -139,12 +139,13 @@ __device__ __forceinline__ u32 group_sum(u32 x)
     return x;
 }
 
-// Value of lane SRC (0 or 1) of this lane's G-group.
+// Value of lane SRC (< G) of this lane's G-group.
 template <int G, int SRC>
 __device__ __forceinline__ u32 group_bcast(u32 x)
 {
+    static_assert(SRC < G, "source lane inside the group");
     if constexpr (G == 4) {
-        return (u32)__builtin_amdgcn_mov_dpp((int)x, SRC ? 0x55 : 0x00, 0xF, 0xF, false);
+        return (u32)__builtin_amdgcn_mov_dpp((int)x, SRC * 0x55, 0xF, 0xF, false);
     } else if constexpr (G <= 32) {
         // ds_swizzle bit mode: src lane = (lane & and_mask) | or_mask in a 32-lane half
         constexpr int and_mask = 0x1F & ~(G - 1);
@@ -509,7 +510,24 @@ __device__ __forceinline__ void epilogue(const Hdr& h, Acc a, uint8_t* __restric
         // uniform) or an ICMP frame is in this wave
         const bool want_rss = !COMPUTE && (xf.hash || xf.queue);
         const bool want_icmp = (flags & GCS_VF_ICMP) && __any(active && (h.d5 >> 24) == 1u);
-        if (want_rss || want_icmp) {
+        // ihl == 5 in every frame of the wave: the tuple sits at fixed places,
+        // chunk 1 dwords 2-3 and chunk 2 dwords 0-1 (bytes 24..39), the TCP
+        // check's word at chunk 3 -- held by group lanes 1, 2, 3: four lane
+        // reads instead of the held_hw selects and group sums
+        bool fast = false;
+        if constexpr (G >= 4)
+            fast = (want_rss || want_icmp) && __all(!active || ihl == 5u);
+        if (fast) {
+            if constexpr (G >= 4) {
+                const u32 c1z = group_bcast<G, 1>(v[0].z), c1w = group_bcast<G, 1>(v[0].w);
+                const u32 c2x = group_bcast<G, 2>(v[0].x), c2y = group_bcast<G, 2>(v[0].y);
+                g_sip = (c1z >> 16) | (c1w << 16);          // bytes 26..29
+                g_dip = (c1w >> 16) | (c2x << 16);          // bytes 30..33
+                g_l4 = (c2x >> 16) | (c2y << 16);           // bytes 34..37
+                if (COMPUTE)
+                    g_tc = group_bcast<G, 3>(v[0].x) >> 16; // bytes 50..51
+            }
+        } else if (want_rss || want_icmp) {
             g_sip = held_hw<G, U>(v, sub, 26) | (held_hw<G, U>(v, sub, 28) << 16);
             g_dip = held_hw<G, U>(v, sub, 30) | (held_hw<G, U>(v, sub, 32) << 16);
             g_l4 = held_hw<G, U>(v, sub, (int)ts) | (held_hw<G, U>(v, sub, (int)ts + 2) << 16);
