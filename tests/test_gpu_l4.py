@@ -325,3 +325,43 @@ def test_rss_arguments_rejected(torch_dev, ctx):
         ctx.set_rss(None, 0, 0)
     with pytest.raises(gpucsum.GcsError):
         ctx.set_rss(b"short", 4, 0)
+
+
+@pytest.mark.parametrize("frame_len", [100, 576, 1500])
+def test_fixed_classify_ip_options_mixed_waves(torch_dev, ctx, O, frame_len):
+    """RSS tuple reads: waves whose frames all have ihl = 5 read the tuple at
+    fixed lanes; a wave holding one frame with IP options takes the general
+    gather.  Options on a whole run of frames (whole waves) and on scattered
+    single frames (mixed waves), all against the oracle."""
+    t = torch_dev
+    n = 8192
+    buf, stride = synth.fixed_frames(n, frame_len, seed=frame_len + 5)
+    off = np.arange(n, dtype=np.uint64) * stride
+    lens = np.full(n, frame_len, dtype=np.uint16)
+    rng = np.random.default_rng(frame_len)
+    opt = rng.random(n) < 0.02
+    opt[1024:1152] = True
+    with_opts = 0
+    for i in np.nonzero(opt)[0]:
+        ihl = int(rng.integers(6, 16))
+        if 14 + 4 * ihl + 20 > frame_len:
+            continue
+        o = int(off[i])
+        buf[o + 14] = 0x40 | ihl
+        buf[o + 14 + 4 * ihl + 12] = 5 << 4
+        with_opts += 1
+    O.compute_batch(buf, off, lens)
+    ctx.set_rss(None, 16, 0)
+    try:
+        rvd, rh, rq = O.classify_fixed(buf.copy(), stride, frame_len, n, 16, 0)
+        v = zeros(t, n, t.uint8)
+        h = zeros(t, n, t.int32)
+        q = zeros(t, n, t.int16)
+        ctx.classify_fixed(dev(t, buf), stride, frame_len, n, v, h, q)
+        ctx.sync()
+        np.testing.assert_array_equal(host(v), rvd)
+        np.testing.assert_array_equal(host(h).view(np.uint32), rh)
+        np.testing.assert_array_equal(host(q).view(np.uint16), rq)
+        assert (rvd == 0).all() and with_opts > 100
+    finally:
+        ctx.set_rss(None, 1, 0)
