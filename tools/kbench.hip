@@ -289,6 +289,24 @@ int tx_main(uint64_t n, int rounds)
     STEPV(WM_SECTOR_SC1, "64B sector sc1 (shipped)")
     STEPV(WM_LINE_SC1, "128B line sc1")
     STEPV(WM_SECTOR, "64B sector plain")
+    STEPV(WM_SECTOR_SC01, "64B sector sc0 sc1")
+    STEPV(WM_SECTOR_NT, "64B sector nt")
+    vs.push_back({"step RX then TX (sector sc1)", cbytes + vbytes, [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_fixed<32, 3, false, false, true, WM_SECTOR_SC1, true>),
+                           dim3((n + 7) / 8), dim3(256), 0, st, rx, stride, L, (u32)n, v1,
+                           nullptr, 0u);
+        hipLaunchKernelGGL((k_fixed<32, 3, true, false, true, WM_SECTOR_SC1, true>),
+                           dim3((n + 7) / 8), dim3(256), 0, st, tx, stride, L, (u32)n, nullptr,
+                           nullptr, 0u);
+    }});
+    vs.push_back({"step TX + pure-fold TX on rx (no writes at all)", 2 * cbytes, [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_fixed<32, 3, true, false, true, WM_SECTOR_SC1, true>),
+                           dim3((n + 7) / 8), dim3(256), 0, st, tx, stride, L, (u32)n, nullptr,
+                           nullptr, (u32)GCS_CF_NO_INPLACE);
+        hipLaunchKernelGGL((k_fixed<32, 3, false, false, true, WM_SECTOR_SC1, true>),
+                           dim3((n + 7) / 8), dim3(256), 0, st, rx, stride, L, (u32)n, v1,
+                           nullptr, 0u);
+    }});
     uint8_t* scratch;
     CK(hipMalloc(&scratch, 64 * n));
 #define MULTI(K_, C_, WM_, OOP_, TAG)                                                         \
