@@ -10,14 +10,19 @@
  * ABI) only when io_module.h itself has not been included, so mTCP sources
  * can include both headers.
  *
- * gpucsum_module_func is a DECORATOR around an inner NIC module (dpdk,
- * netmap, psio, or any io_module_func):
+ * gpucsum_module_func is a DECORATOR around an inner NIC module (dpdk, onvm,
+ * psio, netmap, or any io_module_func):
  *   recv_pkts   inner recv_pkts, then one batched RX verify of the burst on the
  *               GPU (replaces ip_in.c:28-37 + tcp_in.c:1224-1241 per frame)
  *   get_rptr    NULL for frames whose verdict mTCP would count as an ERROR --
  *               exactly how dpdk_get_rptr surfaces bad HW checksums
- *               (dpdk_module.c:536-542); core.c:794-799 counts rx_errors
+ *               (dpdk_module.c:536-542); core.c:794-799 counts rx_errors.
+ *               For every other frame the inner get_rptr is called again with
+ *               the same index, so per-index inner state follows mTCP's walk
+ *               (DPDK's cur_rx_m, dpdk_module.c:543-545, which the ENABLELRO
+ *               gather PKT_RX_TCP_LROSEG reads, :856-857)
  *   get_wptr    inner get_wptr; the buffer is queued for the TX fill
+ *               (GPUCSUM_INNER_TX_EAGER inners: a shadow buffer, see below)
  *   send_pkts   one batched TX fill of the queued frames on the GPU (replaces
  *               ip_out.c:155-173 + tcp_out.c:323-333), then inner send_pkts
  *   dev_ioctl   0 ("done by the device") for PKT_TX_IP_CSUM, PKT_TX_TCPIP_CSUM,
@@ -27,6 +32,28 @@
  *   others      forwarded unchanged
  * Build mTCP WITHOUT -DDISABLE_HWCSUM so that ip_in.c / ip_out.c / tcp_in.c /
  * tcp_out.c consult dev_ioctl (configure.ac:119-125, Makefile.in:63-65).
+ *
+ * Inner-module shapes (gpucsum_set_inner_caps):
+ *   in place (default: dpdk, onvm, psio)  a get_wptr buffer stays put until the
+ *               inner send_pkts (dpdk_module.c:399-436, onvm_module.c:276-309,
+ *               pslib.c:132-156), so frames are filled where mTCP wrote them.
+ *   GPUCSUM_INNER_TX_EAGER (netmap)  the inner get_wptr transmits the previous
+ *               frame and hands out ONE reused buffer (netmap_module.c:149-160).
+ *               mTCP then writes into a decorator-owned shadow slot; at flush
+ *               the shadow frames are filled in one GPU batch and only then
+ *               copied, in order, into inner get_wptr buffers.  set_inner
+ *               selects it by itself when the inner module IS mTCP's
+ *               netmap_module_func (weak reference).
+ *   GPUCSUM_INNER_RX_CHAINED (ENABLELRO)  the inner may return multi-segment
+ *               frames whose *len is the chain's pkt_len (dpdk_module.c:530,
+ *               855-881).  Frames longer than rx_seg_max (default 1514 = one
+ *               MTU frame; a longer frame is an LRO chain, the same size rule
+ *               tcp_ring_buffer.c:18 applies) are not read by the GPU: they are
+ *               left to the inner module's own checks, as the NIC did them.
+ * Not supported: an inner get_rptr that is not idempotent per index, e.g.
+ * DPDK built with IP_DEFRAG (dpdk_module.c:527-529 reassembles on each call);
+ * a frame whose pointer or length changes between the burst's verify and
+ * mTCP's get_rptr is dropped and counted in rx_rptr_changed.
  *
  * RSS check (optional): with RSS configured (gpucsum_set_rss,
  * or GPUCSUM_RSS_QUEUES=<n> [GPUCSUM_RSS_I40E=1] in the environment) each RX
@@ -84,11 +111,23 @@ typedef struct io_module_func {
 /* The decorator vtable (mTCP: `io = gpucsum` once AssignIOModule knows it). */
 extern io_module_func gpucsum_module_func;
 
-/* Set the inner module the decorator wraps.  Call before load_module(). */
+/* Set the inner module the decorator wraps.  Call before load_module().
+ * Resets the inner caps (GPUCSUM_INNER_TX_EAGER if inner is netmap_module_func). */
 int gpucsum_set_inner(io_module_func *inner);
+/* The inner module (NULL if none): for mTCP's module-identity checks, e.g. the
+ * ENABLELRO gather test at tcp_ring_buffer.c:18. */
+io_module_func *gpucsum_get_inner(void);
+
+#define GPUCSUM_INNER_TX_EAGER   0x1u  /* get_wptr may transmit / reuse earlier buffers */
+#define GPUCSUM_INNER_RX_CHAINED 0x2u  /* get_rptr may return multi-segment (LRO) frames */
+/* Shape of the inner module; call after gpucsum_set_inner, before init_handle.
+ * rx_seg_max: longest single-segment frame (0 = 1514). */
+int gpucsum_set_inner_caps(uint32_t caps, uint32_t rx_seg_max);
 
 #define GPUCSUM_MAX_IFS    16     /* MAX_DEVICES, io_engine/include/ps.h:4 */
-#define GPUCSUM_MAX_BURST  8192   /* frames per recv_pkts / per send_pkts queue */
+#define GPUCSUM_MAX_BURST  8192   /* frames per GPU batch: a larger recv_pkts burst is
+                                     verified whole (in several batches); a TX queue
+                                     is filled and kept when it reaches this size */
 
 /* Per-thread counters of the calling context (0 = ok, GCS_E* otherwise). */
 struct gpucsum_stats {
@@ -100,6 +139,9 @@ struct gpucsum_stats {
 	uint64_t gpu_failures;   /* GPU calls that failed (frames then dropped/unsent)*/
 	uint64_t rx_foreign;     /* RSS on: ACCEPT frames steered to another queue    */
 	int      device;         /* HIP device of this context                       */
+	uint64_t rx_inner;       /* RX_CHAINED: chained frames left to the inner's checks */
+	uint64_t rx_rptr_changed;/* inner get_rptr changed a frame after its verify   */
+	uint64_t tx_inner_full;  /* TX_EAGER: inner get_wptr had no buffer: frame lost  */
 };
 int gpucsum_get_stats(struct mtcp_thread_context *ctx, struct gpucsum_stats *out);
 

@@ -17,6 +17,7 @@
 #include <memory>
 #include <mutex>
 #include <new>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -34,6 +35,36 @@ int hip_fail(hipError_t e, const char* what)
     if (e == hipErrorNoDevice || e == hipErrorInvalidDevice)
         return GCS_ENODEV;
     return GCS_EHIP;
+}
+
+// No C++ exception may cross the C ABI (mtcp_gpucsum.h: "no C++ exceptions
+// cross the ABI"): every extern "C" entry point is a function-try-block whose
+// handler maps the in-flight exception to a status code.
+int exception_code() noexcept
+{
+    try {
+        throw;
+    } catch (const std::bad_alloc&) {
+        std::snprintf(g_hip_err, sizeof g_hip_err, "C++ exception: std::bad_alloc");
+        return GCS_ENOMEM;
+    } catch (const std::exception& e) {
+        std::snprintf(g_hip_err, sizeof g_hip_err, "C++ exception: %s", e.what());
+        return GCS_EHIP;
+    } catch (...) {
+        std::snprintf(g_hip_err, sizeof g_hip_err, "C++ exception (unknown type)");
+        return GCS_EHIP;
+    }
+}
+
+#define GCS_CATCH \
+    catch (...) { return exception_code(); }
+
+// Test-only fault injection (tests/test_gpu_host.py): GCS_FAULT_INJECT names
+// the failure to simulate.  Read per use; unset in production.
+bool fault(const char* what)
+{
+    const char* e = std::getenv("GCS_FAULT_INJECT");
+    return e && std::strcmp(e, what) == 0;
 }
 
 #define HIP_TRY(call)                                     \
@@ -104,7 +135,7 @@ class GatherPool {
 
     void run(uint32_t total, uint32_t parts, const std::function<void(uint32_t, uint32_t)>& fn)
     {
-        if (workers_.empty())
+        if (!started_)
             start();
         {
             std::lock_guard<std::mutex> lk(m_);
@@ -130,10 +161,21 @@ class GatherPool {
     }
 
   private:
+    // Spawn the helpers.  A thread that cannot be created is not an error:
+    // the calling thread always works through every part itself (work()), so
+    // fewer helpers only means less parallel copying.
     void start()
     {
-        for (int i = 1; i < threads(); i++)
-            workers_.emplace_back([this] { loop(); });
+        started_ = true;
+        for (int i = 1; i < threads(); i++) {
+            try {
+                if (fault("gather_thread"))
+                    throw std::system_error(std::make_error_code(std::errc::resource_unavailable_try_again));
+                workers_.emplace_back([this] { loop(); });
+            } catch (const std::system_error&) {
+                break;
+            }
+        }
     }
 
     void loop()
@@ -181,6 +223,7 @@ class GatherPool {
     std::atomic<uint32_t> next_{0};
     uint64_t gen_ = 0;
     bool stop_ = false;
+    bool started_ = false;
 };
 
 }  // namespace
@@ -208,8 +251,11 @@ struct gcs_ctx {
             fn(0, count);
             return;
         }
-        if (!pool)
+        if (!pool) {
+            if (fault("gather_alloc"))
+                throw std::bad_alloc();
             pool.reset(new GatherPool());
+        }
         pool->run(count, (uint32_t)std::min<uint64_t>(4ull * t, count), fn);
     }
 };
@@ -373,6 +419,27 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
 
     auto frame_ptr = [&](uint32_t i) -> uint8_t* { return ptrs ? ptrs[i] : base + off[i]; };
 
+    // A frame that cannot fit one staging slot is refused before anything is
+    // launched, so an ERANGE never leaves part of the batch processed.
+    for (uint32_t i = 0; i < n; i++)
+        if (frame_ptr(i) && (len[i] + kSlotAlign - 1) / kSlotAlign * kSlotAlign > ctx->max_bytes)
+            return GCS_ERANGE;
+
+    // Whatever way this call ends (error return, exception), no slot may stay
+    // marked busy: a later call would otherwise drain this call's chunk into
+    // its own output arrays.  On the normal path drain() has cleared them.
+    struct SlotReset {
+        gcs_ctx* c;
+        ~SlotReset()
+        {
+            for (auto& s : c->slot)
+                if (s.busy) {
+                    (void)hipEventSynchronize(s.done);
+                    s.busy = false;
+                }
+        }
+    } slot_reset{ctx};
+
     // span mode needs the whole referenced range pinned
     bool pinned = false;
     if (base) {
@@ -517,6 +584,8 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
         s.busy = true;
         next += cnt;
         k++;
+        if (k == 1 && next < n && fault("second_chunk"))   // a HIP failure mid-batch
+            return hip_fail(hipErrorLaunchFailure, "injected before chunk 2");
     }
     for (auto& s : ctx->slot) {
         int rc = drain(s);
@@ -557,7 +626,7 @@ const char* gcs_strerror(int code)
 const char* gcs_last_hip_error(void) { return g_hip_err; }
 
 int gcs_device_count(int* count)
-{
+try {
     if (!count)
         return GCS_EINVAL;
     int c = 0;
@@ -568,10 +637,10 @@ int gcs_device_count(int* count)
     }
     *count = c;
     return GCS_OK;
-}
+} GCS_CATCH
 
 int gcs_ctx_create(gcs_ctx** out, int device, uint32_t max_frames, uint64_t max_bytes)
-{
+try {
     if (!out)
         return GCS_EINVAL;
     *out = nullptr;
@@ -611,10 +680,10 @@ int gcs_ctx_create(gcs_ctx** out, int device, uint32_t max_frames, uint64_t max_
     }
     *out = ctx;
     return GCS_OK;
-}
+} GCS_CATCH
 
 int gcs_ctx_destroy(gcs_ctx* ctx)
-{
+try {
     if (!ctx)
         return GCS_EINVAL;
     {
@@ -632,84 +701,84 @@ int gcs_ctx_destroy(gcs_ctx* ctx)
     }
     delete ctx;
     return GCS_OK;
-}
+} GCS_CATCH
 
 int gcs_ctx_device(const gcs_ctx* ctx, int* device)
-{
+try {
     if (!ctx || !device)
         return GCS_EINVAL;
     *device = ctx->device;
     return GCS_OK;
-}
+} GCS_CATCH
 
 int gcs_ctx_stream(const gcs_ctx* ctx, void** stream)
-{
+try {
     if (!ctx || !stream)
         return GCS_EINVAL;
     *stream = ctx->stream;
     return GCS_OK;
-}
+} GCS_CATCH
 
 int gcs_sync(gcs_ctx* ctx)
-{
+try {
     if (!ctx)
         return GCS_EINVAL;
     DeviceGuard g(ctx->device);
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     return GCS_OK;
-}
+} GCS_CATCH
 
 int gcs_host_alloc(void** p, uint64_t bytes)
-{
+try {
     if (!p)
         return GCS_EINVAL;
     HIP_TRY(hipHostMalloc(p, bytes, hipHostMallocDefault));
     return GCS_OK;
-}
+} GCS_CATCH
 
 int gcs_host_free(void* p)
-{
+try {
     HIP_TRY(hipHostFree(p));
     return GCS_OK;
-}
+} GCS_CATCH
 
 int gcs_host_register(void* p, uint64_t bytes)
-{
+try {
     if (!p || bytes == 0)
         return GCS_EINVAL;
     HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterDefault));
     return GCS_OK;
-}
+} GCS_CATCH
 
 int gcs_host_unregister(void* p)
-{
+try {
     if (!p)
         return GCS_EINVAL;
     HIP_TRY(hipHostUnregister(p));
     return GCS_OK;
-}
+} GCS_CATCH
 
 int gcs_dev_alloc(gcs_ctx* ctx, void** p, uint64_t bytes)
-{
+try {
     if (!ctx || !p)
         return GCS_EINVAL;
     DeviceGuard g(ctx->device);
     HIP_TRY(hipMalloc(p, bytes));
     return GCS_OK;
-}
+} GCS_CATCH
 
 int gcs_dev_free(gcs_ctx* ctx, void* p)
-{
+try {
     if (!ctx)
         return GCS_EINVAL;
     DeviceGuard g(ctx->device);
     HIP_TRY(hipFree(p));
     return GCS_OK;
-}
+} GCS_CATCH
 
 int gcs_verify_fixed_dev(gcs_ctx* ctx, uint8_t* d_frames, uint64_t stride, uint32_t frame_len,
                          uint32_t n, uint8_t* d_verdict, uint32_t flags, void* stream)
-{
+try {
     if (!ctx || (n && (!d_frames || !d_verdict)) || stride % 16 || stride == 0 ||
         (frame_len + 15u) / 16u * 16u > stride)
         return GCS_EINVAL;
@@ -719,12 +788,12 @@ int gcs_verify_fixed_dev(gcs_ctx* ctx, uint8_t* d_frames, uint64_t stride, uint3
     HIP_TRY(gcs::launch_verify_fixed(d_frames, stride, frame_len, n, d_verdict, flags,
                                      pick_stream(ctx, stream)));
     return GCS_OK;
-}
+} GCS_CATCH
 
 int gcs_compute_fixed_dev(gcs_ctx* ctx, uint8_t* d_frames, uint64_t stride, uint32_t frame_len,
                           uint32_t n, uint8_t* d_status, uint32_t* d_csums, uint32_t flags,
                           void* stream)
-{
+try {
     if (!ctx || (n && !d_frames) || stride % 16 || stride == 0 ||
         (frame_len + 15u) / 16u * 16u > stride)
         return GCS_EINVAL;
@@ -734,12 +803,12 @@ int gcs_compute_fixed_dev(gcs_ctx* ctx, uint8_t* d_frames, uint64_t stride, uint
     HIP_TRY(gcs::launch_compute_fixed(d_frames, stride, frame_len, n, d_status, d_csums, flags,
                                       pick_stream(ctx, stream)));
     return GCS_OK;
-}
+} GCS_CATCH
 
 int gcs_verify_dev(gcs_ctx* ctx, uint8_t* d_frames, uint64_t frames_bytes, const uint64_t* d_off,
                    const uint16_t* d_len, uint32_t n, uint8_t* d_verdict, uint32_t flags,
                    void* stream)
-{
+try {
     if (!ctx || (n && (!d_frames || !d_off || !d_len || !d_verdict)))
         return GCS_EINVAL;
     if (n == 0)
@@ -748,12 +817,12 @@ int gcs_verify_dev(gcs_ctx* ctx, uint8_t* d_frames, uint64_t frames_bytes, const
     HIP_TRY(gcs::launch_verify_desc(d_frames, frames_bytes, d_off, d_len, n, d_verdict, flags,
                                     pick_stream(ctx, stream)));
     return GCS_OK;
-}
+} GCS_CATCH
 
 int gcs_compute_dev(gcs_ctx* ctx, uint8_t* d_frames, uint64_t frames_bytes, const uint64_t* d_off,
                     const uint16_t* d_len, uint32_t n, uint8_t* d_status, uint32_t* d_csums,
                     uint32_t flags, void* stream)
-{
+try {
     if (!ctx || (n && (!d_frames || !d_off || !d_len)))
         return GCS_EINVAL;
     if (n == 0)
@@ -762,12 +831,12 @@ int gcs_compute_dev(gcs_ctx* ctx, uint8_t* d_frames, uint64_t frames_bytes, cons
     HIP_TRY(gcs::launch_compute_desc(d_frames, frames_bytes, d_off, d_len, n, d_status, d_csums,
                                      flags, pick_stream(ctx, stream)));
     return GCS_OK;
-}
+} GCS_CATCH
 
 int gcs_tcp_checksum_dev(gcs_ctx* ctx, const uint8_t* d_buf, uint64_t buf_bytes,
                          const uint64_t* d_off, const uint16_t* d_len, const uint32_t* d_saddr,
                          const uint32_t* d_daddr, uint32_t n, uint16_t* d_out, void* stream)
-{
+try {
     if (!ctx || (n && (!d_buf || !d_off || !d_len || !d_saddr || !d_daddr || !d_out)))
         return GCS_EINVAL;
     if (n == 0)
@@ -776,12 +845,12 @@ int gcs_tcp_checksum_dev(gcs_ctx* ctx, const uint8_t* d_buf, uint64_t buf_bytes,
     HIP_TRY(gcs::launch_tcp_fn(d_buf, buf_bytes, d_off, d_len, d_saddr, d_daddr, n, d_out,
                                pick_stream(ctx, stream)));
     return GCS_OK;
-}
+} GCS_CATCH
 
 int gcs_ip_checksum_dev(gcs_ctx* ctx, const uint8_t* d_buf, uint64_t buf_bytes,
                         const uint64_t* d_off, const uint8_t* d_ihl, uint32_t n, uint16_t* d_out,
                         void* stream)
-{
+try {
     if (!ctx || (n && (!d_buf || !d_off || !d_ihl || !d_out)))
         return GCS_EINVAL;
     if (n == 0)
@@ -789,13 +858,13 @@ int gcs_ip_checksum_dev(gcs_ctx* ctx, const uint8_t* d_buf, uint64_t buf_bytes,
     DeviceGuard g(ctx->device);
     HIP_TRY(gcs::launch_ip_fn(d_buf, buf_bytes, d_off, d_ihl, n, d_out, pick_stream(ctx, stream)));
     return GCS_OK;
-}
+} GCS_CATCH
 
 int gcs_compute_copy_dev(gcs_ctx* ctx, uint8_t* d_frames, uint64_t frames_bytes,
                          const uint64_t* d_off, const uint16_t* d_len, const uint8_t* d_src,
                          uint64_t src_bytes, const uint64_t* d_src_off, uint32_t n,
                          uint8_t* d_status, uint32_t* d_csums, uint32_t flags, void* stream)
-{
+try {
     if (!ctx || flags != 0 || (n && (!d_frames || !d_off || !d_len || !d_src || !d_src_off)))
         return GCS_EINVAL;
     if (n == 0)
@@ -805,13 +874,13 @@ int gcs_compute_copy_dev(gcs_ctx* ctx, uint8_t* d_frames, uint64_t frames_bytes,
                                   d_src_off, n, d_status, d_csums, flags,
                                   pick_stream(ctx, stream)));
     return GCS_OK;
-}
+} GCS_CATCH
 
 int gcs_gro_dev(gcs_ctx* ctx, const uint8_t* d_in, uint64_t in_bytes, const uint64_t* d_off,
                 const uint16_t* d_len, const uint8_t* d_verdict, uint32_t n, uint32_t window,
                 uint32_t max_len, uint8_t* d_out, uint64_t out_bytes, uint64_t* d_out_off,
                 uint16_t* d_out_len, uint32_t* d_head, void* stream)
-{
+try {
     if (!ctx || window == 0 || window > 256 || max_len > 65535 ||
         (n && (!d_in || !d_off || !d_len || !d_verdict || !d_out || !d_out_off || !d_out_len ||
                !d_head)))
@@ -822,12 +891,12 @@ int gcs_gro_dev(gcs_ctx* ctx, const uint8_t* d_in, uint64_t in_bytes, const uint
     HIP_TRY(gcs::launch_gro(d_in, in_bytes, d_off, d_len, d_verdict, n, window, max_len, d_out,
                             out_bytes, d_out_off, d_out_len, d_head, pick_stream(ctx, stream)));
     return GCS_OK;
-}
+} GCS_CATCH
 
 int gcs_icmp_checksum_dev(gcs_ctx* ctx, const uint8_t* d_buf, uint64_t buf_bytes,
                           const uint64_t* d_off, const uint16_t* d_len, uint32_t n,
                           uint16_t* d_out, void* stream)
-{
+try {
     if (!ctx || (n && (!d_buf || !d_off || !d_len || !d_out)))
         return GCS_EINVAL;
     if (n == 0)
@@ -836,11 +905,11 @@ int gcs_icmp_checksum_dev(gcs_ctx* ctx, const uint8_t* d_buf, uint64_t buf_bytes
     HIP_TRY(gcs::launch_icmp_fn(d_buf, buf_bytes, d_off, d_len, n, d_out,
                                 pick_stream(ctx, stream)));
     return GCS_OK;
-}
+} GCS_CATCH
 
 int gcs_ctx_set_rss(gcs_ctx* ctx, const uint8_t* key, uint32_t key_len, uint32_t num_queues,
                     int endian_check)
-{
+try {
     if (!ctx || num_queues == 0 || num_queues > 0xFFFFu || (key && key_len < 16))
         return GCS_EINVAL;
     uint8_t k[40];
@@ -850,12 +919,12 @@ int gcs_ctx_set_rss(gcs_ctx* ctx, const uint8_t* key, uint32_t key_len, uint32_t
     // the parameters travel by value in each launch: no device state to fence
     set_rss_params(ctx, k, num_queues, endian_check ? 1u : 0u);
     return GCS_OK;
-}
+} GCS_CATCH
 
 int gcs_classify_fixed_dev(gcs_ctx* ctx, uint8_t* d_frames, uint64_t stride, uint32_t frame_len,
                            uint32_t n, uint8_t* d_verdict, uint32_t* d_hash, uint16_t* d_queue,
                            uint32_t flags, void* stream)
-{
+try {
     if (!ctx || (n && (!d_frames || !d_verdict)) || stride % 16 || stride == 0 ||
         (frame_len + 15u) / 16u * 16u > stride)
         return GCS_EINVAL;
@@ -865,13 +934,13 @@ int gcs_classify_fixed_dev(gcs_ctx* ctx, uint8_t* d_frames, uint64_t stride, uin
     HIP_TRY(gcs::launch_classify_fixed(d_frames, stride, frame_len, n, d_verdict, flags,
                                        rss_ext(ctx, d_hash, d_queue), pick_stream(ctx, stream)));
     return GCS_OK;
-}
+} GCS_CATCH
 
 int gcs_classify_dev(gcs_ctx* ctx, uint8_t* d_frames, uint64_t frames_bytes,
                      const uint64_t* d_off, const uint16_t* d_len, uint32_t n,
                      uint8_t* d_verdict, uint32_t* d_hash, uint16_t* d_queue, uint32_t flags,
                      void* stream)
-{
+try {
     if (!ctx || (n && (!d_frames || !d_off || !d_len || !d_verdict)))
         return GCS_EINVAL;
     if (n == 0)
@@ -880,12 +949,12 @@ int gcs_classify_dev(gcs_ctx* ctx, uint8_t* d_frames, uint64_t frames_bytes,
     HIP_TRY(gcs::launch_classify_desc(d_frames, frames_bytes, d_off, d_len, n, d_verdict, flags,
                                       rss_ext(ctx, d_hash, d_queue), pick_stream(ctx, stream)));
     return GCS_OK;
-}
+} GCS_CATCH
 
 int gcs_rss_dev(gcs_ctx* ctx, const uint32_t* d_sip, const uint32_t* d_dip, const uint16_t* d_sp,
                 const uint16_t* d_dp, uint32_t n, uint32_t* d_hash, uint16_t* d_queue,
                 void* stream)
-{
+try {
     if (!ctx || (n && (!d_sip || !d_dip || !d_sp || !d_dp || (!d_hash && !d_queue))))
         return GCS_EINVAL;
     if (n == 0)
@@ -894,48 +963,48 @@ int gcs_rss_dev(gcs_ctx* ctx, const uint32_t* d_sip, const uint32_t* d_dip, cons
     HIP_TRY(gcs::launch_rss_fn(d_sip, d_dip, d_sp, d_dp, n, rss_ext(ctx, d_hash, d_queue),
                                pick_stream(ctx, stream)));
     return GCS_OK;
-}
+} GCS_CATCH
 
 int gcs_classify(gcs_ctx* ctx, uint8_t* frames, const uint64_t* off, const uint16_t* len,
                  uint32_t n, uint8_t* verdict, uint32_t* hash, uint16_t* queue, uint32_t flags)
-{
+try {
     if (!hash && !queue)
         return GCS_EINVAL;
     return run_host_batch(ctx, frames, off, nullptr, len, n, verdict, nullptr, flags, false,
                           hash, queue);
-}
+} GCS_CATCH
 
 int gcs_classify_ptrs(gcs_ctx* ctx, uint8_t* const* pkts, const uint16_t* len, uint32_t n,
                       uint8_t* verdict, uint32_t* hash, uint16_t* queue, uint32_t flags)
-{
+try {
     if (!hash && !queue)
         return GCS_EINVAL;
     return run_host_batch(ctx, nullptr, nullptr, pkts, len, n, verdict, nullptr, flags, false,
                           hash, queue);
-}
+} GCS_CATCH
 
 int gcs_verify(gcs_ctx* ctx, uint8_t* frames, const uint64_t* off, const uint16_t* len,
                uint32_t n, uint8_t* verdict, uint32_t flags)
-{
+try {
     return run_host_batch(ctx, frames, off, nullptr, len, n, verdict, nullptr, flags, false);
-}
+} GCS_CATCH
 
 int gcs_compute(gcs_ctx* ctx, uint8_t* frames, const uint64_t* off, const uint16_t* len,
                 uint32_t n, uint8_t* status, uint32_t* csums)
-{
+try {
     return run_host_batch(ctx, frames, off, nullptr, len, n, status, csums, 0u, true);
-}
+} GCS_CATCH
 
 int gcs_verify_ptrs(gcs_ctx* ctx, uint8_t* const* pkts, const uint16_t* len, uint32_t n,
                     uint8_t* verdict, uint32_t flags)
-{
+try {
     return run_host_batch(ctx, nullptr, nullptr, pkts, len, n, verdict, nullptr, flags, false);
-}
+} GCS_CATCH
 
 int gcs_compute_ptrs(gcs_ctx* ctx, uint8_t* const* pkts, const uint16_t* len, uint32_t n,
                      uint8_t* status, uint32_t* csums)
-{
+try {
     return run_host_batch(ctx, nullptr, nullptr, pkts, len, n, status, csums, 0u, true);
-}
+} GCS_CATCH
 
 }  // extern "C"

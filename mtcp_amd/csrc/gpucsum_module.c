@@ -15,6 +15,10 @@
  * context that cannot reach its GPU exits at init_handle like the reference's
  * modules do (dpdk_module.c:243-247), and a failing batch is reported on
  * stderr and its frames are dropped.
+ *
+ * Inner-module shapes (gpucsum_io_module.h): frames are filled in place for
+ * modules whose TX buffers stay put until send_pkts (dpdk, onvm, psio), and
+ * through shadow slots for modules whose get_wptr transmits (netmap).
  */
 #include <pthread.h>
 #include <stdio.h>
@@ -26,13 +30,18 @@
 
 #define GPUCSUM_MAX_THREADS 256
 #define GPUCSUM_STAGE_BYTES_PER_FRAME 2048   /* MAX_PKT_SIZE, mtcp.h:52 */
+#define GPUCSUM_SHADOW_ROOM 2048             /* MAX_PKT_SIZE: mTCP never asks for more */
+#define GPUCSUM_DEFAULT_SEG_MAX 1514         /* ETHERNET_HEADER_LEN + 1500 B MTU */
+#define V_INNER 0xFE                         /* RX_CHAINED frame: inner's own checks */
 
 struct rx_if {
 	int32_t n;
-	uint8_t *ptr[GPUCSUM_MAX_BURST];
-	uint16_t len[GPUCSUM_MAX_BURST];
-	uint8_t verdict[GPUCSUM_MAX_BURST];
-	uint16_t queue[GPUCSUM_MAX_BURST];   /* RSS on */
+	uint32_t cap;
+	uint8_t **ptr;
+	uint16_t *len;      /* length seen at recv_pkts            */
+	uint16_t *glen;     /* length the GPU folds (0 = skip)      */
+	uint8_t *verdict;
+	uint16_t *queue;    /* RSS on */
 };
 
 struct tx_if {
@@ -40,6 +49,7 @@ struct tx_if {
 	uint8_t *ptr[GPUCSUM_MAX_BURST];
 	uint16_t len[GPUCSUM_MAX_BURST];
 	uint8_t status[GPUCSUM_MAX_BURST];
+	uint8_t *shadow;    /* TX_EAGER: GPUCSUM_MAX_BURST rooms of GPUCSUM_SHADOW_ROOM */
 };
 
 struct gthr {
@@ -52,7 +62,13 @@ struct gthr {
 	int own_queue;
 };
 
+/* mTCP's netmap module, when the decorator is linked into mTCP (weak: absent
+ * from other programs).  Its get_wptr transmits, netmap_module.c:149-160. */
+extern io_module_func netmap_module_func __attribute__((weak));
+
 static io_module_func *g_inner;
+static uint32_t g_caps;
+static uint32_t g_seg_max = GPUCSUM_DEFAULT_SEG_MAX;
 static struct gthr *g_table[GPUCSUM_MAX_THREADS];
 static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER;
 static int g_next_ordinal;
@@ -63,6 +79,23 @@ int gpucsum_set_inner(io_module_func *inner)
 	if (!inner || inner == &gpucsum_module_func)
 		return GCS_EINVAL;
 	g_inner = inner;
+	g_caps = (&netmap_module_func && inner == &netmap_module_func) ? GPUCSUM_INNER_TX_EAGER : 0;
+	g_seg_max = GPUCSUM_DEFAULT_SEG_MAX;
+	return GCS_OK;
+}
+
+io_module_func *gpucsum_get_inner(void)
+{
+	return g_inner;
+}
+
+int gpucsum_set_inner_caps(uint32_t caps, uint32_t rx_seg_max)
+{
+	if (!g_inner || (caps & ~(GPUCSUM_INNER_TX_EAGER | GPUCSUM_INNER_RX_CHAINED)) ||
+	    rx_seg_max > 65535)
+		return GCS_EINVAL;
+	g_caps = caps;
+	g_seg_max = rx_seg_max ? rx_seg_max : GPUCSUM_DEFAULT_SEG_MAX;
 	return GCS_OK;
 }
 
@@ -167,17 +200,31 @@ static void gpucsum_release_pkt(struct mtcp_thread_context *ctx, int ifidx,
 
 static struct tx_if *txq(struct gthr *g, int ifidx)
 {
+	struct tx_if *q;
+
 	if (ifidx < 0 || ifidx >= GPUCSUM_MAX_IFS)
 		return NULL;
-	if (!g->tx[ifidx])
-		g->tx[ifidx] = calloc(1, sizeof(struct tx_if));
-	return g->tx[ifidx];
+	if (g->tx[ifidx])
+		return g->tx[ifidx];
+	q = calloc(1, sizeof(struct tx_if));
+	if (q && (g_caps & GPUCSUM_INNER_TX_EAGER)) {
+		q->shadow = malloc((size_t)GPUCSUM_MAX_BURST * GPUCSUM_SHADOW_ROOM);
+		if (!q->shadow) {
+			free(q);
+			q = NULL;
+		}
+	}
+	g->tx[ifidx] = q;
+	return q;
 }
 
 /* TX fill of every queued frame of one interface (ip_out.c:155-173 and
- * tcp_out.c:323-333, batched). */
-static void flush_tx(struct gthr *g, struct tx_if *q)
+ * tcp_out.c:323-333, batched).  TX_EAGER: the queued frames are shadow slots;
+ * once filled they go, in order, into inner get_wptr buffers (the inner may
+ * transmit the previous one on each call, netmap_module.c:155-156). */
+static void flush_tx(struct gthr *g, int ifidx, struct tx_if *q)
 {
+	uint32_t k;
 	int rc;
 
 	if (!q || q->n == 0)
@@ -191,6 +238,19 @@ static void flush_tx(struct gthr *g, struct tx_if *q)
 		g->st.tx_frames += q->n;
 		g->st.tx_batches++;
 	}
+	if (q->shadow) {
+		for (k = 0; k < q->n; k++) {
+			uint8_t *p;
+			if (rc)
+				break;              /* unfilled frames never reach the wire */
+			p = g_inner->get_wptr(g->ctx, ifidx, q->len[k]);
+			if (!p) {
+				g->st.tx_inner_full += q->n - k;
+				break;
+			}
+			memcpy(p, q->ptr[k], q->len[k]);
+		}
+	}
 	q->n = 0;
 }
 
@@ -198,15 +258,24 @@ static uint8_t *gpucsum_get_wptr(struct mtcp_thread_context *ctx, int ifidx, uin
 {
 	struct gthr *g = lookup(ctx);
 	struct tx_if *q;
-	uint8_t *p = g_inner->get_wptr(ctx, ifidx, len);
+	uint8_t *p;
 
-	if (!p || !g)
-		return p;
+	if (!g)
+		return g_inner->get_wptr(ctx, ifidx, len);
 	q = txq(g, ifidx);
-	if (!q)
-		return p;
+	if (!q)   /* no queue: nothing would fill this frame, so give no buffer */
+		return NULL;
 	if (q->n == GPUCSUM_MAX_BURST)
-		flush_tx(g, q);        /* all queued frames are complete by now */
+		flush_tx(g, ifidx, q);  /* all queued frames are complete by now */
+	if (q->shadow) {
+		if (len > GPUCSUM_SHADOW_ROOM)
+			return NULL;
+		p = q->shadow + (size_t)q->n * GPUCSUM_SHADOW_ROOM;
+	} else {
+		p = g_inner->get_wptr(ctx, ifidx, len);
+		if (!p)
+			return NULL;
+	}
 	q->ptr[q->n] = p;
 	q->len[q->n] = len;
 	q->n++;
@@ -218,8 +287,35 @@ static int32_t gpucsum_send_pkts(struct mtcp_thread_context *ctx, int nif)
 	struct gthr *g = lookup(ctx);
 
 	if (g && nif >= 0 && nif < GPUCSUM_MAX_IFS)
-		flush_tx(g, g->tx[nif]);
+		flush_tx(g, nif, g->tx[nif]);
 	return g_inner->send_pkts(ctx, nif);
+}
+
+/* Room for a burst of n frames (an inner module may return more than
+ * GPUCSUM_MAX_BURST at once; gcs_*_ptrs splits a batch by itself). */
+static int rx_reserve(struct rx_if *r, uint32_t n)
+{
+	uint32_t cap = r->cap ? r->cap : 64;
+	void *a, *b, *c, *d, *e;
+
+	if (n <= r->cap)
+		return 0;
+	while (cap < n)
+		cap *= 2;
+	a = realloc(r->ptr, cap * sizeof(*r->ptr));
+	if (a) r->ptr = a;
+	b = realloc(r->len, cap * sizeof(*r->len));
+	if (b) r->len = b;
+	c = realloc(r->glen, cap * sizeof(*r->glen));
+	if (c) r->glen = c;
+	d = realloc(r->verdict, cap);
+	if (d) r->verdict = d;
+	e = realloc(r->queue, cap * sizeof(*r->queue));
+	if (e) r->queue = e;
+	if (!a || !b || !c || !d || !e)
+		return -1;
+	r->cap = cap;
+	return 0;
 }
 
 static int32_t gpucsum_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
@@ -227,6 +323,7 @@ static int32_t gpucsum_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
 	struct gthr *g = lookup(ctx);
 	struct rx_if *r;
 	int32_t n = g_inner->recv_pkts(ctx, ifidx), i;
+	const int chained = (g_caps & GPUCSUM_INNER_RX_CHAINED) != 0;
 	int rc;
 
 	if (!g || ifidx < 0 || ifidx >= GPUCSUM_MAX_IFS)
@@ -235,23 +332,26 @@ static int32_t gpucsum_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
 		g->rx[ifidx] = calloc(1, sizeof(struct rx_if));
 	r = g->rx[ifidx];
 	if (!r)
-		return n;
+		die("calloc", GCS_ENOMEM);
 	r->n = 0;
 	if (n <= 0)
 		return n;
-	if (n > GPUCSUM_MAX_BURST)
-		n = GPUCSUM_MAX_BURST;
+	if (rx_reserve(r, (uint32_t)n))
+		die("RX burst arrays", GCS_ENOMEM);
+	/* One pass over the inner burst to learn every frame's address.  get_rptr
+	 * is called again per index when mTCP walks the burst (below). */
 	for (i = 0; i < n; i++) {
 		r->len[i] = 0;
 		r->ptr[i] = g_inner->get_rptr(ctx, ifidx, i, &r->len[i]);
 		if (!r->ptr[i])
 			r->len[i] = 0;
+		r->glen[i] = (chained && r->len[i] > g_seg_max) ? 0 : r->len[i];
 	}
 	if (g->rss)
-		rc = gcs_classify_ptrs(g->gcs, r->ptr, r->len, (uint32_t)n, r->verdict, NULL,
+		rc = gcs_classify_ptrs(g->gcs, r->ptr, r->glen, (uint32_t)n, r->verdict, NULL,
 		                       r->queue, GCS_VF_ZERO_BAD_TCP_CHECK);
 	else
-		rc = gcs_verify_ptrs(g->gcs, r->ptr, r->len, (uint32_t)n, r->verdict,
+		rc = gcs_verify_ptrs(g->gcs, r->ptr, r->glen, (uint32_t)n, r->verdict,
 		                     GCS_VF_ZERO_BAD_TCP_CHECK);
 	if (rc) {
 		g->st.gpu_failures++;
@@ -261,9 +361,12 @@ static int32_t gpucsum_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
 	} else {
 		g->st.rx_batches++;
 	}
-	for (i = 0; i < n; i++)
+	for (i = 0; i < n; i++) {
 		if (!r->ptr[i])
 			r->verdict[i] = GCS_V_DROP_TRUNC;   /* the inner module's own drop */
+		else if (r->glen[i] != r->len[i])
+			r->verdict[i] = V_INNER;            /* chain: the inner's checks */
+	}
 	if (g->rss && !rc)
 		for (i = 0; i < n; i++)
 			if (r->verdict[i] == GCS_V_ACCEPT && r->queue[i] != (uint16_t)g->own_queue)
@@ -278,15 +381,31 @@ static uint8_t *gpucsum_get_rptr(struct mtcp_thread_context *ctx, int ifidx, int
 {
 	struct gthr *g = lookup(ctx);
 	struct rx_if *r = (g && ifidx >= 0 && ifidx < GPUCSUM_MAX_IFS) ? g->rx[ifidx] : NULL;
+	uint8_t *p;
+	uint16_t l = 0;
 
 	if (!r || index < 0 || index >= r->n)
 		return g_inner->get_rptr(ctx, ifidx, index, len);
+	if (r->verdict[index] == V_INNER) {
+		g->st.rx_inner++;
+		p = g_inner->get_rptr(ctx, ifidx, index, len);
+		if (!p)
+			g->st.rx_errors++;
+		return p;
+	}
 	if (GCS_V_IS_ERROR(r->verdict[index])) {
 		g->st.rx_errors++;
 		return NULL;
 	}
-	*len = r->len[index];
-	return r->ptr[index];
+	/* Same index again: inner per-index state now points at this frame. */
+	p = g_inner->get_rptr(ctx, ifidx, index, &l);
+	if (p != r->ptr[index] || l != r->len[index]) {
+		g->st.rx_rptr_changed++;
+		g->st.rx_errors++;
+		return NULL;
+	}
+	*len = l;
+	return p;
 }
 
 static int32_t gpucsum_select(struct mtcp_thread_context *ctx)
@@ -313,8 +432,18 @@ static void gpucsum_destroy_handle(struct mtcp_thread_context *ctx)
 	if (g->gcs)
 		gcs_ctx_destroy(g->gcs);
 	for (i = 0; i < GPUCSUM_MAX_IFS; i++) {
-		free(g->rx[i]);
-		free(g->tx[i]);
+		if (g->rx[i]) {
+			free(g->rx[i]->ptr);
+			free(g->rx[i]->len);
+			free(g->rx[i]->glen);
+			free(g->rx[i]->verdict);
+			free(g->rx[i]->queue);
+			free(g->rx[i]);
+		}
+		if (g->tx[i]) {
+			free(g->tx[i]->shadow);
+			free(g->tx[i]);
+		}
 	}
 	free(g);
 }
@@ -368,7 +497,7 @@ int gpucsum_rx_verdict(struct mtcp_thread_context *ctx, int ifidx, int index)
 	struct gthr *g = lookup(ctx);
 	struct rx_if *r = (g && ifidx >= 0 && ifidx < GPUCSUM_MAX_IFS) ? g->rx[ifidx] : NULL;
 
-	if (!r || index < 0 || index >= r->n)
+	if (!r || index < 0 || index >= r->n || r->verdict[index] == V_INNER)
 		return -1;
 	return r->verdict[index];
 }

@@ -35,7 +35,9 @@ V_NAMES = {v: k[6:] for k, v in K.items() if k.startswith("GCS_V_") and k != "GC
 
 
 class GcsError(RuntimeError):
-    pass
+    def __init__(self, msg: str, code: int | None = None):
+        super().__init__(msg)
+        self.code = code
 
 
 _lib = None
@@ -134,7 +136,7 @@ def check(rc: int, what: str = "") -> None:
     if rc != 0:
         L = lib()
         raise GcsError(f"{what}: {L.gcs_strerror(rc).decode()} ({rc}) "
-                       f"{L.gcs_last_hip_error().decode()}")
+                       f"{L.gcs_last_hip_error().decode()}", rc)
 
 
 def device_count() -> int:

@@ -170,6 +170,77 @@ int mini_rx_loop(io_module_func *iom, struct mtcp_thread_context *ctx, int ifidx
 	return (int)k;
 }
 
+/* RX loop that also delivers each ACCEPT frame's TCP payload the way
+ * RBPut's __MEMCPY_DATA_2_BUFFER does under ENABLELRO (tcp_ring_buffer.c:15-21):
+ * a payload longer than TCP_DEFAULT_MSS (tcp_in.h:36) is an LRO chain and is
+ * gathered by dev_ioctl(PKT_RX_TCP_LROSEG) from the module's current mbuf when
+ * `lro` is set (the module-identity test of tcp_ring_buffer.c:18), otherwise
+ * memcpy'd.  Payload k goes to out + out_off[k] (out_off[k] = ~0 for frames
+ * that delivered nothing). */
+int mini_rx_deliver(io_module_func *iom, struct mtcp_thread_context *ctx, int ifidx,
+                    struct mini_stats *st, uint8_t *disp, uint32_t max, int lro,
+                    uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint32_t *out_len)
+{
+	uint32_t k = 0;
+	uint64_t used = 0;
+	int32_t n, i;
+
+	memset(st, 0, sizeof(*st));
+	while ((n = iom->recv_pkts(ctx, ifidx)) > 0) {
+		for (i = 0; i < n; i++) {
+			uint16_t len = 0;
+			uint8_t *p = iom->get_rptr(ctx, ifidx, i, &len);
+			int d;
+			st->rx_packets++;
+			if (k < max) {
+				out_off[k] = ~(uint64_t)0;
+				out_len[k] = 0;
+			}
+			if (!p) {
+				st->rx_errors++;
+				d = MINI_NULL;
+			} else {
+				d = process_packet(iom, ctx, ifidx, p, len);
+				if (d == MINI_ERROR)
+					st->rx_errors++;
+				else if (d == MINI_ACCEPT)
+					st->accepted++;
+				else if (d == MINI_RELEASE)
+					st->released++;
+				else if (d == MINI_NOT_TCP)
+					st->not_tcp++;
+				else
+					st->non_ip++;
+			}
+			if (d == MINI_ACCEPT && k < max) {
+				uint8_t *iph = p + 14;
+				uint32_t ihl = iph[0] & 15, ip_len = be16(iph + 2);
+				uint8_t *tcph = iph + 4 * ihl;
+				uint32_t hl = 4 * (ihl + (tcph[12] >> 4));
+				uint32_t plen = ip_len - hl;
+				if (used + plen <= out_cap) {
+					if (lro && plen > 1460)        /* TCP_DEFAULT_MSS */
+						iom->dev_ioctl(ctx, 0, PKT_RX_TCP_LROSEG, out + used);
+					else
+						memcpy(out + used, tcph + (hl - 4 * ihl), plen);
+					out_off[k] = used;
+					out_len[k] = plen;
+					used += plen;
+				}
+			}
+			if (k < max)
+				disp[k] = (uint8_t)d;
+			k++;
+		}
+	}
+	return (int)k;
+}
+
+int32_t mini_send(io_module_func *iom, struct mtcp_thread_context *ctx, int ifidx)
+{
+	return iom->send_pkts(ctx, ifidx);
+}
+
 /* TX: write n prepared frames (check fields as mTCP leaves them: 0) through
  * the module in mTCP's order, flushing with send_pkts every `burst` frames. */
 int mini_tx(io_module_func *iom, struct mtcp_thread_context *ctx, int ifidx,
@@ -184,6 +255,12 @@ int mini_tx(io_module_func *iom, struct mtcp_thread_context *ctx, int ifidx,
 		uint8_t *f = iom->get_wptr(ctx, ifidx, (uint16_t)L);   /* eth_out.c:58 */
 		int rc = -1;
 
+		if (!f) {
+			/* no TX buffer: the stream stays queued (tcp_out.c:799-802) and
+			 * goes out after the next send_pkts round frees buffers */
+			iom->send_pkts(ctx, ifidx);
+			f = iom->get_wptr(ctx, ifidx, (uint16_t)L);
+		}
 		if (!f)
 			return -1;
 		/* Ethernet + IP header, check = 0 (ip_out.c:143-153) */

@@ -438,3 +438,44 @@ def test_shards_equal_whole(torch_dev, ctx):
     ctx.sync()
     assert t.equal(whole, parts)
     assert int((whole != 0).sum()) == len(range(0, n, 37))
+
+
+def test_c4_shard_properties(torch_dev, ctx, O):
+    """C4's per-GPU shard, 4M x 1500 B (6.4 GB at stride 1536, generated in
+    HBM as bench.py does): TX fill then RX verify accepts all; a fill is
+    idempotent; 4,096 sampled frames match the oracle bit for bit (checks and
+    whole filled frames); seeded corruptions are exactly the drops."""
+    t = torch_dev
+    n, L = 4 << 20, 1500
+    d, stride = synth.fixed_frames_device(n, L, seed=0xC4)
+    rows = d.view(n, stride)
+    idx = np.sort(np.random.default_rng(4).choice(n, 4096, replace=False))
+    tidx = t.from_numpy(idx).cuda()
+    sample = rows.index_select(0, tidx).cpu().numpy().reshape(-1)      # unfilled originals
+    st = t.zeros(n, dtype=t.uint8, device="cuda")
+    cs = t.zeros(n, dtype=t.int32, device="cuda")
+    ctx.compute_fixed(d, stride, L, n, st, cs)
+    v = t.zeros(n, dtype=t.uint8, device="cuda")
+    ctx.verify_fixed(d, stride, L, n, v)
+    ctx.sync()
+    assert int((st != 0).sum()) == 0 and int((v != 0).sum()) == 0
+    rst, rcs = O.compute_fixed(sample, stride, L, len(idx))
+    assert (rst == 0).all()
+    np.testing.assert_array_equal(host(cs).view(np.uint32)[idx], rcs)
+    np.testing.assert_array_equal(rows.index_select(0, tidx).cpu().numpy().reshape(-1), sample)
+    before = d.clone()
+    ctx.compute_fixed(d, stride, L, n)                                 # idempotent
+    ctx.sync()
+    assert t.equal(d, before)
+    del before
+    # corruptions: one byte in [14, 1500) of every 997th frame plus a seeded set
+    rng = np.random.default_rng(44)
+    bad = np.unique(np.concatenate([np.arange(5, n, 997), rng.choice(n, 3000, replace=False)]))
+    pos = rng.integers(14, L, len(bad))
+    flip = rng.integers(1, 256, len(bad))
+    flat = t.from_numpy(bad.astype(np.int64) * stride + pos).cuda()
+    d[flat] ^= t.from_numpy(flip.astype(np.uint8)).cuda()
+    ctx.verify_fixed(d, stride, L, n, v)
+    ctx.sync()
+    got = t.nonzero(v).flatten().cpu().numpy()
+    np.testing.assert_array_equal(got, bad)

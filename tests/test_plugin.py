@@ -34,7 +34,8 @@ class Stats(C.Structure):
 class GStats(C.Structure):
     _fields_ = [(k, C.c_uint64) for k in
                 ("rx_frames", "rx_errors", "rx_batches", "tx_frames", "tx_batches",
-                 "gpu_failures", "rx_foreign")] + [("device", C.c_int)]
+                 "gpu_failures", "rx_foreign")] + [("device", C.c_int)] + \
+                [(k, C.c_uint64) for k in ("rx_inner", "rx_rptr_changed", "tx_inner_full")]
 
 
 @pytest.fixture(scope="module")
