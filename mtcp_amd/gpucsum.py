@@ -49,6 +49,17 @@ def lib() -> C.CDLL:
         if not os.path.exists(LIB_PATH):
             raise GcsError(f"{LIB_PATH} is missing: build it with `make -C mtcp_amd/csrc` "
                            "(there is no CPU fallback)")
+        # One HIP runtime per process.  PyTorch-ROCm bundles its own
+        # libamdhip64 / libhsa-runtime64; if this library were loaded first it
+        # would bring in /opt/rocm's copies and torch would then load its own,
+        # a second HSA runtime instance in the process, one of which sees no
+        # device ("no ROCm-capable device").  Loading torch first makes our
+        # libamdhip64.so.7 dependency resolve to torch's already-loaded copy.
+        # (A C program such as mTCP has no torch: /opt/rocm's runtime alone.)
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         vp, u8, u16, u32, u64, i = (C.c_void_p, C.c_uint8, C.c_uint16, C.c_uint32, C.c_uint64,
                                     C.c_int)

@@ -1,0 +1,173 @@
+/*
+ * ref_stack_harness.c -- drives mTCP's OWN RX/TX code around the checksum
+ * path through any io_module_func (TEST INFRASTRUCTURE ONLY; never linked into
+ * the product).
+ *
+ * oracle/Makefile compiles the reference's eth_in.c, ip_in.c, tcp_in.c,
+ * icmp.c, ip_out.c, tcp_out.c, eth_out.c, arp.c and tcp_util.c in place from
+ * /root/reference with the reference flags and WITHOUT -DDISABLE_HWCSUM, i.e.
+ * exactly the objects in which every fold is guarded by mtcp->iom->dev_ioctl
+ * (ip_in.c:28-37, tcp_in.c:1224-1241, ip_out.c:84-101, tcp_out.c:202-214).
+ * This file supplies what those objects need around the checksum prefix:
+ *
+ *   CONFIG        one port (eths[0], nif_to_eidx), one route and one ARP entry
+ *                 that match every address (ip_out.c:8-37, arp.c:98-128)
+ *   mtcp_manager  zeroed except iom / ctx / cur_ts (core.c:1187-1190)
+ *   RX loop       core.c:785-801: recv_pkts, get_rptr per index, NULL ->
+ *                 rx_errors, else ProcessPacket (eth_in.c:9-60)
+ *   TX            SendTCPPacketStandalone (tcp_out.c:135-217) per segment,
+ *                 send_pkts every `burst` segments (core.c:846-848)
+ *
+ * Everything beyond the checksum path stays out of reach: ProcessTCPPacket's
+ * first call after its checksum prefix is StreamHTSearch (tcp_in.c:1251),
+ * which ref_stack_traps.c turns into a longjmp back here ("ACCEPT").  The
+ * stack functions the objects reference but the checksum path never reaches
+ * are traps that abort (ref_stack_traps.c).
+ */
+#include <setjmp.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "mtcp.h"
+#include "eth_in.h"
+#include "tcp_out.h"
+
+struct mtcp_config CONFIG;
+
+/* ref_stack_traps.c */
+extern jmp_buf refs_accept_jb;
+extern int refs_accept_armed;
+
+enum { REFS_ACCEPT = 0, REFS_ERROR = 1, REFS_TRUE = 2, REFS_FALSE = 3, REFS_NULL = 5 };
+
+static struct eth_table g_eth[1];
+static int g_nif_to_eidx[MAX_DEVICES];
+static struct route_table g_route[1];
+static struct arp_entry g_arp[1];
+static struct mtcp_manager refs_mgr;
+
+/* Configure the one port: our IP address (ICMP echo requests to it are
+ * answered, icmp.c:110-119) and MACs. */
+void refs_config(uint32_t my_ip)
+{
+	static const unsigned char src[6] = {0x02, 0, 0, 0, 0, 0x01};
+	static const unsigned char dst[6] = {0x02, 0, 0, 0, 0, 0x02};
+	int i;
+
+	memset(&CONFIG, 0, sizeof(CONFIG));
+	memset(g_eth, 0, sizeof(g_eth));
+	strcpy(g_eth[0].dev_name, "gpucsum0");
+	g_eth[0].ifindex = 0;
+	memcpy(g_eth[0].haddr, src, 6);
+	g_eth[0].ip_addr = my_ip;
+	g_eth[0].netmask = 0;
+	for (i = 0; i < MAX_DEVICES; i++)
+		g_nif_to_eidx[i] = i == 0 ? 0 : -1;
+	g_route[0].daddr = 0;
+	g_route[0].mask = 0;
+	g_route[0].masked = 0;
+	g_route[0].prefix = 1;
+	g_route[0].nif = 0;
+	memset(g_arp, 0, sizeof(g_arp));
+	g_arp[0].prefix = 8;              /* masked entry: matches every dip */
+	g_arp[0].ip_mask = 0;
+	g_arp[0].ip_masked = 0;
+	memcpy(g_arp[0].haddr, dst, 6);
+	CONFIG.eths = g_eth;
+	CONFIG.eths_num = 1;
+	CONFIG.nif_to_eidx = g_nif_to_eidx;
+	CONFIG.rtable = g_route;
+	CONFIG.routes = 1;
+	CONFIG.arp.entry = g_arp;
+	CONFIG.arp.entries = 1;
+	CONFIG.num_cores = 1;
+}
+
+static void refs_bind(struct io_module_func *iom, struct mtcp_thread_context *ctx, uint32_t ts)
+{
+	memset(&refs_mgr, 0, sizeof(refs_mgr));
+	refs_mgr.iom = iom;
+	refs_mgr.ctx = ctx;
+	refs_mgr.cur_ts = ts;
+}
+
+static int process_one(int ifidx, uint32_t ts, unsigned char *pkt, int len)
+{
+	int ret;
+
+	refs_accept_armed = 1;
+	if (setjmp(refs_accept_jb)) {
+		refs_accept_armed = 0;
+		return REFS_ACCEPT;                  /* reached StreamHTSearch */
+	}
+	ret = ProcessPacket(&refs_mgr, ifidx, ts, pkt, len);
+	refs_accept_armed = 0;
+	return ret < 0 ? REFS_ERROR : ret ? REFS_TRUE : REFS_FALSE;
+}
+
+/* core.c:785-801 plus the send_pkts of core.c:846-848 after each round (ICMP
+ * echo replies and ARP answers go out through get_wptr).  Returns frames seen;
+ * disp[k] per frame in arrival order; *rx_errors as nstat.rx_errors counts them. */
+int refs_rx_loop(struct io_module_func *iom, struct mtcp_thread_context *ctx, int ifidx,
+                 uint8_t *disp, uint32_t max, uint64_t *rx_errors)
+{
+	uint32_t k = 0;
+	int32_t n, i;
+
+	refs_bind(iom, ctx, 1000);
+	*rx_errors = 0;
+	while ((n = iom->recv_pkts(ctx, ifidx)) > 0) {
+		for (i = 0; i < n; i++) {
+			uint16_t len = 0;
+			unsigned char *p = iom->get_rptr(ctx, ifidx, i, &len);
+			int d = p ? process_one(ifidx, refs_mgr.cur_ts, p, len) : REFS_NULL;
+			if (d == REFS_NULL || d == REFS_ERROR)
+				(*rx_errors)++;
+			if (k < max)
+				disp[k] = (uint8_t)d;
+			k++;
+		}
+		iom->send_pkts(ctx, ifidx);
+		refs_mgr.cur_ts++;
+	}
+	return (int)k;
+}
+
+/* n segments through SendTCPPacketStandalone (tcp_out.c:135-217), which
+ * builds the headers (IPOutputStandalone, ip_out.c:41-101; EthernetOutput,
+ * eth_out.c:36-80), copies the payload and -- unless the module's dev_ioctl
+ * answers 0 -- folds both checks.  Segment k: payload + pay_off[k],
+ * pay_len[k] bytes (<= 1448 with the timestamp option), tuple / seq / flags
+ * from the arrays.  Returns segments written (-1 on a NULL get_wptr that a
+ * send round does not cure). */
+int refs_tx_tcp(struct io_module_func *iom, struct mtcp_thread_context *ctx, uint32_t n,
+                const uint32_t *saddr, const uint16_t *sport, const uint32_t *daddr,
+                const uint16_t *dport, const uint32_t *seq, const uint32_t *ack,
+                const uint16_t *window, const uint8_t *flags, const uint8_t *payload,
+                const uint64_t *pay_off, const uint16_t *pay_len, uint32_t burst)
+{
+	uint32_t k;
+
+	refs_bind(iom, ctx, 5000);
+	for (k = 0; k < n; k++) {
+		int rc = SendTCPPacketStandalone(&refs_mgr, saddr[k], sport[k], daddr[k], dport[k],
+		                                 seq[k], ack[k], window[k], flags[k],
+		                                 (uint8_t *)payload + pay_off[k], pay_len[k],
+		                                 refs_mgr.cur_ts, 77u + k);
+		if (rc < 0) {
+			iom->send_pkts(ctx, 0);          /* tcp_out.c:799-802: retry later */
+			rc = SendTCPPacketStandalone(&refs_mgr, saddr[k], sport[k], daddr[k], dport[k],
+			                             seq[k], ack[k], window[k], flags[k],
+			                             (uint8_t *)payload + pay_off[k], pay_len[k],
+			                             refs_mgr.cur_ts, 77u + k);
+			if (rc < 0)
+				return -1;
+		}
+		if (burst && (k + 1) % burst == 0)
+			iom->send_pkts(ctx, 0);
+	}
+	iom->send_pkts(ctx, 0);
+	return (int)n;
+}

@@ -38,7 +38,8 @@ def test_gather_threads_unavailable(torch_dev, monkeypatch):
     monkeypatch.setenv("GCS_FAULT_INJECT", "gather_thread")
     monkeypatch.setenv("GCS_GATHER_THREADS", "64")
     buf, off, lens, bad = batch(20000, 10)
-    with gpucsum.Context(0, max_frames=4096, max_bytes=4 << 20) as c:
+    # chunks of ~2 MiB (byte-limited): above the 1 MiB inline-gather threshold
+    with gpucsum.Context(0, max_frames=1 << 16, max_bytes=4 << 20) as c:
         v = c.verify_host(buf.copy(), off, lens)
     np.testing.assert_array_equal(v, Oracle().verify_batch(buf.copy(), off, lens))
     assert (v[bad] != 0).all()
@@ -46,7 +47,7 @@ def test_gather_threads_unavailable(torch_dev, monkeypatch):
 
 def test_bad_alloc_is_a_status_code(torch_dev, monkeypatch):
     buf, off, lens, bad = batch(20000, 20)
-    with gpucsum.Context(0, max_frames=4096, max_bytes=4 << 20) as c:
+    with gpucsum.Context(0, max_frames=1 << 16, max_bytes=4 << 20) as c:
         monkeypatch.setenv("GCS_FAULT_INJECT", "gather_alloc")
         with pytest.raises(gpucsum.GcsError) as e:
             c.verify_host(buf.copy(), off, lens)
@@ -59,11 +60,15 @@ def test_bad_alloc_is_a_status_code(torch_dev, monkeypatch):
 
 @pytest.mark.parametrize("compute", [False, True])
 def test_failed_batch_leaves_no_busy_slot(torch_dev, monkeypatch, compute):
-    """Chunk 1 is in flight when the call fails.  The next call (a different
-    batch, same context) must see none of it: before the fix its first drain
-    copied chunk 1's results into the new call's arrays."""
+    """Chunk 1 (513 frames) is in flight when the call fails.  The next call on
+    the same context (100 frames) must see none of it: before the fix its first
+    drain copied the stale chunk's 513 results into the new call's 100-entry
+    arrays, past their end.  The output arrays carry guard bytes here."""
+    import ctypes as C
+    L = gpucsum.lib()
     b1, off1, len1, _ = batch(6000, 30)
-    b2, off2, len2, bad2 = batch(6000, 40)
+    b2, off2, len2, bad2 = batch(100, 40)
+    guard = 4096
     with gpucsum.Context(0, max_frames=1024, max_bytes=1 << 20) as c:
         monkeypatch.setenv("GCS_FAULT_INJECT", "second_chunk")
         with pytest.raises(gpucsum.GcsError):
@@ -72,20 +77,25 @@ def test_failed_batch_leaves_no_busy_slot(torch_dev, monkeypatch, compute):
             else:
                 c.verify_host(b1.copy(), off1, len1)
         monkeypatch.delenv("GCS_FAULT_INJECT")
+        out = np.full(100 + guard, 0xAA, np.uint8)
+        got = b2.copy()
         if compute:
-            fresh = b2.copy()
-            fresh[off2.astype(np.int64)[:, None] + np.array([24, 25, 50, 51])] = 0
-            got = fresh.copy()
-            st, cs = c.compute_host(got, off2, len2)
-            ref = fresh.copy()
+            got[off2.astype(np.int64)[:, None] + np.array([24, 25, 50, 51])] = 0
+            ref = got.copy()
+            cs = np.full(100 + guard, 0xAAAAAAAA, np.uint32)
+            gpucsum.check(L.gcs_compute(c.h, got.ctypes.data, off2.ctypes.data, len2.ctypes.data,
+                                        100, out.ctypes.data, cs.ctypes.data))
             rst, rcs = Oracle().compute_batch(ref, off2, len2)
-            np.testing.assert_array_equal(st, rst)
-            np.testing.assert_array_equal(cs, rcs)
+            np.testing.assert_array_equal(out[:100], rst)
+            np.testing.assert_array_equal(cs[:100], rcs)
             np.testing.assert_array_equal(got, ref)
+            assert (cs[100:] == 0xAAAAAAAA).all()
         else:
-            v = c.verify_host(b2.copy(), off2, len2)
-            np.testing.assert_array_equal(v, Oracle().verify_batch(b2.copy(), off2, len2))
-            assert (v[bad2] != 0).all()
+            gpucsum.check(L.gcs_verify(c.h, got.ctypes.data, off2.ctypes.data, len2.ctypes.data,
+                                       100, out.ctypes.data, 0))
+            np.testing.assert_array_equal(out[:100], Oracle().verify_batch(b2.copy(), off2, len2))
+            assert (out[bad2] != 0).all()
+        assert (out[100:] == 0xAA).all()
 
 
 def test_frame_larger_than_staging_is_refused_whole(torch_dev):

@@ -302,7 +302,8 @@ def test_lro_gathers_the_right_frame(S, P, burst):  # noqa: F811
     np.testing.assert_array_equal(disp_sw, disp_hw)
     assert (st_sw.rx_errors, st_sw.accepted) == (st_hw.rx_errors, st_hw.accepted)
     assert g_sw == g_hw > 0
-    assert gst.rx_inner == chain.sum() and gst.rx_rptr_changed == 0
+    # chains the NIC flagged bad were NULL already in the burst pass
+    assert gst.rx_inner == (chain & (bad == 0)).sum() and gst.rx_rptr_changed == 0
     for k in range(n):
         if pay_sw[k] is None:
             assert pay_hw[k] is None
@@ -310,8 +311,8 @@ def test_lro_gathers_the_right_frame(S, P, burst):  # noqa: F811
         np.testing.assert_array_equal(pay_sw[k], pay_hw[k])
         # and the gathered bytes are this frame's own payload
         o, L = int(off[k]), int(lens[k])
-        ihl = buf[o + 14] & 15
-        hl = 14 + 4 * ihl + 4 * (buf[o + 14 + 4 * ihl + 12] >> 4)
+        ihl = int(buf[o + 14]) & 15
+        hl = 14 + 4 * ihl + 4 * (int(buf[o + 14 + 4 * ihl + 12]) >> 4)
         np.testing.assert_array_equal(pay_hw[k], buf[o + hl:o + L])
 
 
