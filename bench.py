@@ -58,7 +58,8 @@ def parse():
     return p.parse_args()
 
 
-from mtcp_amd.shard import aggregate_rate, barrier, env_world, max_over_ranks  # noqa: E402
+from mtcp_amd.shard import (aggregate_rate, barrier, env_world, gather_per_rank,  # noqa: E402
+                            max_over_ranks)
 
 
 def dist_setup(args):
@@ -139,16 +140,41 @@ def time_steps(ctx, tx, rx, stride, frame_len, n, steps, warmup, world, torch, s
     return t1 - t0, tx_ms, rx_ms, verdict
 
 
-def pmc_traffic(kernel_key: str):
-    """HBM bytes per launch for the dominant kernel from the committed
-    rocprofv3 PMC summary (profiles/pmc_summary.json, written by
-    profiles/collect_pmc.py with the gfx950 FETCH_SIZE x2 correction)."""
+def pmc_row(label: str):
+    """PMC row of one configuration -- kernel AND frames per launch -- from the
+    committed rocprofv3 summary (profiles/pmc_summary.json: collect.sh +
+    summarize.py, gfx950 FETCH_SIZE x2 correction), or None when that exact
+    configuration was not profiled."""
     p = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
-        d = json.load(open(p))
-        return d["kernels"][kernel_key]["hbm_bytes_per_launch"]
+        return json.load(open(p))["configs"][label]
     except Exception:
         return None
+
+
+def dominant_frac(n, L, compute_ms, verify_ms):
+    """Algorithmic GB/s of the slower of the two kernels / the HBM peak."""
+    if compute_ms >= verify_ms:
+        gbs = n * (L + 4) / (compute_ms * 1e-3) / 1e9
+    else:
+        gbs = n * (L + 1) / (verify_ms * 1e-3) / 1e9
+    return gbs / HBM_PEAK_GBS
+
+
+def host_cpus():
+    """CPUs this process may run on and the cgroup CPU quota (the GPU box gives
+    a job a share of a large host: sched_getaffinity lists the whole machine,
+    cpu.max bounds what the job can use at once)."""
+    cpus = sorted(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(per)
+    except Exception:
+        pass
+    usable = len(cpus) if quota is None else max(1, min(len(cpus), int(quota)))
+    return cpus, usable, quota
 
 
 def cpu_baseline(tx, rx, stride, frame_len, budget_s, sample, torch):
@@ -164,51 +190,61 @@ def cpu_baseline(tx, rx, stride, frame_len, budget_s, sample, torch):
     kind = "reference" if RefHarness.available() else "port"
     if kind == "reference":
         R = RefHarness()
-        run = lambda buf, compute, thr: R.run_fixed(buf, stride, frame_len, m, compute, thr)  # noqa
+
+        def run(buf, compute, pin):
+            return R.run_fixed(buf, stride, frame_len, m, compute, cpus=pin)
     else:
         O = Oracle()
 
-        def run(buf, compute, thr):
+        def run(buf, compute, pin):
             if compute:
-                return O.compute_fixed(buf, stride, frame_len, m, threads=thr, want=False)
-            return O.verify_fixed(buf, stride, frame_len, m, threads=thr)
+                return O.compute_fixed(buf, stride, frame_len, m, threads=len(pin), want=False)
+            return O.verify_fixed(buf, stride, frame_len, m, threads=len(pin))
 
-    def measure(threads, budget):
+    cpus, usable, quota = host_cpus()
+    one = [cpus[0]]
+    allc = cpus[:usable]
+
+    def measure(pin, budget):
         rates = []
         t_start = time.perf_counter()
         while True:
             t0 = time.perf_counter()
-            run(tx_h, True, threads)
-            run(rx_h, False, threads)
+            run(tx_h, True, pin)
+            run(rx_h, False, pin)
             dt = time.perf_counter() - t0
             rates.append(2 * m / dt)
             if time.perf_counter() - t_start >= budget and len(rates) >= 3:
                 break
         return float(np.median(rates)), len(rates)
 
-    r1, reps1 = measure(1, budget_s)
-    threads = max(1, min(16, (os.cpu_count() or 1)))
-    rmt, repsmt = measure(threads, max(1.0, budget_s / 4))
+    r1, reps1 = measure(one, budget_s)
+    rmt, repsmt = measure(allc, max(1.0, budget_s / 4))
     try:
         cpu_model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo")
                          if l.startswith("model name"))
     except Exception:
         cpu_model = "unknown"
+    pinned = "pinned" if kind == "reference" else "unpinned (port fallback)"
     return {
         "value": r1 / 1e9, "unit": "Gpkt/s", "cores": 1, "kind": kind,
         "sample": f"{m} TX + {m} RX frames of the bench batches ({frame_len} B, stride {stride}),"
-                  f" median of {reps1} passes, 1 pinned-free thread",
+                  f" median of {reps1} passes, 1 thread {pinned} to CPU {one[0]}",
         "gib_per_s": r1 * frame_len / 2**30,
-        "multi_core": {"value": rmt / 1e9, "unit": "Gpkt/s", "cores": threads,
-                       "gib_per_s": rmt * frame_len / 2**30, "passes": repsmt},
+        "multi_core": {"value": rmt / 1e9, "unit": "Gpkt/s", "cores": len(allc),
+                       "gib_per_s": rmt * frame_len / 2**30, "passes": repsmt,
+                       "threads": f"one per usable host core, each {pinned} to its CPU",
+                       "affinity_cpus": len(cpus), "cgroup_cpu_quota": quota},
         "cpu_model": cpu_model,
     }
 
 
-def c1_small_frames(ctx, torch, steps=20):
-    """C1 side measurement: 1M x 64 B frames, IP+TCP verify, device-resident."""
+def c1_small_frames(ctx, torch, n=1 << 20, steps=20):
+    """C1 side measurement: n x 64 B frames (C1: 1M), IP+TCP verify,
+    device-resident.  At 1M the 64 MiB batch is Infinity-Cache resident; 8M
+    (512 MiB) is the HBM-resident figure."""
     from mtcp_amd import synth
-    n, L = 1 << 20, 64
+    L = 64
     buf, stride = synth.fixed_frames_device(n, L, seed=0x6401)
     stream = torch.cuda.current_stream().cuda_stream
     ctx.compute_fixed(buf, stride, L, n, stream=stream)
@@ -224,10 +260,13 @@ def c1_small_frames(ctx, torch, steps=20):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / steps
     assert int((v != 0).sum()) == 0
-    return {"workload": "C1: 1M x 64B verify, stride 64, back-to-back launches",
-            "ms_per_launch": ms, "gpkt_per_s": n / ms / 1e6,
-            "gib_per_s": n * L / (ms * 1e-3) / 2**30,
-            "hbm_gbs_algorithmic": n * (L + 1) / (ms * 1e-3) / 1e9}
+    out = {"workload": f"{n} x 64B verify, stride 64, back-to-back launches",
+           "ms_per_launch": ms, "gpkt_per_s": n / ms / 1e6,
+           "gib_per_s": n * L / (ms * 1e-3) / 2**30}
+    key = "cache_resident_gbs_algorithmic" if n * stride <= (128 << 20) else \
+        "hbm_gbs_algorithmic"
+    out[key] = n * (L + 1) / (ms * 1e-3) / 1e9
+    return out
 
 
 def _settle(torch, fn, seconds=0.25):
@@ -450,7 +489,10 @@ def main():
     bad_seen = int((verdict != 0).sum())
     if bad_seen != nbad:
         raise SystemExit(f"rank {rank}: verify flagged {bad_seen} frames, {nbad} corrupted")
-    t = max_over_ranks(world, elapsed, device="cuda" if args.dist_backend == "nccl" else "cpu")
+    red_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
+    t = max_over_ranks(world, elapsed, device=red_dev)
+    per = gather_per_rank(world, [float(rank), float(local), elapsed, tx_ms, rx_ms,
+                                  float(bad_seen), float(nbad)], device=red_dev)
 
     rate = aggregate_rate(2 * n, world, args.steps, t)   # TX fills + RX verifies, all ranks
     value = rate / 1e9
@@ -463,6 +505,7 @@ def main():
     else:
         kname, kms, kbytes = "compute", tx_ms, tx_bytes
     achieved = kbytes / (kms * 1e-3) / 1e9
+    prow = pmc_row(f"{kname}_fixed_{L}_{n}")
     line = {
         "metric": METRIC,
         "value": value,
@@ -486,17 +529,27 @@ def main():
         "gib_per_s": gib,
         "roofline": {
             "bound": "hbm",
-            "kernel": (f"gcs::k_fixed<32,3,{'true' if kname == 'compute' else 'false'},"
-                       f"false,true,4,true,1> ({kname}: G=32 lanes x U=3 chunks, NT loads, "
-                       f"sc1 sector write-back, XCD block map)"),
+            "kernel": f"{kname} of {n} x {L}B: " + (prow["kernel"] if prow else "see kernels_ms"),
             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": pmc_traffic(f"{kname}_{L}"),
+            # HBM bytes per launch of THIS configuration (kernel and frames per
+            # launch) from rocprofv3 PMC; null when it was not profiled
+            "traffic": prow["hbm_bytes_per_launch"] if prow else None,
+            "traffic_source": (f"profiles/pmc_summary.json configs[{kname}_fixed_{L}_{n}]"
+                               if prow else None),
             "bytes_per_launch_algorithmic": kbytes, "avg_launch_ms": kms,
         },
         "kernels_ms": {"compute": tx_ms, "verify": rx_ms,
                        "compute_first_last": [tx_list[0], tx_list[-1]],
                        "verify_first_last": [rx_list[0], rx_list[-1]]},
+        # per GPU, like mTCP's per-thread NETSTAT (core.c:189-218): each rank's
+        # own rate, dominant-kernel fraction of peak and bad-frame count
+        "per_gpu": [{"rank": int(r), "device": int(d), "gpkt_per_s": 2 * n * args.steps / e / 1e9,
+                     "gib_per_s": 2 * n * args.steps * L / e / 2**30,
+                     "compute_us": c * 1e3, "verify_us": v * 1e3,
+                     "frac_peak": dominant_frac(n, L, c, v),
+                     "bad_frames_detected": int(b), "corrupted_frames": int(nb)}
+                    for r, d, e, c, v, b, nb in per],
         "settle_s": args.settle_s,
         "corrupted_frames_detected": bad_seen,
     }
@@ -508,6 +561,7 @@ def main():
             del tx, rx
             torch.cuda.empty_cache()
             line["c1_64B"] = c1_small_frames(ctx, torch)
+            line["c1_64B_8M"] = c1_small_frames(ctx, torch, n=8 << 20)
             line["c3_imix"] = c3_imix(ctx, torch)
             torch.cuda.empty_cache()
             line["rows_8f"] = rows_8f(ctx, torch)

@@ -45,6 +45,20 @@ def max_over_ranks(world: int, x: float, device: str = "cuda") -> float:
     return float(t.item())
 
 
+def gather_per_rank(world: int, values: list[float], device: str = "cuda") -> list[list[float]]:
+    """Every rank's `values` (same length on all ranks), on every rank: the
+    per-GPU report of the bench line (mTCP prints per-thread NETSTAT the same
+    way, core.c:189-218).  Called outside the timed region."""
+    if world == 1:
+        return [list(values)]
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(values, dtype=torch.float64, device=device)
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    return [p.cpu().tolist() for p in parts]
+
+
 def aggregate_rate(frames_per_rank: int, world: int, steps: int, seconds: float) -> float:
     """Whole-job frames per second: all ranks' frames over the max-over-ranks time."""
     return frames_per_rank * world * steps / seconds

@@ -1,3 +1,4 @@
+#define _GNU_SOURCE
 /*
  * ref_harness.c -- drives the REFERENCE's own checksum code (test
  * infrastructure only; see csum_ref.h for the rules on oracle/).
@@ -241,4 +242,44 @@ void refx_run_fixed_mt(uint8_t *buf, uint64_t stride, uint32_t frame_len,
 	for (t = 1; t < threads; t++)
 		if (live[t])
 			pthread_join(tid[t], NULL);
+}
+
+/* The same shards, each on a thread pinned to cpus[t] before it starts
+ * (1 pinned core, and one thread per host core).  The caller's
+ * own affinity is left alone: it only waits. */
+int refx_run_fixed_pinned(uint8_t *buf, uint64_t stride, uint32_t frame_len, uint32_t n,
+                          uint8_t *out, int compute, int threads, const int *cpus)
+{
+	enum { MAXT = 256 };
+	pthread_t tid[MAXT];
+	struct rshard sh[MAXT];
+	int t, rc = 0;
+
+	if (threads < 1 || threads > MAXT || !cpus)
+		return -1;
+	for (t = 0; t < threads; t++) {
+		pthread_attr_t at;
+		cpu_set_t set;
+		sh[t].buf = buf;
+		sh[t].stride = stride;
+		sh[t].frame_len = frame_len;
+		sh[t].lo = (uint32_t)((uint64_t)n * t / threads);
+		sh[t].hi = (uint32_t)((uint64_t)n * (t + 1) / threads);
+		sh[t].out = out;
+		sh[t].compute = compute;
+		CPU_ZERO(&set);
+		CPU_SET(cpus[t], &set);
+		pthread_attr_init(&at);
+		pthread_attr_setaffinity_np(&at, sizeof(set), &set);
+		if (pthread_create(&tid[t], &at, rshard_main, &sh[t]) != 0) {
+			pthread_attr_destroy(&at);
+			threads = t;
+			rc = -1;
+			break;
+		}
+		pthread_attr_destroy(&at);
+	}
+	for (t = 0; t < threads; t++)
+		pthread_join(tid[t], NULL);
+	return rc;
 }

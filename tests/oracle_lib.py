@@ -249,6 +249,8 @@ class RefHarness:
                                          C.c_void_p]
         L.refx_run_fixed_mt.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32,
                                         C.c_void_p, C.c_int, C.c_int]
+        L.refx_run_fixed_pinned.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32,
+                                            C.c_void_p, C.c_int, C.c_int, C.c_void_p]
         L.refx_icmp_checksum.restype = C.c_uint16
         L.refx_icmp_checksum.argtypes = [C.c_void_p, C.c_int]
         L.refx_rss_hash.restype = C.c_uint32
@@ -297,7 +299,14 @@ class RefHarness:
         st = self.L.refx_tx_fill(C.c_void_p(buf.ctypes.data + pos), length, C.byref(cs))
         return st, cs.value
 
-    def run_fixed(self, buf, stride, frame_len, n, compute, threads=1):
+    def run_fixed(self, buf, stride, frame_len, n, compute, threads=1, cpus=None):
+        """cpus: pin thread t to cpus[t] (len(cpus) threads); None: unpinned."""
         out = np.zeros(n, dtype=np.uint8)
-        self.L.refx_run_fixed_mt(_p(buf), stride, frame_len, n, _p(out), int(compute), threads)
+        if cpus is None:
+            self.L.refx_run_fixed_mt(_p(buf), stride, frame_len, n, _p(out), int(compute),
+                                     threads)
+            return out
+        c = np.ascontiguousarray(cpus, np.int32)
+        assert self.L.refx_run_fixed_pinned(_p(buf), stride, frame_len, n, _p(out),
+                                            int(compute), len(c), _p(c)) == 0
         return out

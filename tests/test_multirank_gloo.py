@@ -38,9 +38,12 @@ whole = O.verify_fixed(buf, stride, L, n)
 got = torch.cat([p[: h - l] for p, (l, h) in zip(parts, sizes)]).numpy()
 ok = np.array_equal(got, whole)
 t = shard.max_over_ranks(world, float(rank + 1), device="cpu")
+per = shard.gather_per_rank(world, [float(rank), float(hi - lo), float((mine != 0).sum())],
+                            device="cpu")
 shard.barrier(world)
 if rank == 0:
     print(json.dumps({{"ok": bool(ok), "t": t, "bad": int((whole != 0).sum()), "nbad": len(bad),
+                      "per": per,
                       "rate": shard.aggregate_rate(hi - lo, world, 1, t)}}))
 dist.destroy_process_group()
 """
@@ -78,3 +81,6 @@ def test_two_rank_gloo_shards_equal_whole(tmp_path):
     assert res["ok"]
     assert res["t"] == 2.0                       # max over ranks
     assert res["bad"] == res["nbad"] > 0
+    per = res["per"]                             # per-rank report, gathered
+    assert [p[0] for p in per] == [0.0, 1.0]
+    assert sum(p[1] for p in per) == 5003 and sum(p[2] for p in per) == res["bad"]

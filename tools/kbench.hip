@@ -72,6 +72,48 @@ __global__ void __launch_bounds__(256) k_read(const uint4* __restrict__ p, uint6
     if (acc == 0x9E3779B9u) out[0] = acc;
 }
 
+// One-shot read of a contiguous buffer: block b reads 256*U*16 consecutive
+// bytes, lane t the chunks j*256 + t (every load instruction of a wave covers
+// 1 KiB), all U loads issued before any is consumed -- the access pattern of
+// the shipped verify (k_fixed<32,3>: 8 frames x 1536 B = 12 KiB per block)
+// without its arithmetic.  XCD: the product's XCD-contiguous block order.
+template <int U, bool XCD>
+__global__ void __launch_bounds__(256) k_read1(const uint8_t* __restrict__ p, uint64_t nbytes,
+                                               uint32_t* out)
+{
+    const uint32_t blk = XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint64_t base = (uint64_t)blk * (256 * U * 16);
+    uint4 v[U];
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+        const uint64_t o = base + (uint64_t)(j * 256 + threadIdx.x) * 16;
+        v[j] = o + 16 <= nbytes ? ldg16<true>(p + o) : make_uint4(0, 0, 0, 0);
+    }
+    uint32_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < U; j++) acc += v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
+    if (acc == 0x9E3779B9u) out[0] = acc;
+}
+
+// 512 MiB of writes between timed launches (KB_SCRUB=1): twice the 256 MiB
+// Infinity Cache, so a timed kernel starts with nothing of its batch cached.
+__global__ void k_scrub(uint4* p, uint64_t n16, uint32_t seed)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        p[i] = make_uint4((uint32_t)i, seed, (uint32_t)(i >> 32), ~seed);
+}
+
+static uint4* g_scrub = nullptr;
+static const uint64_t kScrubBytes = 512ull << 20;
+
+static void scrub(hipStream_t s)
+{
+    static uint32_t seed = 1;
+    if (!g_scrub) return;
+    hipLaunchKernelGGL(k_scrub, dim3(4096), dim3(256), 0, s, g_scrub, kScrubBytes / 16, seed++);
+}
+
 struct Variant {
     std::string name;
     double bytes;                       // algorithmic bytes per launch
@@ -603,10 +645,13 @@ void run_variants(std::vector<Variant>& vs, hipStream_t s, int rounds)
     // KB_BLOCKED=1: each variant's rounds back to back (after 3 untimed runs of
     // it), instead of interleaved -- no variant then runs behind another's
     // dirty lines or write-back.
+    if (std::getenv("KB_SCRUB") && !g_scrub)
+        CK(hipMalloc(&g_scrub, kScrubBytes));
     if (std::getenv("KB_BLOCKED")) {
         for (auto& v : vs) {
             for (int w = 0; w < 3; w++) v.run(s);
             for (int r = 0; r < rounds; r++) {
+                scrub(s);
                 CK(hipEventRecord(e0, s));
                 v.run(s);
                 CK(hipEventRecord(e1, s));
@@ -620,6 +665,7 @@ void run_variants(std::vector<Variant>& vs, hipStream_t s, int rounds)
     }
     for (int r = 0; r < rounds; r++) {
         for (auto& v : vs) {
+            scrub(s);
             CK(hipEventRecord(e0, s));
             v.run(s);
             CK(hipEventRecord(e1, s));
@@ -639,8 +685,60 @@ void run_variants(std::vector<Variant>& vs, hipStream_t s, int rounds)
     }
 }
 
+// RX roofline: the shipped verify against one-shot read ceilings of the same
+// bytes (KB_SCRUB=1: Infinity Cache cold before every timed launch).
+int rx_main(uint64_t n, int rounds)
+{
+    const uint32_t L = 1500;
+    const uint64_t stride = 1536, nb = n * stride;
+    uint8_t *rx, *v1;
+    uint32_t* sink;
+    CK(hipMalloc(&rx, nb));
+    CK(hipMalloc(&v1, n));
+    CK(hipMalloc(&sink, 4));
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    hipLaunchKernelGGL(k_init, dim3(4096), dim3(256), 0, s, rx, n, stride, L);
+    hipLaunchKernelGGL(k_hdr, dim3((n + 255) / 256), dim3(256), 0, s, rx, n, stride, L);
+    CK(launch_compute_fixed(rx, stride, L, n, nullptr, nullptr, 0, s));
+    CK(hipStreamSynchronize(s));
+    int dev = 0, cus = 0;
+    CK(hipGetDevice(&dev));
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    std::printf("RX roofline: n %llu x %u B, stride %llu, %.3f GB; scrub %s\n",
+                (unsigned long long)n, L, (unsigned long long)stride, nb / 1e9,
+                std::getenv("KB_SCRUB") ? "on (512 MiB write before each launch)" : "off");
+    const double vbytes = (double)n * (L + 1);
+    std::vector<Variant> vs;
+    vs.push_back({"verify (launch_verify_fixed, shipped)", vbytes, [&](hipStream_t st) {
+        CK(launch_verify_fixed(rx, stride, L, (u32)n, v1, 0u, st));
+    }});
+#define RD1(U_, X_)                                                                        \
+    vs.push_back({"read one-shot U=" #U_ " xcd=" #X_ " (batch bytes)", (double)nb,         \
+                  [&](hipStream_t st) {                                                   \
+        const uint64_t per = 256ull * U_ * 16;                                            \
+        hipLaunchKernelGGL((k_read1<U_, X_>), dim3((nb + per - 1) / per), dim3(256), 0, st, \
+                           rx, nb, sink);                                                 \
+    }});
+    RD1(3, true) RD1(3, false) RD1(4, true) RD1(6, true) RD1(8, true) RD1(12, true)
+    vs.push_back({"read grid-stride NT (round-1 ceiling)", (double)nb, [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_read<true>), dim3(cus * 8), dim3(256), 0, st, (const uint4*)rx,
+                           nb / 16, sink);
+    }});
+    run_variants(vs, s, rounds);
+    std::vector<uint8_t> h(n);
+    CK(hipMemcpy(h.data(), v1, n, hipMemcpyDeviceToHost));
+    size_t bad = 0;
+    for (auto b : h) bad += b != 0;
+    std::printf("non-accept verdicts: %zu (expect 0)\n", bad);
+    return 0;
+}
+
 int main(int argc, char** argv)
 {
+    if (argc > 1 && std::string(argv[1]) == "rx")
+        return rx_main(argc > 2 ? std::strtoull(argv[2], nullptr, 10) : (1u << 20),
+                       argc > 3 ? std::atoi(argv[3]) : 15);
     if (argc > 1 && std::string(argv[1]) == "imix")
         return imix_main(argc > 2 ? std::strtoull(argv[2], nullptr, 10) : (4u << 20),
                          argc > 3 ? std::atoi(argv[3]) : 10);
@@ -838,6 +936,7 @@ int main(int argc, char** argv)
         for (auto& v : vs) {
             for (int w = 0; w < 3; w++) v.run(s);
             for (int r = 0; r < rounds; r++) {
+                scrub(s);
                 CK(hipEventRecord(e0, s));
                 v.run(s);
                 CK(hipEventRecord(e1, s));
@@ -851,6 +950,7 @@ int main(int argc, char** argv)
     }
     for (int r = 0; r < rounds; r++) {
         for (auto& v : vs) {
+            scrub(s);
             CK(hipEventRecord(e0, s));
             v.run(s);
             CK(hipEventRecord(e1, s));
