@@ -162,9 +162,12 @@ def dominant_frac(n, L, compute_ms, verify_ms):
 
 
 def host_cpus():
-    """CPUs this process may run on and the cgroup CPU quota (the GPU box gives
-    a job a share of a large host: sched_getaffinity lists the whole machine,
-    cpu.max bounds what the job can use at once)."""
+    """CPUs this process may run on, ordered for the CPU baseline, and how
+    many it may use at once.  The GPU box gives a job a share of a large host:
+    sched_getaffinity lists the whole machine, the cgroup's cpu.max bounds
+    what runs at once.  Order: one hardware thread per physical core (SMT
+    siblings last), round-robin over the L3 domains (CCDs), so N threads get
+    N cores' worth of cache and memory links; CPU 0 (interrupts) last."""
     cpus = sorted(os.sched_getaffinity(0))
     quota = None
     try:
@@ -174,7 +177,29 @@ def host_cpus():
     except Exception:
         pass
     usable = len(cpus) if quota is None else max(1, min(len(cpus), int(quota)))
-    return cpus, usable, quota
+
+    def first_of(path, c):
+        try:
+            txt = open(f"/sys/devices/system/cpu/cpu{c}/{path}").read().strip()
+            return int(txt.replace("-", ",").split(",")[0])
+        except Exception:
+            return c
+
+    domains: dict[int, list[int]] = {}
+    siblings = []
+    for c in cpus:
+        if first_of("topology/thread_siblings_list", c) != c:
+            siblings.append(c)                 # a second hardware thread of a core
+            continue
+        domains.setdefault(first_of("cache/index3/shared_cpu_list", c), []).append(c)
+    order = []
+    lists = [sorted(v) for _, v in sorted(domains.items())]
+    for k in range(max((len(v) for v in lists), default=0)):
+        order += [v[k] for v in lists if k < len(v)]
+    order += siblings
+    if order and order[0] == 0 and len(order) > 1:
+        order = order[1:] + [0]
+    return order or cpus, usable, quota
 
 
 def cpu_baseline(tx, rx, stride, frame_len, budget_s, sample, torch):
@@ -203,7 +228,7 @@ def cpu_baseline(tx, rx, stride, frame_len, budget_s, sample, torch):
 
     cpus, usable, quota = host_cpus()
     one = [cpus[0]]
-    allc = cpus[:usable]
+    allc = cpus[:usable]            # spread over cores and L3 domains (host_cpus)
 
     def measure(pin, budget):
         rates = []
@@ -233,7 +258,9 @@ def cpu_baseline(tx, rx, stride, frame_len, budget_s, sample, torch):
         "gib_per_s": r1 * frame_len / 2**30,
         "multi_core": {"value": rmt / 1e9, "unit": "Gpkt/s", "cores": len(allc),
                        "gib_per_s": rmt * frame_len / 2**30, "passes": repsmt,
-                       "threads": f"one per usable host core, each {pinned} to its CPU",
+                       "threads": f"one per usable host core, each {pinned} to its CPU, "
+                                  "one per physical core, spread over the L3 domains",
+                       "cpus": allc,
                        "affinity_cpus": len(cpus), "cgroup_cpu_quota": quota},
         "cpu_model": cpu_model,
     }
@@ -425,43 +452,80 @@ def pcie_inclusive(gcs, torch, frame_len=1500, n=1 << 20):
     return out
 
 
-def plugin_bursts(gcs, reps=200):
+def plugin_bursts(gcs, reps=300):
     """Per-call latency of the entry points the io_module plugin calls on an
-    mTCP burst (gcs_verify_ptrs / gcs_compute_ptrs, recv_pkts / send_pkts):
-    64 frames scattered in pageable 2048 B rooms, as DPDK mbufs
-    (dpdk_module.c:76, 184-193); host batches <= 2 MiB run in direct mode."""
+    mTCP burst (gcs_verify_ptrs / gcs_compute_ptrs in recv_pkts / send_pkts):
+    64 frames, each in its own 2048 B room as DPDK mbufs hold them
+    (dpdk_module.c:76, 184-193).  Modes:
+      pageable_direct     rooms in pageable memory: gathered into pinned
+                          staging, one kernel launch + event wait per call
+      pageable_server     the same, served by the resident burst grid
+      registered_direct   rooms registered with gcs_host_register (an mbuf
+                          pool would be): read and filled in place over PCIe
+      registered_server   in place AND served by the resident grid
+    Timed in C (tools/libburst_timer.so, clock_gettime per call) when built,
+    else from Python (adds the interpreter's call overhead)."""
     import ctypes as C
     from mtcp_amd import synth
     L_ = gcs.lib()
-    out = {"workload": "64-frame bursts (mTCP MAX_PKT_BURST) in pageable 2048 B rooms, "
-                       f"median of {reps} calls"}
-    with gcs.Context(0, max_frames=1 << 12, max_bytes=16 << 20) as ctx:
-        for L in (64, 1500):
-            n = 64
-            src, stride = synth.fixed_frames(n, L, seed=L)
-            mb = np.zeros(n * 2048, dtype=np.uint8)
-            for i in range(n):
-                mb[i * 2048:i * 2048 + L] = src[i * stride:i * stride + L]
-            ptrs = (C.c_void_p * n)(*[mb.ctypes.data + i * 2048 for i in range(n)])
-            lens = np.full(n, L, dtype=np.uint16)
-            v = np.zeros(n, dtype=np.uint8)
-            st = np.zeros(n, dtype=np.uint8)
-            cs = np.zeros(n, dtype=np.uint32)
-            res = {}
-            for op in ("compute", "verify"):
-                ts = []
-                for _ in range(reps):
-                    t0 = time.perf_counter()
-                    if op == "verify":
-                        rc = L_.gcs_verify_ptrs(ctx.h, ptrs, lens.ctypes.data, n, v.ctypes.data, 0)
-                    else:
-                        rc = L_.gcs_compute_ptrs(ctx.h, ptrs, lens.ctypes.data, n,
-                                                 st.ctypes.data, cs.ctypes.data)
-                    ts.append(time.perf_counter() - t0)
-                    gcs.check(rc, op)
-                res[op + "_us"] = float(np.median(ts) * 1e6)
-            assert int((v != 0).sum()) == 0 and int((st != 0).sum()) == 0
-            out[f"64x{L}B"] = res
+    tpath = os.path.join(ROOT, "tools", "libburst_timer.so")
+    T = C.CDLL(tpath) if os.path.exists(tpath) else None
+    out = {"workload": "64-frame bursts (mTCP MAX_PKT_BURST) in 2048 B rooms, median of "
+                       f"{reps} calls",
+           "timer": "C clock_gettime per call" if T else "python perf_counter per call"}
+    n = 64
+    rooms = np.zeros(n * 2048 + 4096, dtype=np.uint8)
+    base = (-rooms.ctypes.data) % 4096               # page-aligned rooms (registrable)
+    mb = rooms[base:base + n * 2048]
+    for mode in ("pageable_direct", "pageable_server", "registered_direct",
+                 "registered_server"):
+        registered = mode.startswith("registered")
+        if registered:
+            gcs.check(L_.gcs_host_register(mb.ctypes.data, mb.nbytes), "register")
+        res = {}
+        try:
+            with gcs.Context(0, max_frames=1 << 12, max_bytes=16 << 20) as ctx:
+                if mode.endswith("server"):
+                    ctx.set_burst_server(True)
+                for L in (64, 1500):
+                    src, stride = synth.fixed_frames(n, L, seed=L)
+                    for i in range(n):
+                        mb[i * 2048:i * 2048 + L] = src[i * stride:i * stride + L]
+                    ptrs = (C.c_void_p * n)(*[mb.ctypes.data + i * 2048 for i in range(n)])
+                    lens = np.full(n, L, dtype=np.uint16)
+                    v = np.zeros(n, dtype=np.uint8)
+                    st = np.zeros(n, dtype=np.uint8)
+                    cs = np.zeros(n, dtype=np.uint32)
+                    r = {}
+                    for op in ("compute", "verify"):
+                        fn = L_.gcs_verify_ptrs if op == "verify" else L_.gcs_compute_ptrs
+                        outp = v if op == "verify" else st
+                        extra = None if op == "verify" else cs.ctypes.data
+                        if T is not None:
+                            us = np.zeros(reps, dtype=np.float64)
+                            gcs.check(T.bt_run(C.cast(fn, C.c_void_p), ctx.h, ptrs,
+                                               C.c_void_p(lens.ctypes.data), C.c_uint32(n),
+                                               C.c_void_p(outp.ctypes.data), C.c_void_p(extra),
+                                               C.c_uint32(reps), C.c_void_p(us.ctypes.data)),
+                                      op)
+                            ts = us
+                        else:
+                            ts = []
+                            for _ in range(reps):
+                                t0 = time.perf_counter()
+                                rc = (fn(ctx.h, ptrs, lens.ctypes.data, n, v.ctypes.data, 0)
+                                      if op == "verify" else
+                                      fn(ctx.h, ptrs, lens.ctypes.data, n, st.ctypes.data,
+                                         cs.ctypes.data))
+                                ts.append((time.perf_counter() - t0) * 1e6)
+                                gcs.check(rc, op)
+                        r[op + "_us"] = float(np.median(ts))
+                    assert int((v != 0).sum()) == 0 and int((st != 0).sum()) == 0
+                    res[f"64x{L}B"] = r
+        finally:
+            if registered:
+                gcs.check(L_.gcs_host_unregister(mb.ctypes.data), "unregister")
+        out[mode] = res
     return out
 
 

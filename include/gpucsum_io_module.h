@@ -62,6 +62,9 @@
  * Frames whose queue is not this thread's own are counted in rx_foreign --
  * flows that mTCP's RSS-aware address pool (addr_pool.c:168,251) would have
  * placed on another core.
+ * Burst server: each thread's context serves its bursts through a resident
+ * grid polling a pinned mailbox (gcs_ctx_set_burst_server) unless the
+ * environment sets GPUCSUM_BURST_SERVER=0 (then: one kernel launch per burst).
  * Threading (core.c:1153-1245): load_module once on the main thread; every
  * other call from the owning mTCP thread.  Per-thread state is keyed by the
  * mtcp_thread_context pointer; mTCP thread k uses GPU k mod n_gpus (override:

@@ -134,6 +134,16 @@ int gcs_ctx_device(const gcs_ctx *ctx, int *device);
 int gcs_ctx_stream(const gcs_ctx *ctx, void **stream);   /* hipStream_t */
 int gcs_sync(gcs_ctx *ctx);                               /* wait for ctx stream */
 
+/* Burst server (on = 1): host batches small enough for direct mode (the
+ * kernel reads pinned staging over PCIe: an mTCP burst) are served by a
+ * resident grid that polls a mailbox in pinned memory, instead of one kernel
+ * launch and one event wait per batch.  The grid leaves after
+ * GCS_SERVER_IDLE_US (default 200) without work and after GCS_SERVER_LIFE_US
+ * (default 2000) in total; a later batch starts it again.  Other work on the
+ * context makes it leave first.  Default: off, or the environment variable
+ * GCS_BURST_SERVER=1 at gcs_ctx_create. */
+int gcs_ctx_set_burst_server(gcs_ctx *ctx, int on);
+
 /* Pinned host memory for zero-copy host batches: when every frame of a
  * gcs_verify / gcs_compute call lies in pinned memory (allocated here, or an
  * existing buffer such as an mbuf pool registered with gcs_host_register) and

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <condition_variable>
 #include <cstdio>
@@ -110,6 +111,7 @@ struct Slot {
     uint16_t* m_queue = nullptr;
     // bookkeeping of the chunk in flight
     bool busy = false;
+    bool served = false;           // results already complete (burst server)
     uint32_t first = 0, count = 0;
 };
 
@@ -228,6 +230,179 @@ class GatherPool {
 
 }  // namespace
 
+namespace {
+
+// Host side of the burst server (gcs_kernels.hip k_burst_server): small host
+// batches in direct mode are posted to a resident grid through a mailbox in
+// pinned fine-grained memory, instead of one kernel launch + event wait each.
+// The grid lives at most life_us and leaves after idle_us without work; a
+// batch posted to a grid that has gone (or is going) is served by a fresh
+// launch, so every batch completes and the grid never outlives its bounds.
+class BurstServer {
+  public:
+    ~BurstServer()
+    {
+        if (prof_ && prof_n_)
+            std::fprintf(stderr,
+                         "[gcs burst server] %llu requests: request writes %.2f us; post->ack "
+                         "%.2f us, of which serving %.2f us and release fence %.2f us "
+                         "(slowest block)\n",
+                         (unsigned long long)prof_n_, prof_write_ / prof_n_, prof_total_ / prof_n_,
+                         prof_serve_ / prof_n_, prof_release_ / prof_n_);
+        (void)stop();
+        if (stream_) (void)hipStreamDestroy(stream_);
+        if (mb_) (void)hipHostFree(mb_);
+    }
+
+    int init(int device)
+    {
+        HIP_TRY(hipHostMalloc((void**)&mb_, sizeof(gcs::ServerMailbox),
+                              hipHostMallocCoherent | hipHostMallocMapped));
+        std::memset(mb_, 0, sizeof(gcs::ServerMailbox));
+        HIP_TRY(hipHostGetDevicePointer((void**)&dmb_, mb_, 0));
+        HIP_TRY(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+        int khz = 0;
+        HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
+        const double ticks_per_us = ticks_per_us_ = khz > 0 ? khz / 1000.0 : 100.0;
+        const char* e = std::getenv("GCS_SERVER_IDLE_US");
+        idle_ticks_ = (uint64_t)((e ? std::atof(e) : 200.0) * ticks_per_us);
+        e = std::getenv("GCS_SERVER_LIFE_US");
+        life_ticks_ = (uint64_t)((e ? std::atof(e) : 2000.0) * ticks_per_us);
+        prof_ = std::getenv("GCS_SERVER_PROF") != nullptr;
+        return GCS_OK;
+    }
+
+    // Serve one request (n <= gcs::kServerMaxFrames): frames at device address
+    // `frames` (bytes, a multiple of 16), frame i at off[i], len[i] bytes.
+    // Returns when every block has acknowledged it, with the verdicts /
+    // statuses in code[] and, for a fill, the checks in csum[].
+    int serve(uint8_t* frames, uint64_t bytes, const uint64_t* off, const uint16_t* len,
+              uint32_t n, bool compute, uint32_t flags, uint8_t* code, uint32_t* csum)
+    {
+        if (launched_ && any_exited()) {
+            int rc = wait_exit();
+            if (rc) return rc;
+        }
+        if (!launched_) {
+            int rc = launch(seq_);
+            if (rc) return rc;
+        }
+        const uint32_t q = ++seq_;
+        const auto tw = std::chrono::steady_clock::now();
+        // each 16 B line: its fields, then its seq (x86 keeps the order)
+        for (uint32_t i = 0; i < n; i++) {
+            gcs::ServerDesc& d = mb_->desc[i];
+            d.off = off[i];
+            d.len = len[i];
+            __atomic_store_n(&d.seq, q, __ATOMIC_RELEASE);
+        }
+        mb_->b.frames = reinterpret_cast<uint64_t>(frames);
+        mb_->b.bytes16 = (uint32_t)(bytes / 16);
+        __atomic_store_n(&mb_->b.seq, q, __ATOMIC_RELEASE);
+        mb_->a.n = n;
+        mb_->a.mode = (compute ? 1u : 0u) | (flags << 1);
+        const auto t0 = std::chrono::steady_clock::now();
+        __atomic_store_n(&mb_->a.seq, q, __ATOMIC_RELEASE);
+        for (;;) {
+            bool all = true, gone = false;
+            for (int b = 0; b < gcs::kServerBlocks; b++) {
+                if (__atomic_load_n(&mb_->ack[b].v, __ATOMIC_ACQUIRE) == q)
+                    continue;
+                all = false;
+                if (__atomic_load_n(&mb_->state[b].v, __ATOMIC_ACQUIRE) == 2)
+                    gone = true;
+            }
+            if (all)
+                break;
+            if (gone) {
+                // the grid left before serving q: a fresh grid serves it again
+                // (blocks that had served it redo their share: same results)
+                int rc = wait_exit();
+                if (!rc) rc = launch(q - 1);
+                if (rc) return rc;
+                continue;
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+                (void)stop();
+                std::snprintf(g_hip_err, sizeof g_hip_err, "burst server: no answer in 2 s");
+                return GCS_EHIP;
+            }
+            __builtin_ia32_pause();
+        }
+        if (code)
+            std::memcpy(code, mb_->code, n);
+        if (compute && csum)
+            std::memcpy(csum, mb_->csum, n * sizeof(uint32_t));
+        if (prof_) {
+            // GCS_SERVER_PROF: per request, the slowest block's serve and
+            // release times (wall clock), averaged and printed at exit
+            double sv = 0, rl = 0;
+            for (int b = 0; b < gcs::kServerBlocks; b++) {
+                sv = std::max(sv, (double)(mb_->prof[b][1] - mb_->prof[b][0]));
+                rl = std::max(rl, (double)(mb_->prof[b][2] - mb_->prof[b][1]));
+            }
+            prof_n_++;
+            prof_serve_ += sv / ticks_per_us_;
+            prof_release_ += rl / ticks_per_us_;
+            prof_total_ += std::chrono::duration<double, std::micro>(
+                               std::chrono::steady_clock::now() - t0).count();
+            prof_write_ += std::chrono::duration<double, std::micro>(t0 - tw).count();
+        }
+        return GCS_OK;
+    }
+
+    // Ask the grid to leave and wait until it has.
+    int stop()
+    {
+        if (!launched_) return GCS_OK;
+        __atomic_store_n(&mb_->a.cmd, 1u, __ATOMIC_RELEASE);
+        return wait_exit();
+    }
+
+  private:
+    bool any_exited() const
+    {
+        for (int b = 0; b < gcs::kServerBlocks; b++)
+            if (__atomic_load_n(&mb_->state[b].v, __ATOMIC_ACQUIRE) == 2)
+                return true;
+        return false;
+    }
+
+    // Every block ends within life_ticks of its start (or at the exit
+    // command); the stream sync then confirms the grid has drained.
+    int wait_exit()
+    {
+        HIP_TRY(hipStreamSynchronize(stream_));
+        launched_ = false;
+        return GCS_OK;
+    }
+
+    int launch(uint32_t done)
+    {
+        for (int b = 0; b < gcs::kServerBlocks; b++)
+            __atomic_store_n(&mb_->state[b].v, 0u, __ATOMIC_RELAXED);
+        __atomic_store_n(&mb_->a.cmd, 0u, __ATOMIC_RELEASE);
+        HIP_TRY(gcs::launch_burst_server(dmb_, done, idle_ticks_, life_ticks_, kMaxPolls,
+                                         prof_, stream_));
+        launched_ = true;
+        return GCS_OK;
+    }
+
+    static constexpr uint32_t kMaxPolls = 1u << 22;   // hard bound beside the clock
+    gcs::ServerMailbox* mb_ = nullptr;    // host view
+    gcs::ServerMailbox* dmb_ = nullptr;   // device view
+    hipStream_t stream_ = nullptr;
+    uint64_t idle_ticks_ = 0, life_ticks_ = 0;
+    uint32_t seq_ = 0;
+    bool launched_ = false;
+    bool prof_ = false;
+    double ticks_per_us_ = 100.0;
+    uint64_t prof_n_ = 0;
+    double prof_total_ = 0, prof_serve_ = 0, prof_release_ = 0, prof_write_ = 0;
+};
+
+}  // namespace
+
 struct gcs_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -240,6 +415,7 @@ struct gcs_ctx {
     bool direct_spread = true; // direct mode on k_desc (8 frames per block), not k_desc_mixed
     Slot slot[kSlots];
     std::unique_ptr<GatherPool> pool;
+    std::unique_ptr<BurstServer> server;   // gcs_ctx_set_burst_server / GCS_BURST_SERVER
 
     // Copy work for `count` frames / `bytes` bytes: inline when small, else
     // spread over the gather pool.
@@ -390,6 +566,42 @@ bool is_pinned(const void* p, uint64_t bytes)
     return true;
 }
 
+// tcp_in.c:1237 (tcph->check = 0 on a TCP checksum failure), on the host copy.
+template <class FramePtr>
+void zero_bad_tcp_checks(const uint8_t* code, uint32_t n, FramePtr frame_ptr, const uint16_t* len)
+{
+    for (uint32_t i = 0; i < n; i++) {
+        if (code[i] != GCS_V_DROP_TCPCSUM)
+            continue;
+        uint8_t* f = frame_ptr(i);
+        uint32_t ts = 14 + 4u * (f[14] & 15u);
+        if (ts + 18 <= len[i])
+            f[ts + 16] = f[ts + 17] = 0;
+    }
+}
+
+// Host regions registered with gcs_host_register, with their device views.
+// A host batch whose frames all lie in one of them can be served in place.
+struct RegRegion {
+    uint8_t* host;
+    uint64_t bytes;
+    uint8_t* dev;
+};
+std::mutex g_reg_mu;
+std::vector<RegRegion> g_regions;
+
+bool find_region(const void* p, RegRegion* out)
+{
+    const uint8_t* q = static_cast<const uint8_t*>(p);
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    for (const auto& r : g_regions)
+        if (q >= r.host && q < r.host + r.bytes) {
+            *out = r;
+            return true;
+        }
+    return false;
+}
+
 // Generic staged host batch.  Frames are addressed by base + off[i] or by
 // ptrs[i]; `compute` selects TX fill vs RX verify.
 //
@@ -434,8 +646,10 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
         {
             for (auto& s : c->slot)
                 if (s.busy) {
-                    (void)hipEventSynchronize(s.done);
+                    if (!s.served)
+                        (void)hipEventSynchronize(s.done);
                     s.busy = false;
+                    s.served = false;
                 }
         }
     } slot_reset{ctx};
@@ -453,8 +667,10 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
     auto drain = [&](Slot& s) -> int {
         if (!s.busy)
             return GCS_OK;
-        HIP_TRY(hipEventSynchronize(s.done));
+        if (!s.served)
+            HIP_TRY(hipEventSynchronize(s.done));
         s.busy = false;
+        s.served = false;
         if (!compute) {
             std::memcpy(code + s.first, s.h_code, s.count);
             if (hash)
@@ -477,6 +693,61 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
         });
         return GCS_OK;
     };
+
+    // In-place mode: a small batch whose frames all lie in ONE registered
+    // region (e.g. an mbuf pool registered with gcs_host_register) at 16 B-
+    // aligned addresses.  The kernel reads -- and for TX fills -- the frames
+    // where they are, over PCIe: no gather into staging, no scatter back.
+    if (!classify && !(flags & GCS_VF_ICMP) && n <= ctx->max_frames && ctx->direct_max) {
+        RegRegion reg{};
+        uint32_t first = 0;
+        while (first < n && !frame_ptr(first))
+            first++;
+        bool ok = first < n && find_region(frame_ptr(first), &reg);
+        uint64_t total = 0;
+        for (uint32_t i = 0; ok && i < n; i++) {
+            const uint8_t* p = frame_ptr(i);
+            if (!p)
+                continue;
+            // inside the region's whole 16 B chunks (the kernel never reads past them)
+            ok = p >= reg.host && (uint64_t)(p - reg.host) + len[i] <= (reg.bytes & ~15ull) &&
+                 ((uintptr_t)p & 15) == 0;
+            total += len[i];
+        }
+        if (ok && total <= ctx->direct_max) {
+            Slot& s = ctx->slot[0];
+            for (auto& sl : ctx->slot) {
+                int rc = drain(sl);
+                if (rc) return rc;
+            }
+            for (uint32_t i = 0; i < n; i++) {
+                const uint8_t* p = frame_ptr(i);
+                s.h_off[i] = p ? (uint64_t)(p - reg.host) : 0;
+                s.h_len[i] = p ? len[i] : 0;
+            }
+            if (ctx->server && n <= (uint32_t)gcs::kServerMaxFrames) {
+                int rc = ctx->server->serve(reg.dev, reg.bytes & ~15ull, s.h_off, s.h_len, n,
+                                            compute, 0u, s.h_code, compute ? s.h_csum : nullptr);
+                if (rc) return rc;
+            } else {
+                if (compute)
+                    HIP_TRY(gcs::launch_compute_desc_spread(reg.dev, reg.bytes, s.m_off, s.m_len,
+                                                            n, s.m_code, s.m_csum, 0u, s.stream));
+                else
+                    HIP_TRY(gcs::launch_verify_desc_spread(reg.dev, reg.bytes, s.m_off, s.m_len,
+                                                           n, s.m_code, 0u, s.stream));
+                HIP_TRY(hipEventRecord(s.done, s.stream));
+                HIP_TRY(hipEventSynchronize(s.done));
+            }
+            if (code)
+                std::memcpy(code, s.h_code, n);
+            if (compute && csums)
+                std::memcpy(csums, s.h_csum, n * sizeof(uint32_t));
+            if (!compute && (flags & GCS_VF_ZERO_BAD_TCP_CHECK))
+                zero_bad_tcp_checks(code, n, frame_ptr, len);
+            return GCS_OK;
+        }
+    }
 
     uint32_t next = 0;
     int k = 0;
@@ -551,6 +822,24 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
                                    hipMemcpyHostToDevice, s.stream));
         }
         const bool spread = direct && ctx->direct_spread && !(flags & GCS_VF_ICMP);
+        if (spread && !classify && ctx->server && cnt <= (uint32_t)gcs::kServerMaxFrames) {
+            // resident grid: no launch, no event; results complete on return
+            int rc = ctx->server->serve(frames_d, (used + 15) / 16 * 16, s.h_off, s.h_len, cnt,
+                                        compute, compute ? GCS_CF_NO_INPLACE : 0u, s.h_code,
+                                        compute ? s.h_csum : nullptr);
+            if (rc) return rc;
+            s.busy = true;
+            s.served = true;
+            next += cnt;
+            k++;
+            continue;
+        }
+        if (ctx->server) {
+            // other work on this context's streams: the grid leaves first, so
+            // nothing queues behind it on a shared hardware queue
+            int rc = ctx->server->stop();
+            if (rc) return rc;
+        }
         if (compute && spread) {
             HIP_TRY(gcs::launch_compute_desc_spread(frames_d, used, off_d, len_d, cnt, code_d,
                                                     csum_d, GCS_CF_NO_INPLACE, s.stream));
@@ -591,16 +880,8 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
         int rc = drain(s);
         if (rc) return rc;
     }
-    if (!compute && (flags & GCS_VF_ZERO_BAD_TCP_CHECK)) {
-        for (uint32_t i = 0; i < n; i++) {
-            if (code[i] != GCS_V_DROP_TCPCSUM)
-                continue;
-            uint8_t* f = frame_ptr(i);
-            uint32_t ts = 14 + 4u * (f[14] & 15u);
-            if (ts + 18 <= len[i])
-                f[ts + 16] = f[ts + 17] = 0;          // tcp_in.c:1237
-        }
-    }
+    if (!compute && (flags & GCS_VF_ZERO_BAD_TCP_CHECK))
+        zero_bad_tcp_checks(code, n, frame_ptr, len);
     return GCS_OK;
 }
 
@@ -666,6 +947,12 @@ try {
         ctx->direct_max = std::strtoull(e, nullptr, 10);
     if (const char* e = std::getenv("GCS_DIRECT_SPREAD"))
         ctx->direct_spread = std::atoi(e) != 0;
+    if (const char* e = std::getenv("GCS_BURST_SERVER")) {
+        if (std::atoi(e) != 0 && (rc = gcs_ctx_set_burst_server(ctx, 1)) != GCS_OK) {
+            gcs_ctx_destroy(ctx);
+            return rc;
+        }
+    }
     if (max_frames && max_bytes) {
         // split the requested staging between the two slots
         ctx->max_frames = std::max<uint32_t>(1, max_frames / kSlots + 1);
@@ -688,6 +975,7 @@ try {
         return GCS_EINVAL;
     {
         DeviceGuard g(ctx->device);
+        ctx->server.reset();   // exit command, wait for the grid to drain
         for (auto& s : ctx->slot) {
             if (s.stream)
                 (void)hipStreamSynchronize(s.stream);
@@ -746,7 +1034,11 @@ int gcs_host_register(void* p, uint64_t bytes)
 try {
     if (!p || bytes == 0)
         return GCS_EINVAL;
-    HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterDefault));
+    HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterMapped));
+    uint8_t* dev = nullptr;
+    HIP_TRY(hipHostGetDevicePointer((void**)&dev, p, 0));
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_regions.push_back(RegRegion{static_cast<uint8_t*>(p), bytes, dev});
     return GCS_OK;
 } GCS_CATCH
 
@@ -754,6 +1046,14 @@ int gcs_host_unregister(void* p)
 try {
     if (!p)
         return GCS_EINVAL;
+    {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        for (auto it = g_regions.begin(); it != g_regions.end(); ++it)
+            if (it->host == p) {
+                g_regions.erase(it);
+                break;
+            }
+    }
     HIP_TRY(hipHostUnregister(p));
     return GCS_OK;
 } GCS_CATCH
@@ -904,6 +1204,25 @@ try {
     DeviceGuard g(ctx->device);
     HIP_TRY(gcs::launch_icmp_fn(d_buf, buf_bytes, d_off, d_len, n, d_out,
                                 pick_stream(ctx, stream)));
+    return GCS_OK;
+} GCS_CATCH
+
+int gcs_ctx_set_burst_server(gcs_ctx* ctx, int on)
+try {
+    if (!ctx)
+        return GCS_EINVAL;
+    DeviceGuard g(ctx->device);
+    if (!on) {
+        ctx->server.reset();
+        return GCS_OK;
+    }
+    if (ctx->server)
+        return GCS_OK;
+    std::unique_ptr<BurstServer> sv(new BurstServer());
+    int rc = sv->init(ctx->device);
+    if (rc)
+        return rc;
+    ctx->server = std::move(sv);
     return GCS_OK;
 } GCS_CATCH
 

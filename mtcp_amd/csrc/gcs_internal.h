@@ -17,6 +17,57 @@ struct Ext {
     uint32_t nq, nq_magic, endian;   // nq_magic = ceil(2^32 / nq) (0 for nq == 1)
 };
 
+// Burst server (gcs_api.cpp BurstServer, gcs_kernels.hip k_burst_server): a
+// short-lived resident grid that takes host batches from a mailbox in pinned
+// fine-grained memory instead of one kernel launch per batch.
+//
+// One poll is ONE load instruction of wave 0 of each block: lane 0 reads
+// request line A, lane 1 line B, lanes 2.. the descriptors of the block's
+// first frames.  Each 16 B line is read in one piece, and every line carries
+// the request number, so a poll that sees seq q in all the lines it needs
+// has a consistent request (the host writes each line's fields before its
+// seq, and the lines before line A's seq).  Results go to fixed arrays of the
+// mailbox; each block then writes ack[b] = q (release).
+constexpr int kServerBlocks = 8;
+constexpr int kServerMaxFrames = 4096;
+struct alignas(16) ServerReqA {
+    uint32_t seq;                       // request number (written last)
+    uint32_t cmd;                       // 0 = serve, 1 = exit now
+    uint32_t n;                         // frames
+    uint32_t mode;                      // bit 0: compute (TX fill); bits 1..: flags
+};
+struct alignas(16) ServerReqB {
+    uint64_t frames;                    // device address of the frame buffer
+    uint32_t bytes16;                   // its size / 16
+    uint32_t seq;
+};
+struct alignas(16) ServerDesc {
+    uint64_t off;
+    uint16_t len;
+    uint16_t pad;
+    uint32_t seq;
+};
+struct alignas(64) ServerLine {
+    uint32_t v;
+    uint32_t pad[15];
+};
+struct ServerMailbox {
+    ServerReqA a;                        // host
+    ServerReqB b;                        // host
+    uint8_t pad0[32];
+    ServerLine ack[kServerBlocks];       // device
+    ServerLine state[kServerBlocks];     // device: 1 serving, 2 exited
+    uint64_t prof[kServerBlocks][8];     // device, GCS_SERVER_PROF: wall-clock marks of
+                                         // the last request (seen, served, released)
+    ServerDesc desc[kServerMaxFrames];   // host
+    uint8_t code[kServerMaxFrames];      // device: verdicts / TX statuses
+    uint32_t csum[kServerMaxFrames];     // device: TX checks (ip | tcp << 16)
+};
+
+hipError_t launch_burst_server(ServerMailbox* mb, uint32_t done_seq, uint64_t idle_ticks,
+                               uint64_t life_ticks, uint32_t max_polls, bool prof,
+                               hipStream_t s);
+
 hipError_t launch_verify_fixed(uint8_t* frames, uint64_t stride, uint32_t frame_len, uint32_t n,
                                uint8_t* verdict, uint32_t flags, hipStream_t s);
 hipError_t launch_compute_fixed(uint8_t* frames, uint64_t stride, uint32_t frame_len, uint32_t n,

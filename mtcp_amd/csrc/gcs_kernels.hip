@@ -210,6 +210,159 @@ k_desc(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __re
                                                 out_csum ? out_csum + i : nullptr);
 }
 
+// Burst server: a grid of kServerBlocks blocks that stays resident for at most
+// life_ticks (wall clock) and serves host batches posted in a mailbox
+// (gcs_internal.h ServerMailbox) -- each batch with the per-frame work of
+// k_desc<G,U> (frames in pinned host memory, read and written over PCIe),
+// without a kernel launch and event wait per batch.
+//
+// Every block ends: on the host's exit command, after idle_ticks without a
+// request, after life_ticks in total, or after max_polls polls -- whichever
+// comes first, so the grid always drains and work queued behind it on the
+// same hardware queue waits at most life_ticks.  All decisions are taken by
+// thread 0 from the poll's lines in LDS and broadcast (block-uniform control
+// flow: no wave leaves the loop while another waits at a barrier).
+template <int G, int U, bool PROF, int kPollWaves>
+__global__ void __launch_bounds__(kBlock)
+k_burst_server(ServerMailbox* mb, uint32_t done_seq, uint64_t idle_ticks, uint64_t life_ticks,
+               uint32_t max_polls)
+{
+    enum { IDLE = 0, WORK = 1, EXIT = 2 };
+    constexpr int FPB = kBlock / G;
+    // kPollWaves = 2: a second wave polls half a round trip behind the first
+    __shared__ uint4 s_line[2 + FPB];
+    __shared__ uint32_t s_claim;             // IDLE until a polling wave claims WORK / EXIT
+    const int t = threadIdx.x, sub = t & (G - 1), grp = t / G;
+    const int wave = t >> 6, lane = t & 63;
+    uint32_t last = done_seq, polls = 0;
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    uint64_t t_last = t_start;
+    if (t == 0) {
+        s_claim = IDLE;
+        __hip_atomic_store(&mb->state[blockIdx.x].v, 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __syncthreads();
+    // what lane < 2 + FPB of a polling wave reads each poll
+    const volatile u32x4* src = nullptr;
+    if (lane == 0)
+        src = reinterpret_cast<const volatile u32x4*>(&mb->a);
+    else if (lane == 1)
+        src = reinterpret_cast<const volatile u32x4*>(&mb->b);
+    else if (lane < 2 + FPB)
+        src = reinterpret_cast<const volatile u32x4*>(&mb->desc[blockIdx.x * FPB + lane - 2]);
+    for (;;) {
+        if (wave < kPollWaves) {
+            if (wave == 1)
+                __builtin_amdgcn_s_sleep(32);   // stagger: ~2k cycles behind wave 0
+            for (;;) {
+                if (__hip_atomic_load(&s_claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+                    break;                      // the other polling wave has claimed
+                u32x4 v = {0, 0, 0, 0};
+                if (src)
+                    v = *src;                   // one 16 B read per lane, one round trip
+                // lane 0 judges the poll from the lanes' lines (wave-wide shuffles)
+                const uint32_t q = __shfl(v.x, 0), cmd = __shfl(v.y, 0), n = __shfl(v.z, 0);
+                const uint32_t bseq = __shfl(v.w, 1);
+                bool ok = bseq == q;
+                for (int j = 0; j < FPB; j++) {
+                    const uint32_t dseq = __shfl(v.w, 2 + j);
+                    if (blockIdx.x * FPB + j < n && dseq != q)
+                        ok = false;
+                }
+                const uint64_t now = __builtin_amdgcn_s_memrealtime();
+                uint32_t act = IDLE;
+                if (cmd != 0 || now - t_start > life_ticks || ++polls >= max_polls)
+                    act = EXIT;
+                else if (q != last)
+                    act = ok ? WORK : IDLE;     // torn poll: look again
+                else if (now - t_last > idle_ticks)
+                    act = EXIT;
+                if (act == IDLE) {
+                    __builtin_amdgcn_s_sleep(2);
+                    continue;
+                }
+                uint32_t won = 0;
+                if (lane == 0)
+                    won = atomicCAS(&s_claim, (uint32_t)IDLE, act) == IDLE;
+                won = __shfl(won, 0);
+                if (won && lane < 2 + FPB)
+                    s_line[lane] = make_uint4(v.x, v.y, v.z, v.w);
+                break;
+            }
+        }
+        __syncthreads();
+        const uint32_t act = s_claim;
+        if (act == EXIT)
+            break;
+        // a request: its lines were written before its seq (fence-acquire
+        // after observing it: later loads see everything the host wrote)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        const uint64_t t_seen = __builtin_amdgcn_s_memrealtime();
+        const uint4 a = s_line[0], b = s_line[1];
+        const uint32_t q = a.x, n = a.z, compute = a.w & 1u, flags = a.w >> 1;
+        uint8_t* frames = reinterpret_cast<uint8_t*>((uint64_t)b.x | ((uint64_t)b.y << 32));
+        const uint64_t bytes = (uint64_t)b.z * 16;
+        const uint4 d0 = s_line[2 + grp];
+        for (uint32_t i = blockIdx.x * FPB + grp, pass = 0; i < n;
+             i += gridDim.x * FPB, pass++) {
+            const uint4 d = pass == 0 ? d0 : *reinterpret_cast<const uint4*>(&mb->desc[i]);
+            const uint64_t o = (uint64_t)d.x | ((uint64_t)d.y << 32);
+            const u32 len = d.z & 0xFFFFu;
+            const bool ok = (o & 15) == 0 && o <= bytes && len <= bytes - o;
+            uint8_t* f = frames + (ok ? o : 0);
+            const int64_t avail = ok ? (int64_t)(bytes - o) : 0;
+            if (compute)
+                do_frame<G, U, true, true, true, kNT, kWM>(f, len, avail, ok, sub, flags,
+                                                           mb->code + i, mb->csum + i);
+            else
+                do_frame<G, U, false, true, true, kNT, kWM>(f, len, avail, ok, sub, flags,
+                                                            mb->code + i, nullptr);
+        }
+        uint64_t t_served = 0;
+        if (PROF) {
+            __syncthreads();
+            t_served = __builtin_amdgcn_s_memrealtime();
+        }
+        __threadfence_system();              // this wave's results reach host memory
+        __syncthreads();                     // every wave done with s_line / s_claim
+        if (t == 0) {
+            if (PROF) {
+                mb->prof[blockIdx.x][0] = t_seen;
+                mb->prof[blockIdx.x][1] = t_served;
+                mb->prof[blockIdx.x][2] = __builtin_amdgcn_s_memrealtime();
+                mb->prof[blockIdx.x][3] = polls;
+            }
+            s_claim = IDLE;
+            __hip_atomic_store(&mb->ack[blockIdx.x].v, q, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        last = q;
+        t_last = __builtin_amdgcn_s_memrealtime();
+        __syncthreads();                     // s_claim reset before anyone polls again
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (t == 0)
+        __hip_atomic_store(&mb->state[blockIdx.x].v, 2u, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_burst_server(ServerMailbox* mb, uint32_t done_seq, uint64_t idle_ticks,
+                               uint64_t life_ticks, uint32_t max_polls, bool prof,
+                               hipStream_t s)
+{
+    // One polling wave: a second one, half a round trip behind, measured no
+    // faster (64 x 1500 B: 8.5-9.2 vs 8.5-8.7 us, profiles/r02/burst_latency.md).
+    if (prof)
+        hipLaunchKernelGGL((k_burst_server<32, 3, true, 1>), dim3(kServerBlocks), dim3(kBlock),
+                           0, s, mb, done_seq, idle_ticks, life_ticks, max_polls);
+    else
+        hipLaunchKernelGGL((k_burst_server<32, 3, false, 1>), dim3(kServerBlocks), dim3(kBlock),
+                           0, s, mb, done_seq, idle_ticks, life_ticks, max_polls);
+    return hipGetLastError();
+}
+
 // Mixed-size descriptor batch (IMIX, plugin bursts): a block takes 256
 // consecutive frames, keeps their validated descriptors in LDS, sorts them
 // into three LDS lists by size, and runs each list on a group shape that fits
@@ -224,10 +377,17 @@ k_desc(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __re
 // spill at 6 waves per SIMD and lose (kbench imix).
 // F = descriptors per block (<= kBlock): fewer per block means more, shorter
 // blocks -- a smaller tail when large frames make every block long.
-template <int G0_, int U0_, int G1_, int U1_, int G2_, int U2_, int WM_ = kWM, int F_ = kBlock>
+// ORDERED: the class lists keep frame order (wave ballot + prefix count)
+// instead of atomicAdd arrival order, so the groups of one list instruction
+// work on neighbouring frames: a wave's 64 B-class loads and sector stores
+// then cover runs of adjacent frames (two frames per 128 B line) instead of
+// frames scattered over the block's whole range.
+template <int G0_, int U0_, int G1_, int U1_, int G2_, int U2_, int WM_ = kWM, int F_ = kBlock,
+          bool ORDERED_ = true>
 struct DescShape {
     static constexpr int G0 = G0_, U0 = U0_, G1 = G1_, U1 = U1_, G2 = G2_, U2 = U2_, WM = WM_;
     static constexpr int F = F_;
+    static constexpr bool ORDERED = ORDERED_;
     static_assert(F <= kBlock, "one descriptor per thread");
     static constexpr int T0 = 16 * G0 * U0, T1 = 16 * G1 * U1;
 };
@@ -277,6 +437,7 @@ __device__ __forceinline__ void desc_mixed(uint8_t* __restrict__ frames, uint64_
     __shared__ uint16_t slen[F];
     __shared__ uint16_t list[3][F];
     __shared__ int cnt[3];
+    __shared__ int wcnt[3][kBlock / 64];
     __shared__ uint8_t codes[F];
     __shared__ uint32_t csums[COMPUTE ? F : 1];
     __shared__ uint32_t hashes[EXT && !COMPUTE ? F : 1];
@@ -289,6 +450,7 @@ __device__ __forceinline__ void desc_mixed(uint8_t* __restrict__ frames, uint64_
     __syncthreads();
     // phase 0: validate and classify
     const uint64_t i = f0 + t;
+    int cls = -1;
     if (t < F && i < n) {
         const uint64_t o = off[i];
         const u32 len = lens[i];
@@ -304,8 +466,36 @@ __device__ __forceinline__ void desc_mixed(uint8_t* __restrict__ frames, uint64_
         } else {
             soff[t] = o;
             slen[t] = (uint16_t)len;
-            const int c = len <= (u32)S::T0 ? 0 : (len <= (u32)S::T1 ? 1 : 2);
-            list[c][atomicAdd(&cnt[c], 1)] = (uint16_t)t;
+            cls = len <= (u32)S::T0 ? 0 : (len <= (u32)S::T1 ? 1 : 2);
+            if (!S::ORDERED)
+                list[cls][atomicAdd(&cnt[cls], 1)] = (uint16_t)t;
+        }
+    }
+    if (S::ORDERED) {
+        // per wave and class: ballot, then the lane's rank among its class
+        const int lane = t & 63, w = t >> 6;
+        const uint64_t below = (1ull << lane) - 1;
+        int rank = 0;
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            const uint64_t m = __ballot(cls == c);
+            if (lane == 0)
+                wcnt[c][w] = __popcll(m);
+            if (cls == c)
+                rank = __popcll(m & below);
+        }
+        __syncthreads();
+        if (cls >= 0) {
+            int base = 0;
+            for (int ww = 0; ww < w; ww++)
+                base += wcnt[cls][ww];
+            list[cls][base + rank] = (uint16_t)t;
+        }
+        if (t < 3) {
+            int tot = 0;
+            for (int ww = 0; ww < kBlock / 64; ww++)
+                tot += wcnt[t][ww];
+            cnt[t] = tot;
         }
     }
     __syncthreads();

@@ -176,6 +176,14 @@ static void gpucsum_init_handle(struct mtcp_thread_context *ctx)
 		die("gcs_ctx_create", rc);
 	g->st.device = dev;
 	t_cache = g;
+	/* bursts go to the resident burst grid unless GPUCSUM_BURST_SERVER=0
+	 * (64 x 1500 B: ~9 us per burst instead of ~19 us with a launch each) */
+	env = getenv("GPUCSUM_BURST_SERVER");
+	if (!env || atoi(env) != 0) {
+		rc = gcs_ctx_set_burst_server(g->gcs, 1);
+		if (rc)
+			die("gcs_ctx_set_burst_server", rc);
+	}
 	env = getenv("GPUCSUM_RSS_QUEUES");
 	if (env && atoi(env) > 0) {
 		const char *e40 = getenv("GPUCSUM_RSS_I40E");

@@ -95,6 +95,7 @@ def lib() -> C.CDLL:
             "gcs_compute_copy_dev": (i, [vp, vp, u64, vp, vp, vp, u64, vp, u32, vp, vp, u32,
                                          vp]),
             "gcs_ctx_set_rss": (i, [vp, vp, u32, u32, i]),
+            "gcs_ctx_set_burst_server": (i, [vp, i]),
             "gcs_classify_fixed_dev": (i, [vp, vp, u64, u32, u32, vp, vp, vp, u32, vp]),
             "gcs_classify_dev": (i, [vp, vp, u64, vp, vp, u32, vp, vp, vp, u32, vp]),
             "gcs_rss_dev": (i, [vp, vp, vp, vp, vp, u32, vp, vp, vp]),
@@ -311,6 +312,9 @@ class Context:
                                            _daddr(out), stream), "icmp_checksum")
 
     # -- RSS steering (rss.c) -------------------------------------------------
+    def set_burst_server(self, on: bool = True):
+        check(self.L.gcs_ctx_set_burst_server(self.h, 1 if on else 0), "gcs_ctx_set_burst_server")
+
     def set_rss(self, key: bytes | None = None, num_queues: int = 1, endian_check: int = 0):
         k = None if key is None else np.frombuffer(bytes(key), dtype=np.uint8).copy()
         check(self.L.gcs_ctx_set_rss(self.h, _addr(k), 0 if k is None else k.size, num_queues,

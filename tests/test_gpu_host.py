@@ -112,3 +112,124 @@ def test_frame_larger_than_staging_is_refused_whole(torch_dev):
         ok = np.arange(200)
         st, _ = c.compute_host(buf, off[ok], lens[ok])
         assert set(np.unique(st)) <= {0}
+
+
+# ---------------------------------------------------------------------------
+# burst server (gcs_ctx_set_burst_server): resident grid for direct-mode batches
+
+def bursts(n_bursts, n, seed, jumbo=False):
+    out = []
+    for k in range(n_bursts):
+        lens = synth.imix_lengths(n, seed=seed + k)
+        if jumbo and n > 2:
+            lens[n // 2] = 9000
+        buf, off, lens = synth.packed_frames(lens, seed=seed + 100 + k)
+        out.append((buf, off, lens))
+    return out
+
+
+@pytest.mark.parametrize("idle_us,life_us,gap_s", [(200, 2000, 0.0), (30, 2000, 0.002),
+                                                   (200, 150, 0.0)])
+def test_burst_server_matches_oracle(torch_dev, monkeypatch, idle_us, life_us, gap_s):
+    """Bursts through the resident grid, including grids that leave between
+    bursts (idle exit: gaps longer than GCS_SERVER_IDLE_US) and in the middle
+    of a run (lifetime exit): every burst is exact."""
+    import time
+    monkeypatch.setenv("GCS_SERVER_IDLE_US", str(idle_us))
+    monkeypatch.setenv("GCS_SERVER_LIFE_US", str(life_us))
+    O = Oracle()
+    with gpucsum.Context(0, max_frames=1024, max_bytes=4 << 20) as c:
+        c.set_burst_server(True)
+        for k, (buf, off, lens) in enumerate(bursts(60, 64, 300, jumbo=True)):
+            b1 = buf.copy()
+            st, cs = c.compute_host(b1, off, lens)
+            ref = buf.copy()
+            rst, rcs = O.compute_batch(ref, off, lens)
+            np.testing.assert_array_equal(st, rst)
+            np.testing.assert_array_equal(cs, rcs)
+            np.testing.assert_array_equal(b1, ref)
+            bad = synth.corrupt(ref, off, lens, frac_log2=2, seed=k)
+            v = c.verify_host(ref.copy(), off, lens, flags=1)
+            np.testing.assert_array_equal(v, O.verify_batch(ref.copy(), off, lens, flags=1))
+            assert (v[bad] != 0).all()
+            if gap_s:
+                time.sleep(gap_s)
+
+
+def test_burst_server_yields_to_large_batches(torch_dev):
+    """With the server on, a batch too large for direct mode takes the DMA
+    path (the grid leaves first), and bursts after it are served again."""
+    O = Oracle()
+    big = bursts(1, 60000, 900)[0]
+    with gpucsum.Context(0, max_frames=1 << 16, max_bytes=8 << 20) as c:
+        c.set_burst_server(True)
+        for buf, off, lens in bursts(3, 64, 910) + [big] + bursts(3, 64, 920):
+            v = c.verify_host(buf.copy(), off, lens)
+            np.testing.assert_array_equal(v, O.verify_batch(buf.copy(), off, lens))
+        c.set_burst_server(False)
+        buf, off, lens = bursts(1, 64, 930)[0]
+        v = c.verify_host(buf.copy(), off, lens)
+        np.testing.assert_array_equal(v, O.verify_batch(buf.copy(), off, lens))
+
+
+@pytest.mark.parametrize("server", [False, True])
+def test_registered_rooms_in_place(torch_dev, server):
+    """Frames in one registered region (an mbuf pool) are verified and filled
+    in place over PCIe -- no gather, no scatter -- with the same results; a
+    frame outside the region, or misaligned, sends the batch down the staged
+    path, also exact."""
+    import ctypes as C
+    L = gpucsum.lib()
+    O = Oracle()
+    n = 64
+    rooms = np.zeros(n * 2048 + 8192, dtype=np.uint8)
+    base = (-rooms.ctypes.data) % 4096
+    mb = rooms[base:base + n * 2048]
+    other = np.zeros(4096, dtype=np.uint8)
+    gpucsum.check(L.gcs_host_register(mb.ctypes.data, mb.nbytes))
+    try:
+        with gpucsum.Context(0, max_frames=1024, max_bytes=4 << 20) as c:
+            if server:
+                c.set_burst_server(True)
+            for k in range(6):
+                buf, off, lens = bursts(1, n, 500 + k, jumbo=False)[0]
+                lens = lens.copy()
+                for i in range(n):
+                    mb[i * 2048:i * 2048 + int(lens[i])] = buf[int(off[i]):int(off[i]) + int(lens[i])]
+                addrs = [mb.ctypes.data + i * 2048 for i in range(n)]
+                if k == 4:                      # one frame outside the region
+                    other[:int(lens[3])] = mb[3 * 2048:3 * 2048 + int(lens[3])]
+                    addrs[3] = other.ctypes.data
+                if k == 5:                      # one misaligned frame
+                    mb[9 * 2048 + 2:9 * 2048 + 2 + int(lens[9])] = mb[9 * 2048:9 * 2048 + int(lens[9])].copy()
+                    addrs[9] += 2
+                ptrs = (C.c_void_p * n)(*addrs)
+                frames = [np.ctypeslib.as_array((C.c_uint8 * int(lens[i])).from_address(addrs[i]))
+                          for i in range(n)]
+                ref_frames = [f.copy() for f in frames]
+                st = np.zeros(n, np.uint8)
+                cs = np.zeros(n, np.uint32)
+                gpucsum.check(L.gcs_compute_ptrs(c.h, ptrs, lens.ctypes.data, n, st.ctypes.data,
+                                                 cs.ctypes.data))
+                o64, total = synth.packed_offsets(lens)
+                pk = np.zeros(total + 64, np.uint8)
+                for i in range(n):
+                    pk[int(o64[i]):int(o64[i]) + int(lens[i])] = ref_frames[i]
+                rst, rcs = O.compute_batch(pk, o64, lens)
+                np.testing.assert_array_equal(st, rst)
+                np.testing.assert_array_equal(cs, rcs)
+                for i in range(n):
+                    np.testing.assert_array_equal(frames[i], pk[int(o64[i]):int(o64[i]) + int(lens[i])])
+                # corrupt a few and verify in place (tcp_in.c:1237 side effect on)
+                for i in (1, 17, 40):
+                    frames[i][30] ^= 0x5A
+                    pk[int(o64[i]) + 30] ^= 0x5A
+                v = np.zeros(n, np.uint8)
+                gpucsum.check(L.gcs_verify_ptrs(c.h, ptrs, lens.ctypes.data, n, v.ctypes.data, 1))
+                rv = O.verify_batch(pk, o64, lens, flags=1)
+                np.testing.assert_array_equal(v, rv)
+                for i in range(n):
+                    np.testing.assert_array_equal(frames[i], pk[int(o64[i]):int(o64[i]) + int(lens[i])])
+                assert (v[[1, 17, 40]] != 0).all()
+    finally:
+        gpucsum.check(L.gcs_host_unregister(mb.ctypes.data))

@@ -333,3 +333,32 @@ def test_rx_burst_larger_than_gpu_batch(H, P):  # noqa: F811
     assert st.rx_errors == len(bad) and st.accepted == n - len(bad)
     assert (disp[bad] == MINI_NULL).all()
     assert gst.rx_frames == n and gst.gpu_failures == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("burst", [64, 7])
+def test_decorator_without_burst_server(H, P, monkeypatch, burst):  # noqa: F811
+    """The plugin serves bursts through the resident grid by default (every
+    other plugin test runs that way); with GPUCSUM_BURST_SERVER=0 each burst
+    is one kernel launch.  Dispositions and wire bytes are the same."""
+    from test_plugin import rx_run, tx_run
+    monkeypatch.setenv("GPUCSUM_BURST_SERVER", "0")
+    g = load("frames_rx")
+    buf, off, lens = tx_frames(1500, 77)
+    sw_ctx = C.create_string_buffer(64)
+    sw_disp, sw = rx_run(H, vtab(H, "synth_module_func"), C.addressof(sw_ctx), g["buf"].copy(),
+                         g["off"], g["len"], burst)
+    sw_wire = tx_run(H, vtab(H, "synth_module_func"), C.addressof(sw_ctx), buf, off, lens, burst)
+    d = Decorated(H, P, "synth_module_func", 0)
+    try:
+        hw_disp, hw = rx_run(H, d.iom, d.ctx, g["buf"].copy(), g["off"], g["len"], burst)
+        hw_wire = tx_run(H, d.iom, d.ctx, buf, off, lens, burst)
+        st = d.stats()
+    finally:
+        d.close()
+    err = lambda x: np.isin(x, [MINI_ERROR, MINI_NULL])  # noqa: E731
+    np.testing.assert_array_equal(err(sw_disp), err(hw_disp))
+    assert (sw.rx_errors, sw.accepted, sw.released) == (hw.rx_errors, hw.accepted, hw.released)
+    for a, b in zip(sw_wire, hw_wire):
+        np.testing.assert_array_equal(a, b)
+    assert st.gpu_failures == 0 and st.tx_frames == 1500

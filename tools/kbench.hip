@@ -193,18 +193,16 @@ int imix_main(uint64_t n, int rounds)
                            std::string(TAG).find("no write") != std::string::npos           \
                                ? (u32)GCS_CF_NO_INPLACE : 0u);                              \
     }});
-    // shapes (round 1: <4,1|16,3|32,3> wins; U = 6 / 9 spill at 6 waves, 270 -> 360-780 us)
-    MIXED(false, 6, "6 <4,1|16,3|32,3>", 4, 1, 16, 3, 32, 3)
-
-    MIXED(true, 6, "6 <4,1|16,3|32,3>", 4, 1, 16, 3, 32, 3)
-    MIXED(true, 5, "5 <4,1|16,3|32,3>", 4, 1, 16, 3, 32, 3)
-    MIXED(true, 8, "8 <4,1|16,3|32,3>", 4, 1, 16, 3, 32, 3)
-    // TX write-back modes
-    MIXED(true, 6, "6 <4,1|16,3|32,3> 16B chunks sc1", 4, 1, 16, 3, 32, 3, WM_CHUNK_SC1)
-    MIXED(true, 6, "6 <4,1|16,3|32,3> 2B stores", 4, 1, 16, 3, 32, 3, WM_HALFWORD)
-    MIXED(true, 6, "6 <4,1|16,3|32,3> 64B sector plain", 4, 1, 16, 3, 32, 3, WM_SECTOR)
-    MIXED(true, 6, "6 <4,1|16,3|32,3> 128B line sc1", 4, 1, 16, 3, 32, 3, WM_LINE_SC1)
-    MIXED(true, 6, "6 <4,1|16,3|32,3> no write-back", 4, 1, 16, 3, 32, 3)
+    // round 2: class lists in frame order (ballot) vs atomicAdd arrival order
+    MIXED(false, 6, "6 ordered", 4, 1, 16, 3, 32, 3, kWM, 256, true)
+    MIXED(false, 6, "6 atomic", 4, 1, 16, 3, 32, 3, kWM, 256, false)
+    MIXED(true, 6, "6 ordered", 4, 1, 16, 3, 32, 3, kWM, 256, true)
+    MIXED(true, 6, "6 atomic", 4, 1, 16, 3, 32, 3, kWM, 256, false)
+    MIXED(true, 6, "6 ordered 64B sector plain", 4, 1, 16, 3, 32, 3, WM_SECTOR, 256, true)
+    MIXED(true, 6, "6 ordered 128B line sc1", 4, 1, 16, 3, 32, 3, WM_LINE_SC1, 256, true)
+    MIXED(true, 6, "6 ordered 16B chunks sc1", 4, 1, 16, 3, 32, 3, WM_CHUNK_SC1, 256, true)
+    MIXED(true, 6, "6 ordered no write-back", 4, 1, 16, 3, 32, 3, kWM, 256, true)
+    MIXED(true, 6, "6 ordered F=128", 4, 1, 16, 3, 32, 3, kWM, 128, true)
     vs.push_back({"verify  desc (launch_verify_desc)", vb, [&](hipStream_t st) {
         CK(launch_verify_desc(rx, total, doff, dlen, (u32)n, v1, 0u, st));
     }});
