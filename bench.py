@@ -210,8 +210,19 @@ def cpu_baseline(tx, rx, stride, frame_len, budget_s, sample, torch):
     from oracle_lib import Oracle, RefHarness
 
     m = min(sample, tx.numel() // stride)
-    tx_h = tx[: m * stride].cpu().numpy().copy()
-    rx_h = rx[: m * stride].cpu().numpy().copy()
+    cpus, usable, quota = host_cpus()
+    one = [cpus[0]]
+    allc = cpus[:usable]            # spread over cores and L3 domains (host_cpus)
+    # The sample is first touched by this thread pinned to the 1-core CPU, so
+    # its pages sit on that CPU's memory node, as under `taskset -c <cpu>`
+    # (BASELINE.md); the affinity is restored afterwards.
+    keep = os.sched_getaffinity(0)
+    os.sched_setaffinity(0, set(one))
+    try:
+        tx_h = tx[: m * stride].cpu().numpy().copy()
+        rx_h = rx[: m * stride].cpu().numpy().copy()
+    finally:
+        os.sched_setaffinity(0, keep)
     kind = "reference" if RefHarness.available() else "port"
     if kind == "reference":
         R = RefHarness()
@@ -225,10 +236,6 @@ def cpu_baseline(tx, rx, stride, frame_len, budget_s, sample, torch):
             if compute:
                 return O.compute_fixed(buf, stride, frame_len, m, threads=len(pin), want=False)
             return O.verify_fixed(buf, stride, frame_len, m, threads=len(pin))
-
-    cpus, usable, quota = host_cpus()
-    one = [cpus[0]]
-    allc = cpus[:usable]            # spread over cores and L3 domains (host_cpus)
 
     def measure(pin, budget):
         rates = []

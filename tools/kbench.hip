@@ -455,6 +455,59 @@ __global__ void k_seq_off(uint64_t* off, uint64_t* soff, uint16_t* lens, uint64_
     lens[i] = (uint16_t)L;
 }
 
+// Copy ceilings for k_copy_fill's data movement: a 32-lane group moves one
+// 1500 B frame (94 chunks, 3 per lane), writing dst + i*1536 aligned, reading
+// src + i*sstride (+ shift): sstride 1434 / shift 0 = the payload layout
+// (unaligned 16 B loads), sstride 1536 = aligned.  No fold, no headers.
+template <bool NTS, int G = 32, int U = 3>
+__global__ void __launch_bounds__(256) k_copy_frames(uint8_t* __restrict__ dst,
+                                                     const uint8_t* __restrict__ src,
+                                                     uint64_t sstride, u32 n)
+{
+    const int sub = threadIdx.x & (G - 1);
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);
+    const uint64_t i = (uint64_t)blk * (256 / G) + threadIdx.x / G;
+    if (i >= n) return;
+    const uint8_t* s = src + i * sstride;
+    uint8_t* d = dst + i * 1536;
+    u32x4 v[U];
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+        const int c = j * G + sub;
+        v[j] = c < 94 ? *reinterpret_cast<const u32x4_u*>(s + 16 * c) : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+        const int c = j * G + sub;
+        if (c < 94) {
+            if (NTS)
+                __builtin_nontemporal_store(v[j], reinterpret_cast<u32x4*>(d + 16 * c));
+            else
+                *reinterpret_cast<u32x4*>(d + 16 * c) = v[j];
+        }
+    }
+}
+
+// Plain float4-style streaming copy of a contiguous buffer (the guide's copy
+// ceiling pattern): each thread moves U chunks, one-shot grid.
+template <int U>
+__global__ void __launch_bounds__(256) k_copy_flat(u32x4* __restrict__ dst,
+                                                   const u32x4* __restrict__ src, uint64_t n16)
+{
+    const uint64_t base = ((uint64_t)xcd_block(blockIdx.x, gridDim.x) * U) * 256 + threadIdx.x;
+    u32x4 v[U];
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+        const uint64_t k = base + (uint64_t)j * 256;
+        v[j] = k < n16 ? __builtin_nontemporal_load(src + k) : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+        const uint64_t k = base + (uint64_t)j * 256;
+        if (k < n16) dst[k] = v[j];
+    }
+}
+
 int copy_main(uint64_t n, int rounds)
 {
     const uint32_t L = 1500, hl = 66, plen = L - hl;
@@ -484,6 +537,51 @@ int copy_main(uint64_t n, int rounds)
     vs.push_back({"fused copy + fill (launch_copy_fill)", bytes, [&](hipStream_t st_) {
         CK(launch_copy_fill(tx, n * stride, off, lens, src, n * plen + 64, soff, (u32)n, st,
                             nullptr, 0u, st_));
+    }});
+    uint8_t *asrc, *cdst;                     // copy ceilings write cdst, never tx
+    CK(hipMalloc(&asrc, n * stride));
+    CK(hipMalloc(&cdst, n * stride));
+    CK(hipMemcpyAsync(asrc, tx, n * stride, hipMemcpyDeviceToDevice, s));
+    const double cpb = (double)n * 1504 * 2;   // 94 chunks read + written per frame
+    vs.push_back({"  copy frames, src stride 1434 (unaligned)", cpb, [&](hipStream_t st_) {
+        hipLaunchKernelGGL((k_copy_frames<false>), dim3((n + 7) / 8), dim3(256), 0, st_, cdst, src,
+                           (uint64_t)plen, (u32)n);
+    }});
+    vs.push_back({"  copy frames G=64 U=2, src stride 1434", cpb, [&](hipStream_t st_) {
+        hipLaunchKernelGGL((k_copy_frames<false, 64, 2>), dim3((n + 3) / 4), dim3(256), 0, st_,
+                           cdst, src, (uint64_t)plen, (u32)n);
+    }});
+    vs.push_back({"  copy frames G=128 U=1 (2 waves/frame), 1434", cpb, [&](hipStream_t st_) {
+        hipLaunchKernelGGL((k_copy_frames<false, 128, 1>), dim3((n + 1) / 2), dim3(256), 0, st_,
+                           cdst, src, (uint64_t)plen, (u32)n);
+    }});
+    vs.push_back({"fused copy + fill <64,2>", bytes, [&](hipStream_t st_) {
+        hipLaunchKernelGGL((k_copy_fill<64, 2, 1>), dim3((n + 3) / 4), dim3(256), 0, st_, tx,
+                           n * stride, off, lens, src, n * plen + 64, soff, (u32)n, st, nullptr, 0u);
+    }});
+    vs.push_back({"fused copy + fill <64,2> occ 8", bytes, [&](hipStream_t st_) {
+        hipLaunchKernelGGL((k_copy_fill<64, 2, 8>), dim3((n + 3) / 4), dim3(256), 0, st_, tx,
+                           n * stride, off, lens, src, n * plen + 64, soff, (u32)n, st, nullptr, 0u);
+    }});
+    vs.push_back({"  copy frames, src stride 1536 (aligned)", cpb, [&](hipStream_t st_) {
+        hipLaunchKernelGGL((k_copy_frames<false>), dim3((n + 7) / 8), dim3(256), 0, st_, cdst, asrc,
+                           stride, (u32)n);
+    }});
+    vs.push_back({"  copy frames, aligned, NT stores", cpb, [&](hipStream_t st_) {
+        hipLaunchKernelGGL((k_copy_frames<true>), dim3((n + 7) / 8), dim3(256), 0, st_, cdst, asrc,
+                           stride, (u32)n);
+    }});
+#define CFLAT(U_)                                                                             \
+    vs.push_back({"  flat copy U=" #U_ " (whole 1.61 GB buffer)", (double)n * stride * 2,    \
+                  [&](hipStream_t st_) {                                                      \
+        const uint64_t n16 = n * stride / 16;                                                 \
+        hipLaunchKernelGGL((k_copy_flat<U_>), dim3((n16 + 256 * U_ - 1) / (256 * U_)),         \
+                           dim3(256), 0, st_, (u32x4*)cdst, (const u32x4*)asrc, n16);          \
+    }});
+    CFLAT(1) CFLAT(4) CFLAT(8)
+    vs.push_back({"  hipMemcpyAsync D2D (whole 1.61 GB buffer)", (double)n * stride * 2,
+                  [&](hipStream_t st_) {
+        CK(hipMemcpyAsync(cdst, asrc, n * stride, hipMemcpyDeviceToDevice, st_));
     }});
 #define CFO(O_)                                                                              \
     vs.push_back({"fused copy + fill, occupancy " #O_, bytes, [&](hipStream_t st_) {          \
