@@ -382,12 +382,19 @@ hipError_t launch_burst_server(ServerMailbox* mb, uint32_t done_seq, uint64_t id
 // work on neighbouring frames: a wave's 64 B-class loads and sector stores
 // then cover runs of adjacent frames (two frames per 128 B line) instead of
 // frames scattered over the block's whole range.
+// K0 / K1: frames per group per list iteration for classes 0 / 1, all their
+// loads issued before the first is folded (as k_fixed<4,1,K> does).  Measured
+// on C3 (K0 = 3, K1 = 2): verify 278 vs 280 us, fill 388 vs 390 us -- the
+// list passes' memory waits are not what bounds it -- so the shipped shape
+// keeps K = 1 (profiles/r02/kbench_imix_K.log; other class shapes:
+// kbench_imix_shapes2.log).
 template <int G0_, int U0_, int G1_, int U1_, int G2_, int U2_, int WM_ = kWM, int F_ = kBlock,
-          bool ORDERED_ = true>
+          bool ORDERED_ = true, int K0_ = 1, int K1_ = 1>
 struct DescShape {
     static constexpr int G0 = G0_, U0 = U0_, G1 = G1_, U1 = U1_, G2 = G2_, U2 = U2_, WM = WM_;
     static constexpr int F = F_;
     static constexpr bool ORDERED = ORDERED_;
+    static constexpr int K0 = K0_, K1 = K1_;
     static_assert(F <= kBlock, "one descriptor per thread");
     static constexpr int T0 = 16 * G0 * U0, T1 = 16 * G1 * U1;
 };
@@ -396,31 +403,45 @@ struct DescShape {
 template <bool COMPUTE>
 using DescShip = DescShape<4, 1, 16, 3, 32, 3>;
 
-template <int G, int U, bool COMPUTE, bool LOOP, bool EXT, int WM>
+template <int G, int U, bool COMPUTE, bool LOOP, bool EXT, int WM, int K = 1>
 __device__ __forceinline__ void desc_class(uint8_t* __restrict__ frames, uint64_t frames_bytes,
                                            const uint64_t* soff, const uint16_t* slen,
                                            const uint16_t* list, int count, u32 flags,
                                            uint8_t* codes, uint32_t* csums, const Ext& ext,
                                            uint32_t* hashes, uint16_t* queues)
 {
+    static_assert(K == 1 || !LOOP, "K > 1 is for frames that fit one batch");
     constexpr int GPB = kBlock / G;                    // groups per block
     const int g = threadIdx.x / G, sub = threadIdx.x & (G - 1);
-    for (int base = 0; base < count; base += GPB) {    // block-uniform trip count
-        const int k = base + g;
-        const bool active = k < count;
-        const int t = active ? list[k] : list[0];      // list[0] exists: count > 0
-        const uint64_t o = soff[t];                    // LDS: no dependent global load
-        const u32 len = slen[t];
-        uint8_t* f = frames + o;                       // descriptor validated in phase 0
-        const XFrame xf =
-            EXT ? XFrame{{ext.key[0], ext.key[1], ext.key[2], ext.key[3]},
-                         hashes ? hashes + t : nullptr, queues ? queues + t : nullptr, ext.nq,
-                         ext.nq_magic, ext.endian, nullptr}
-                : XFrame{};
-        do_frame<G, U, COMPUTE, LOOP, true, kNT, WM, EXT>(f, len, (int64_t)(frames_bytes - o),
-                                                           true, sub, flags, codes + t,
-                                                           COMPUTE ? csums + t : nullptr, active,
-                                                           xf);
+    auto xframe_of = [&](int t) {
+        return EXT ? XFrame{{ext.key[0], ext.key[1], ext.key[2], ext.key[3]},
+                            hashes ? hashes + t : nullptr, queues ? queues + t : nullptr, ext.nq,
+                            ext.nq_magic, ext.endian, nullptr}
+                   : XFrame{};
+    };
+    for (int base = 0; base < count; base += GPB * K) {   // block-uniform trip count
+        uint4 v[K][U];
+        int tk[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const int idx = base + k * GPB + g;
+            const bool active = idx < count;
+            const int t = active ? list[idx] : list[0];  // list[0] exists: count > 0
+            tk[k] = active ? t : -1;
+            const uint64_t o = soff[t];                  // LDS: no dependent global load
+            const int nch = active ? (int)((slen[t] + 15u) >> 4) : 0;
+            load_first<G, U, true, kNT>(frames + o, nch, (int64_t)(frames_bytes - o), sub, v[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const bool active = tk[k] >= 0;
+            const int t = active ? tk[k] : list[0];
+            const uint64_t o = soff[t];                  // descriptor validated in phase 0
+            uint8_t* f = frames + o;
+            frame_body<G, U, COMPUTE, LOOP, true, kNT, WM, EXT>(
+                v[k], f, f, slen[t], (int64_t)(frames_bytes - o), true, sub, flags, codes + t,
+                COMPUTE ? csums + t : nullptr, active, xframe_of(t));
+        }
     }
 }
 
@@ -502,8 +523,8 @@ __device__ __forceinline__ void desc_mixed(uint8_t* __restrict__ frames, uint64_
     const int n0 = cnt[0], n1 = cnt[1], n2 = cnt[2];
     uint32_t* hl = EXT && !COMPUTE ? hashes : nullptr;
     uint16_t* ql = EXT && !COMPUTE ? queues : nullptr;
-    if (n0) desc_class<S::G0, S::U0, COMPUTE, false, EXT, S::WM>(frames, frames_bytes, soff, slen, list[0], n0, flags, codes, csums, ext, hl, ql);
-    if (n1) desc_class<S::G1, S::U1, COMPUTE, false, EXT, S::WM>(frames, frames_bytes, soff, slen, list[1], n1, flags, codes, csums, ext, hl, ql);
+    if (n0) desc_class<S::G0, S::U0, COMPUTE, false, EXT, S::WM, S::K0>(frames, frames_bytes, soff, slen, list[0], n0, flags, codes, csums, ext, hl, ql);
+    if (n1) desc_class<S::G1, S::U1, COMPUTE, false, EXT, S::WM, S::K1>(frames, frames_bytes, soff, slen, list[1], n1, flags, codes, csums, ext, hl, ql);
     if (n2) desc_class<S::G2, S::U2, COMPUTE, true, EXT, S::WM>(frames, frames_bytes, soff, slen, list[2], n2, flags, codes, csums, ext, hl, ql);
     __syncthreads();
     if (t < F && i < n) {

@@ -193,16 +193,18 @@ int imix_main(uint64_t n, int rounds)
                            std::string(TAG).find("no write") != std::string::npos           \
                                ? (u32)GCS_CF_NO_INPLACE : 0u);                              \
     }});
-    // round 2: class lists in frame order (ballot) vs atomicAdd arrival order
-    MIXED(false, 6, "6 ordered", 4, 1, 16, 3, 32, 3, kWM, 256, true)
-    MIXED(false, 6, "6 atomic", 4, 1, 16, 3, 32, 3, kWM, 256, false)
-    MIXED(true, 6, "6 ordered", 4, 1, 16, 3, 32, 3, kWM, 256, true)
-    MIXED(true, 6, "6 atomic", 4, 1, 16, 3, 32, 3, kWM, 256, false)
-    MIXED(true, 6, "6 ordered 64B sector plain", 4, 1, 16, 3, 32, 3, WM_SECTOR, 256, true)
-    MIXED(true, 6, "6 ordered 128B line sc1", 4, 1, 16, 3, 32, 3, WM_LINE_SC1, 256, true)
-    MIXED(true, 6, "6 ordered 16B chunks sc1", 4, 1, 16, 3, 32, 3, WM_CHUNK_SC1, 256, true)
-    MIXED(true, 6, "6 ordered no write-back", 4, 1, 16, 3, 32, 3, kWM, 256, true)
-    MIXED(true, 6, "6 ordered F=128", 4, 1, 16, 3, 32, 3, kWM, 128, true)
+    // round 2: class-1 / class-2 group shapes (fewer lanes per frame = fewer
+    // per-frame epilogues per wave instruction)
+    MIXED(false, 6, "6 <4,1|16,3|32,3>", 4, 1, 16, 3, 32, 3)
+    MIXED(false, 6, "6 <4,1|8,5|32,3>", 4, 1, 8, 5, 32, 3)
+    MIXED(false, 5, "5 <4,1|8,5|32,3>", 4, 1, 8, 5, 32, 3)
+    MIXED(false, 6, "6 <4,1|8,5|16,6>", 4, 1, 8, 5, 16, 6)
+    MIXED(false, 5, "5 <4,1|8,5|16,6>", 4, 1, 8, 5, 16, 6)
+    MIXED(false, 4, "4 <4,1|8,5|16,6>", 4, 1, 8, 5, 16, 6)
+    MIXED(false, 6, "6 <4,1|16,3|16,6>", 4, 1, 16, 3, 16, 6)
+    MIXED(true, 6, "6 <4,1|16,3|32,3>", 4, 1, 16, 3, 32, 3)
+    MIXED(true, 6, "6 <4,1|8,5|32,3>", 4, 1, 8, 5, 32, 3)
+    MIXED(true, 5, "5 <4,1|8,5|16,6>", 4, 1, 8, 5, 16, 6)
     vs.push_back({"verify  desc (launch_verify_desc)", vb, [&](hipStream_t st) {
         CK(launch_verify_desc(rx, total, doff, dlen, (u32)n, v1, 0u, st));
     }});
