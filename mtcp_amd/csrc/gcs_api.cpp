@@ -276,8 +276,12 @@ class BurstServer {
     // `frames` (bytes, a multiple of 16), frame i at off[i], len[i] bytes.
     // Returns when every block has acknowledged it, with the verdicts /
     // statuses in code[] and, for a fill, the checks in csum[].
+    // in_place: the kernel writes the frames themselves (host memory), so the
+    // call also waits for every block's release + ack; otherwise the tagged
+    // result records alone complete it.
     int serve(uint8_t* frames, uint64_t bytes, const uint64_t* off, const uint16_t* len,
-              uint32_t n, bool compute, uint32_t flags, uint8_t* code, uint32_t* csum)
+              uint32_t n, bool compute, uint32_t flags, uint8_t* code, uint32_t* csum,
+              bool in_place = false)
     {
         if (launched_ && any_exited()) {
             int rc = wait_exit();
@@ -288,7 +292,9 @@ class BurstServer {
             if (rc) return rc;
         }
         const uint32_t q = ++seq_;
+        const uint64_t tag = (uint64_t)(q & 0xFFFFu) << 48;
         const auto tw = std::chrono::steady_clock::now();
+        std::memset(mb_->rec, 0, n * sizeof(uint64_t));   // no record of an older request
         // each 16 B line: its fields, then its seq (x86 keeps the order)
         for (uint32_t i = 0; i < n; i++) {
             gcs::ServerDesc& d = mb_->desc[i];
@@ -303,12 +309,17 @@ class BurstServer {
         mb_->a.mode = (compute ? 1u : 0u) | (flags << 1);
         const auto t0 = std::chrono::steady_clock::now();
         __atomic_store_n(&mb_->a.seq, q, __ATOMIC_RELEASE);
+        uint32_t have = 0;                   // records [0, have) carry q
         for (;;) {
-            bool all = true, gone = false;
+            while (have < n &&
+                   (__atomic_load_n(&mb_->rec[have], __ATOMIC_ACQUIRE) >> 48) == (tag >> 48))
+                have++;
+            bool all = have == n, gone = false;
             for (int b = 0; b < gcs::kServerBlocks; b++) {
                 if (__atomic_load_n(&mb_->ack[b].v, __ATOMIC_ACQUIRE) == q)
                     continue;
-                all = false;
+                if (in_place)
+                    all = false;
                 if (__atomic_load_n(&mb_->state[b].v, __ATOMIC_ACQUIRE) == 2)
                     gone = true;
             }
@@ -329,10 +340,11 @@ class BurstServer {
             }
             __builtin_ia32_pause();
         }
-        if (code)
-            std::memcpy(code, mb_->code, n);
-        if (compute && csum)
-            std::memcpy(csum, mb_->csum, n * sizeof(uint32_t));
+        for (uint32_t i = 0; i < n; i++) {
+            const uint64_t r = mb_->rec[i];
+            if (code) code[i] = (uint8_t)(r >> 32);
+            if (compute && csum) csum[i] = (uint32_t)r;
+        }
         if (prof_) {
             // GCS_SERVER_PROF: per request, the slowest block's serve and
             // release times (wall clock), averaged and printed at exit
@@ -727,7 +739,8 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
             }
             if (ctx->server && n <= (uint32_t)gcs::kServerMaxFrames) {
                 int rc = ctx->server->serve(reg.dev, reg.bytes & ~15ull, s.h_off, s.h_len, n,
-                                            compute, 0u, s.h_code, compute ? s.h_csum : nullptr);
+                                            compute, 0u, s.h_code, compute ? s.h_csum : nullptr,
+                                            /*in_place=*/compute);
                 if (rc) return rc;
             } else {
                 if (compute)

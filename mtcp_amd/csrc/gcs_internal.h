@@ -26,8 +26,9 @@ struct Ext {
 // first frames.  Each 16 B line is read in one piece, and every line carries
 // the request number, so a poll that sees seq q in all the lines it needs
 // has a consistent request (the host writes each line's fields before its
-// seq, and the lines before line A's seq).  Results go to fixed arrays of the
-// mailbox; each block then writes ack[b] = q (release).
+// seq, and the lines before line A's seq).  Results go to tagged per-frame
+// records in the mailbox; each block then releases and writes ack[b] = q
+// (what the host waits for when the frames themselves were written in place).
 constexpr int kServerBlocks = 8;
 constexpr int kServerMaxFrames = 4096;
 struct alignas(16) ServerReqA {
@@ -60,8 +61,11 @@ struct ServerMailbox {
     uint64_t prof[kServerBlocks][8];     // device, GCS_SERVER_PROF: wall-clock marks of
                                          // the last request (seen, served, released)
     ServerDesc desc[kServerMaxFrames];   // host
-    uint8_t code[kServerMaxFrames];      // device: verdicts / TX statuses
-    uint32_t csum[kServerMaxFrames];     // device: TX checks (ip | tcp << 16)
+    // device: one record per frame, written in ONE 8 B store once the frame
+    // is done: csum (ip | tcp << 16) | code << 32 | (seq & 0xFFFF) << 48.  The
+    // host sees a request's results complete when every record carries its
+    // seq -- without waiting for the blocks' release fence and ack.
+    uint64_t rec[kServerMaxFrames];
 };
 
 hipError_t launch_burst_server(ServerMailbox* mb, uint32_t done_seq, uint64_t idle_ticks,

@@ -232,6 +232,8 @@ k_burst_server(ServerMailbox* mb, uint32_t done_seq, uint64_t idle_ticks, uint64
     // kPollWaves = 2: a second wave polls half a round trip behind the first
     __shared__ uint4 s_line[2 + FPB];
     __shared__ uint32_t s_claim;             // IDLE until a polling wave claims WORK / EXIT
+    __shared__ uint8_t s_code[FPB];          // a frame's results, packed into its record
+    __shared__ uint32_t s_csum[FPB];
     const int t = threadIdx.x, sub = t & (G - 1), grp = t / G;
     const int wave = t >> 6, lane = t & 63;
     uint32_t last = done_seq, polls = 0;
@@ -312,19 +314,25 @@ k_burst_server(ServerMailbox* mb, uint32_t done_seq, uint64_t idle_ticks, uint64
             const bool ok = (o & 15) == 0 && o <= bytes && len <= bytes - o;
             uint8_t* f = frames + (ok ? o : 0);
             const int64_t avail = ok ? (int64_t)(bytes - o) : 0;
+            s_csum[grp] = 0;
             if (compute)
                 do_frame<G, U, true, true, true, kNT, kWM>(f, len, avail, ok, sub, flags,
-                                                           mb->code + i, mb->csum + i);
+                                                           s_code + grp, s_csum + grp);
             else
                 do_frame<G, U, false, true, true, kNT, kWM>(f, len, avail, ok, sub, flags,
-                                                            mb->code + i, nullptr);
+                                                            s_code + grp, nullptr);
+            if (sub == 0) {                  // the group's results, in one 8 B store
+                const uint64_t r = (uint64_t)s_csum[grp] | ((uint64_t)s_code[grp] << 32) |
+                                   ((uint64_t)(q & 0xFFFFu) << 48);
+                __hip_atomic_store(&mb->rec[i], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
         }
         uint64_t t_served = 0;
         if (PROF) {
             __syncthreads();
             t_served = __builtin_amdgcn_s_memrealtime();
         }
-        __threadfence_system();              // this wave's results reach host memory
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // this wave's results reach host memory
         __syncthreads();                     // every wave done with s_line / s_claim
         if (t == 0) {
             if (PROF) {
