@@ -536,6 +536,20 @@ def plugin_bursts(gcs, reps=300):
     return out
 
 
+def plugin_threads():
+    """Bursts from several mTCP-like threads per GPU (tools/mt_probe.py), in a
+    child process with GPU_MAX_HW_QUEUES=16 as the plugin's load_module sets
+    it (this process's HIP runtime already runs with the default 4)."""
+    import subprocess
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="16")
+    try:
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "mt_probe.py")], env=env,
+                           capture_output=True, text=True, timeout=180)
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    except Exception as e:   # a side measurement: report, never fail the bench line
+        return {"error": repr(e)[:200]}
+
+
 def main():
     args = parse()
     import torch
@@ -639,6 +653,7 @@ def main():
             torch.cuda.empty_cache()
             line["pcie_inclusive"] = pcie_inclusive(gpucsum, torch)
             line["plugin_bursts"] = plugin_bursts(gpucsum)
+            line["plugin_threads"] = plugin_threads()
     ctx.close()
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -65,6 +65,9 @@
  * Burst server: each thread's context serves its bursts through a resident
  * grid polling a pinned mailbox (gcs_ctx_set_burst_server) unless the
  * environment sets GPUCSUM_BURST_SERVER=0 (then: one kernel launch per burst).
+ * load_module sets GPU_MAX_HW_QUEUES=16 unless the environment already sets
+ * it, before the process's first HIP call, so that every thread's grid has a
+ * hardware queue of its own (mTCP runs cores / n_gpus threads per GPU).
  * Threading (core.c:1153-1245): load_module once on the main thread; every
  * other call from the owning mTCP thread.  Per-thread state is keyed by the
  * mtcp_thread_context pointer; mTCP thread k uses GPU k mod n_gpus (override:

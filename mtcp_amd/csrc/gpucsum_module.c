@@ -136,6 +136,12 @@ static void gpucsum_load_module(void)
 		fprintf(stderr, "[gpucsum] no inner I/O module: call gpucsum_set_inner() first\n");
 		exit(EXIT_FAILURE);
 	}
+	/* Before the process's first HIP call: one hardware queue per burst grid.
+	 * mTCP puts cores / n_gpus threads on each GPU, each context with its own
+	 * resident grid; with HIP's default 4 queues, grids beyond the fourth wait
+	 * behind others (8 threads per GPU: 32.7 us per burst with 4 queues,
+	 * 11.6 us with 16; tests/test_gpu_mt.py).  An explicit setting wins. */
+	setenv("GPU_MAX_HW_QUEUES", "16", 0);
 	rc = gcs_device_count(&n);
 	if (rc || n <= 0)
 		die("gcs_device_count (no MI355X visible)", rc ? rc : GCS_ENODEV);

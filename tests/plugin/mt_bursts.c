@@ -1,0 +1,151 @@
+/*
+ * mt_bursts.c -- several mTCP-like threads, each with its own context on the
+ * SAME GPU, pushing 64-frame bursts through the host entry points at once
+ * (TEST ONLY).  mTCP runs one thread per core and maps thread k to GPU
+ * k mod n (gpucsum_module.c), so with 64 cores and 8 GPUs eight contexts --
+ * and with the burst server eight resident grids -- share one device and its
+ * GPU_MAX_HW_QUEUES hardware queues.  Every burst is checked against the
+ * oracle (oracle/csum_ref.c) on the thread that made it.
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "../../include/mtcp_gpucsum.h"
+#include "../../oracle/csum_ref.h"
+
+#define ROOM 2048
+#define BURST 64
+
+struct job {
+	int id, iters, server;
+	uint64_t mismatches, frames;
+	int rc;
+	double us;
+};
+
+static uint32_t xorshift(uint64_t *s)
+{
+	*s ^= *s << 13;
+	*s ^= *s >> 7;
+	*s ^= *s << 17;
+	return (uint32_t)*s;
+}
+
+/* An mTCP-shaped TCP frame of len bytes (IMIX length), checks zero. */
+static void make_frame(uint8_t *f, uint32_t len, uint64_t *rng)
+{
+	uint32_t k, tot = len - 14;
+	for (k = 0; k < len; k++)
+		f[k] = (uint8_t)xorshift(rng);
+	f[12] = 0x08; f[13] = 0x00; f[14] = 0x45; f[15] = 0;
+	f[16] = (uint8_t)(tot >> 8); f[17] = (uint8_t)tot;
+	f[20] = 0x40; f[21] = 0; f[22] = 64; f[23] = 6; f[24] = f[25] = 0;
+	f[46] = (uint8_t)((len < 66 ? 5 : 8) << 4); f[47] = 0x10;
+	f[50] = f[51] = 0;
+	if (len >= 66) { f[54] = 1; f[55] = 1; f[56] = 8; f[57] = 10; }
+}
+
+static double now_us(void)
+{
+	struct timespec t;
+	clock_gettime(CLOCK_MONOTONIC, &t);
+	return t.tv_sec * 1e6 + t.tv_nsec * 1e-3;
+}
+
+static void *run(void *arg)
+{
+	struct job *j = arg;
+	uint8_t *rooms = malloc((size_t)BURST * ROOM), *ref = malloc((size_t)BURST * ROOM);
+	uint8_t *ptrs[BURST], st[BURST], vd[BURST];
+	uint16_t len[BURST];
+	uint32_t cs[BURST];
+	uint64_t rng = 0x9E3779B97F4A7C15ull ^ (uint64_t)(j->id + 1) * 0x100000001B3ull;
+	gcs_ctx *ctx = NULL;
+	double in_calls = 0;
+	int it, i;
+
+	j->rc = gcs_ctx_create(&ctx, 0, 4096, 8u << 20);
+	if (!j->rc && j->server)
+		j->rc = gcs_ctx_set_burst_server(ctx, 1);
+	for (it = 0; it < j->iters && !j->rc; it++) {
+		double t0, t1;
+		for (i = 0; i < BURST; i++) {
+			uint32_t u = xorshift(&rng) % 12;
+			len[i] = (uint16_t)(u < 7 ? 64 : u < 11 ? 576 : 1500);
+			ptrs[i] = rooms + (size_t)i * ROOM;
+			make_frame(ptrs[i], len[i], &rng);
+			memcpy(ref + (size_t)i * ROOM, ptrs[i], len[i]);
+		}
+		t0 = now_us();
+		j->rc = gcs_compute_ptrs(ctx, ptrs, len, BURST, st, cs);
+		in_calls += now_us() - t0;
+		if (j->rc)
+			break;
+		for (i = 0; i < BURST; i++) {
+			uint32_t rc2 = 0;
+			uint8_t *r = ref + (size_t)i * ROOM;
+			int rs = ref_tx_fill(r, len[i], &rc2);
+			if (rs != st[i] || rc2 != cs[i] || memcmp(r, ptrs[i], len[i]))
+				j->mismatches++;
+			if (xorshift(&rng) % 8 == 0) {         /* corrupt one byte */
+				uint32_t p = 14 + xorshift(&rng) % (len[i] - 14);
+				uint8_t x = (uint8_t)(1 + xorshift(&rng) % 255);
+				ptrs[i][p] ^= x;
+				r[p] ^= x;
+			}
+		}
+		t1 = now_us();
+		j->rc = gcs_verify_ptrs(ctx, ptrs, len, BURST, vd, GCS_VF_ZERO_BAD_TCP_CHECK);
+		in_calls += now_us() - t1;
+		if (j->rc)
+			break;
+		for (i = 0; i < BURST; i++) {
+			uint8_t *r = ref + (size_t)i * ROOM;
+			int v = ref_rx_verdict(r, len[i], GCS_VF_ZERO_BAD_TCP_CHECK);
+			if (v != vd[i] || memcmp(r, ptrs[i], len[i]))
+				j->mismatches++;
+		}
+		j->frames += 2 * BURST;
+	}
+	j->us = in_calls / (2.0 * (it ? it : 1));     /* inside the gcs calls only */
+	if (ctx)
+		gcs_ctx_destroy(ctx);
+	free(rooms);
+	free(ref);
+	return NULL;
+}
+
+/* threads x iters bursts (fill, then verify, per iteration).  Returns the
+ * first non-zero status; mismatches / frames / mean us per call summed or
+ * averaged over the threads. */
+int mt_bursts(int threads, int iters, int server, uint64_t *mismatches, uint64_t *frames,
+              double *us_per_call)
+{
+	pthread_t tid[64];
+	struct job jobs[64];
+	int t, rc = 0;
+
+	if (threads < 1 || threads > 64)
+		return GCS_EINVAL;
+	for (t = 0; t < threads; t++) {
+		memset(&jobs[t], 0, sizeof(jobs[t]));
+		jobs[t].id = t;
+		jobs[t].iters = iters;
+		jobs[t].server = server;
+		pthread_create(&tid[t], NULL, run, &jobs[t]);
+	}
+	*mismatches = *frames = 0;
+	*us_per_call = 0;
+	for (t = 0; t < threads; t++) {
+		pthread_join(tid[t], NULL);
+		if (jobs[t].rc && !rc)
+			rc = jobs[t].rc;
+		*mismatches += jobs[t].mismatches;
+		*frames += jobs[t].frames;
+		*us_per_call += jobs[t].us / threads;
+	}
+	return rc;
+}

@@ -1,0 +1,27 @@
+"""Burst latency with several mTCP-like threads per GPU (tests/plugin/mt_bursts.c),
+as the plugin runs them (GPU_MAX_HW_QUEUES=16 when run through bench.py).
+Prints one JSON object (tools/, not product)."""
+import ctypes as C
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from mtcp_amd import gpucsum  # noqa: E402
+
+gpucsum.lib()
+M = C.CDLL(os.path.join(ROOT, "tests", "plugin", "libmt_bursts.so"))
+M.mt_bursts.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint64),
+                        C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
+out = {"workload": "threads each with its own context on GPU 0, 64-frame IMIX bursts "
+                   "(fill + verify), every frame checked against the oracle; mean us per call "
+                   "inside the gcs calls",
+       "GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES", "default (4)")}
+for threads in (1, 4, 8, 12):
+    for server in (1, 0):
+        mis, fr, us = C.c_uint64(), C.c_uint64(), C.c_double()
+        rc = M.mt_bursts(threads, 300, server, C.byref(mis), C.byref(fr), C.byref(us))
+        assert rc == 0 and mis.value == 0, (rc, mis.value)
+        out[f"{threads}_threads_{'server' if server else 'launch'}_us"] = us.value
+print(json.dumps(out))
