@@ -1284,20 +1284,45 @@ k_ip_fn(const uint8_t* __restrict__ buf, uint64_t buf_bytes, const uint64_t* __r
 // ---------------------------------------------------------------------------
 // launchers (called from gcs_api.cpp)
 
+// TX write-back of a fixed-stride frame: the 64 B sector holding both check
+// fields, or its whole first 128 B line.  The line lies inside the frame's own
+// slot (16 * chunks <= stride), so no other frame shares it, and at a 128 B-
+// multiple stride it is one aligned line.  A whole line drains cheaper than a
+// partial one while the written lines stay in the Infinity Cache, but it is
+// twice the bytes once they spill to HBM: C2 1M x 1500 B 260.6 -> 254.6 us,
+// 2M 524.9 -> 563.7 us, 4M 1114 -> 1178 us (profiles/r02/pmc_configs.csv,
+// kbench_tx_nt.log).  So lines up to kLineWbBytes of them per launch, sectors
+// beyond.  (Descriptor batches keep the sector: a packed frame's line can hold
+// its neighbour's bytes.)
+constexpr uint64_t kLineWbBytes = 128ull << 20;
+
+template <int G, int U, bool COMPUTE, bool LOOP, bool EXT, int K = 1, int WM = kWM>
+static hipError_t launch_fixed_wm(uint8_t* frames, uint64_t stride, u32 frame_len, u32 n,
+                                  uint8_t* code, uint32_t* csum, u32 flags, const Ext& ext,
+                                  hipStream_t s)
+{
+    constexpr int FPB = kBlock / G * K;                // frames per block
+    dim3 grid((n + FPB - 1) / FPB);
+    if (EXT)
+        hipLaunchKernelGGL((k_fixed_x<G, U, COMPUTE, LOOP, kNT, WM, kXCD, K>), grid, dim3(kBlock),
+                           0, s, frames, stride, frame_len, n, code, csum, flags, ext);
+    else
+        hipLaunchKernelGGL((k_fixed<G, U, COMPUTE, LOOP, kNT, WM, kXCD, K>), grid, dim3(kBlock),
+                           0, s, frames, stride, frame_len, n, code, csum, flags);
+    return hipGetLastError();
+}
+
 template <int G, int U, bool COMPUTE, bool LOOP, bool EXT, int K = 1>
 static hipError_t launch_fixed(uint8_t* frames, uint64_t stride, u32 frame_len, u32 n,
                                uint8_t* code, uint32_t* csum, u32 flags, const Ext& ext,
                                hipStream_t s)
 {
-    constexpr int FPB = kBlock / G * K;                // frames per block
-    dim3 grid((n + FPB - 1) / FPB);
-    if (EXT)
-        hipLaunchKernelGGL((k_fixed_x<G, U, COMPUTE, LOOP, kNT, kWM, kXCD, K>), grid, dim3(kBlock),
-                           0, s, frames, stride, frame_len, n, code, csum, flags, ext);
-    else
-        hipLaunchKernelGGL((k_fixed<G, U, COMPUTE, LOOP, kNT, kWM, kXCD, K>), grid, dim3(kBlock),
-                           0, s, frames, stride, frame_len, n, code, csum, flags);
-    return hipGetLastError();
+    if constexpr (COMPUTE && G >= 8)
+        if (stride % 128 == 0 && (uint64_t)n * 128 <= kLineWbBytes)
+            return launch_fixed_wm<G, U, COMPUTE, LOOP, EXT, K, WM_LINE_SC1>(
+                frames, stride, frame_len, n, code, csum, flags, ext, s);
+    return launch_fixed_wm<G, U, COMPUTE, LOOP, EXT, K>(frames, stride, frame_len, n, code, csum,
+                                                        flags, ext, s);
 }
 
 // (G, U) by frame size: G*16 B per load instruction of a group, U loads per lane.
