@@ -493,7 +493,8 @@ __device__ __forceinline__ void epilogue(const Hdr& h, Acc a, uint8_t* __restric
                                          int64_t wlim, bool desc_ok, int sub, u32 flags,
                                          uint8_t* __restrict__ out_code,
                                          uint32_t* __restrict__ out_csum, bool active,
-                                         const uint4 (&v)[U], const XFrame& xf = XFrame{})
+                                         const uint4 (&v)[U], const XFrame& xf = XFrame{},
+                                         uint8_t* stage = nullptr)
 {
     const u32 ihl = (h.d3 >> 16) & 15u;
     const u32 ts = 14 + 4 * ihl;
@@ -650,7 +651,10 @@ __device__ __forceinline__ void epilogue(const Hdr& h, Acc a, uint8_t* __restric
                     w = patch_hi(w, (int)((ts + 14) >> 2) & 3, l4c); // bytes ts+16..17
                 if (has_icmp)
                     w = patch_lo(w, (int)((ts + 2) >> 2) & 3, l4c);  // bytes ts+2..3
-                stg16<WM>(f + 16 * c, w);
+                if (stage != nullptr && c < 4)                      // sector 0 staged in LDS
+                    *reinterpret_cast<uint4*>(stage + 16 * c) = w;
+                else
+                    stg16<WM>(f + 16 * c, w);
             }
         }
     }
@@ -694,7 +698,7 @@ __device__ __forceinline__ void frame_body(const uint4 (&v)[U], uint8_t* __restr
                                            bool desc_ok, int sub, u32 flags,
                                            uint8_t* __restrict__ out_code,
                                            uint32_t* __restrict__ out_csum, bool active,
-                                           const XFrame& xf = XFrame{})
+                                           const XFrame& xf = XFrame{}, uint8_t* stage = nullptr)
 {
     const int nchunks = (desc_ok && active) ? (int)((len + 15) >> 4) : 0;
     // header words: chunk 0 lives in group lane 0, chunk 1 in group lane 1 (j = 0)
@@ -732,7 +736,7 @@ __device__ __forceinline__ void frame_body(const uint4 (&v)[U], uint8_t* __restr
         }
     }
     epilogue<G, U, COMPUTE, WM, EXT>(h, a, wf, len, avail, desc_ok, sub, flags, out_code, out_csum,
-                                     active, v, xf);
+                                     active, v, xf, stage);
 }
 
 template <int G, int U, bool COMPUTE, bool LOOP, bool SAFE, bool NT, int WM, bool EXT = false>

@@ -193,18 +193,18 @@ int imix_main(uint64_t n, int rounds)
                            std::string(TAG).find("no write") != std::string::npos           \
                                ? (u32)GCS_CF_NO_INPLACE : 0u);                              \
     }});
-    // round 2: class-1 / class-2 group shapes (fewer lanes per frame = fewer
-    // per-frame epilogues per wave instruction)
-    MIXED(false, 6, "6 <4,1|16,3|32,3>", 4, 1, 16, 3, 32, 3)
-    MIXED(false, 6, "6 <4,1|8,5|32,3>", 4, 1, 8, 5, 32, 3)
-    MIXED(false, 5, "5 <4,1|8,5|32,3>", 4, 1, 8, 5, 32, 3)
-    MIXED(false, 6, "6 <4,1|8,5|16,6>", 4, 1, 8, 5, 16, 6)
-    MIXED(false, 5, "5 <4,1|8,5|16,6>", 4, 1, 8, 5, 16, 6)
-    MIXED(false, 4, "4 <4,1|8,5|16,6>", 4, 1, 8, 5, 16, 6)
-    MIXED(false, 6, "6 <4,1|16,3|16,6>", 4, 1, 16, 3, 16, 6)
-    MIXED(true, 6, "6 <4,1|16,3|32,3>", 4, 1, 16, 3, 32, 3)
-    MIXED(true, 6, "6 <4,1|8,5|32,3>", 4, 1, 8, 5, 32, 3)
-    MIXED(true, 5, "5 <4,1|8,5|16,6>", 4, 1, 8, 5, 16, 6)
+    // round 2b: sector-0 write-backs staged in LDS and stored at block end in
+    // frame order (STAGE) vs in each list pass's epilogue
+    MIXED(true, 6, "6 shipped (epilogue sectors sc1)", 4, 1, 16, 3, 32, 3)
+    MIXED(true, 6, "6 epilogue sectors nt", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT)
+    MIXED(true, 6, "6 STAGE nt", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true)
+    MIXED(true, 7, "7 STAGE nt", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true)
+    MIXED(true, 5, "5 STAGE nt", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true)
+    MIXED(true, 6, "6 STAGE sc0 sc1", 4, 1, 16, 3, 32, 3, WM_SECTOR_SC01, 256, true, 1, 1, true)
+    MIXED(true, 6, "6 STAGE nt unordered", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, false, 1, 1, true)
+    MIXED(true, 6, "6 STAGE nt K0=2", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 2, 1, true)
+    MIXED(true, 6, "6 no write-back", 4, 1, 16, 3, 32, 3)
+    MIXED(false, 6, "6 verify shipped", 4, 1, 16, 3, 32, 3)
     vs.push_back({"verify  desc (launch_verify_desc)", vb, [&](hipStream_t st) {
         CK(launch_verify_desc(rx, total, doff, dlen, (u32)n, v1, 0u, st));
     }});
@@ -222,6 +222,19 @@ int imix_main(uint64_t n, int rounds)
     size_t bad = 0;
     for (auto b : h) bad += b != 0;
     std::printf("non-accept verdicts: %zu (expect 0)\n", bad);
+    // every compute variant alone on freshly zeroed check fields: verify accepts all
+    for (auto& v : vs) {
+        if (v.name.rfind("compute", 0) != 0 || v.name.find("no write") != std::string::npos)
+            continue;
+        hipLaunchKernelGGL(k_hdr_desc, dim3((n + 255) / 256), dim3(256), 0, s, tx, doff, dlen, n);
+        v.run(s);
+        CK(launch_verify_desc(tx, total, doff, dlen, (u32)n, v1, 0u, s));
+        CK(hipMemcpy(h.data(), v1, n, hipMemcpyDeviceToHost));
+        bad = 0;
+        for (auto b : h) bad += b != 0;
+        std::printf("check %-40s non-accept after a fill from zero: %zu (expect 0)\n",
+                    v.name.c_str(), bad);
+    }
     return 0;
 }
 
@@ -540,6 +553,14 @@ int copy_main(uint64_t n, int rounds)
         CK(launch_copy_fill(tx, n * stride, off, lens, src, n * plen + 64, soff, (u32)n, st,
                             nullptr, 0u, st_));
     }});
+#define CF2(G_, U_, O_)                                                                      \
+    vs.push_back({"fused copy + fill2 <" #G_ "," #U_ "> occ " #O_, bytes, [&](hipStream_t st_) { \
+        hipLaunchKernelGGL((k_copy_fill2<G_, U_, O_>), dim3((n + 256 / G_ - 1) / (256 / G_)),  \
+                           dim3(256), 0, st_, tx, n * stride, off, lens, src, n * plen + 64, soff, \
+                           (u32)n, st, nullptr, 0u);                                           \
+    }});
+    CF2(32, 3, 6) CF2(32, 3, 7) CF2(16, 6, 1) CF2(16, 6, 5) CF2(16, 6, 6) CF2(32, 4, 1)
+    CF2(32, 4, 5) CF2(16, 7, 1)
     uint8_t *asrc, *cdst;                     // copy ceilings write cdst, never tx
     CK(hipMalloc(&asrc, n * stride));
     CK(hipMalloc(&cdst, n * stride));
@@ -698,7 +719,13 @@ int lro_main(uint64_t n, int rounds)
         hipLaunchKernelGGL((k_gro<U_, W_, O_>), dim3((n + 63) / 64), dim3(256), 0, st, in, n * stride, \
                            off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd);  \
     }});
-    GROO(2, 64, 6) GROO(2, 64, 8) GROO(1, 64, 8)
+    GROO(2, 64, 6)
+#define GRO2(U_, W_, O_)                                                                     \
+    vs.push_back({"k_gro2<" #U_ "," #W_ "," #O_ "> (window 64, max 16384)", bytes, [&](hipStream_t st) { \
+        hipLaunchKernelGGL((k_gro2<U_, W_, O_>), dim3((n + 63) / 64), dim3(256), 0, st, in, n * stride, \
+                           off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd);  \
+    }});
+    GRO2(2, 64, 6) GRO2(2, 64, 8) GRO2(3, 64, 1) GRO2(3, 64, 6) GRO2(4, 64, 1) GRO2(4, 64, 5)
     vs.push_back({"verify (launch_verify_desc) for scale", (double)n * (L + 1), [&](hipStream_t st) {
         CK(launch_verify_desc(in, n * stride, off, lens, (u32)n, vd, 0u, st));
     }});
@@ -706,6 +733,23 @@ int lro_main(uint64_t n, int rounds)
         CK(hipMemcpyAsync(out, in, n * stride, hipMemcpyDeviceToDevice, st));
     }});
     run_variants(vs, s, rounds);
+    // every variant's output against launch_gro's, byte for byte
+    {
+        std::vector<uint8_t> ref(n * stride), got(n * stride);
+        CK(hipMemsetAsync(out, 0, n * stride, s));
+        CK(launch_gro(in, n * stride, off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol,
+                      hd, s));
+        CK(hipMemcpy(ref.data(), out, n * stride, hipMemcpyDeviceToHost));
+        for (auto& v : vs) {
+            if (v.name.rfind("k_gro", 0) != 0)
+                continue;
+            CK(hipMemsetAsync(out, 0, n * stride, s));
+            v.run(s);
+            CK(hipMemcpy(got.data(), out, n * stride, hipMemcpyDeviceToHost));
+            std::printf("check %-44s output %s launch_gro's\n", v.name.c_str(),
+                        ref == got ? "equals" : "DIFFERS FROM");
+        }
+    }
     CK(launch_gro(in, n * stride, off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd,
                   s));
     std::vector<uint16_t> hl(n);
