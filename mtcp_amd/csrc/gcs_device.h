@@ -43,8 +43,15 @@ enum { WM_HALFWORD = 0,   // two 2-byte stores by the group leader
        WM_SECTOR_SC1 = 4, // ... with sc1 (write-through past the XCD L2) stores
        WM_LINE_SC1 = 5,   // the 128 B line(s) holding a check field, sc1 stores
        WM_CHUNK_SC1 = 6,  // WM_CHUNK with sc1 stores
-       WM_SECTOR_SC01 = 7 // WM_SECTOR with sc0 sc1 (system scope) stores
+       WM_SECTOR_SC01 = 7, // WM_SECTOR with sc0 sc1 (system scope) stores
+       WM_LINE_NT = 8,     // WM_LINE_SC1 with non-temporal stores
+       WM_LINE = 9         // WM_LINE_SC1 with plain stores
 };
+
+__host__ __device__ constexpr bool wm_line(int wm)
+{
+    return wm == WM_LINE_SC1 || wm == WM_LINE_NT || wm == WM_LINE;
+}
 
 __host__ __device__ constexpr bool wm_sc1(int wm)
 {
@@ -169,7 +176,7 @@ template <int WM>
 __device__ __forceinline__ void stg16(uint8_t* p, uint4 v)
 {
     u32x4 d = u32x4{v.x, v.y, v.z, v.w};
-    if constexpr (WM == WM_SECTOR_NT) {
+    if constexpr (WM == WM_SECTOR_NT || WM == WM_LINE_NT) {
         __builtin_nontemporal_store(d, reinterpret_cast<u32x4*>(p));
     } else if constexpr (wm_sc1(WM)) {
         // No result register, so nothing to wait for before the kernel ends; but
@@ -629,7 +636,7 @@ __device__ __forceinline__ void epilogue(const Hdr& h, Acc a, uint8_t* __restric
                 const bool has_icmp = wicmp && c == cicmp;
                 const bool take = (WM == WM_CHUNK || WM == WM_CHUNK_SC1)
                                       ? (has_ip || has_tcp || has_icmp)
-                                      : WM == WM_LINE_SC1
+                                      : wm_line(WM)
                                       ? true                       // c < 8: line 0 holds all
                                       : ((c >> 2) == 0 || (wtcp && (c >> 2) == (ctcp >> 2)) ||
                                          (wicmp && (c >> 2) == (cicmp >> 2)));

@@ -536,13 +536,15 @@ __device__ __forceinline__ void desc_mixed(uint8_t* __restrict__ frames, uint64_
         }
     }
     __syncthreads();
-    const int n0 = cnt[0], n1 = cnt[1], n2 = cnt[2];
-    uint32_t* hl = EXT && !COMPUTE ? hashes : nullptr;
-    uint16_t* ql = EXT && !COMPUTE ? queues : nullptr;
-    uint4* stg = COMPUTE && S::STAGE ? stage : nullptr;
-    if (n0) desc_class<S::G0, S::U0, COMPUTE, false, EXT, S::WM, S::K0>(frames, frames_bytes, soff, slen, list[0], n0, flags, codes, csums, ext, hl, ql, stg);
-    if (n1) desc_class<S::G1, S::U1, COMPUTE, false, EXT, S::WM, S::K1>(frames, frames_bytes, soff, slen, list[1], n1, flags, codes, csums, ext, hl, ql, stg);
-    if (n2) desc_class<S::G2, S::U2, COMPUTE, true, EXT, S::WM>(frames, frames_bytes, soff, slen, list[2], n2, flags, codes, csums, ext, hl, ql, stg);
+    {
+        const int n0 = cnt[0], n1 = cnt[1], n2 = cnt[2];
+        uint32_t* hl = EXT && !COMPUTE ? hashes : nullptr;
+        uint16_t* ql = EXT && !COMPUTE ? queues : nullptr;
+        uint4* stg = COMPUTE && S::STAGE ? stage : nullptr;
+        if (n0) desc_class<S::G0, S::U0, COMPUTE, false, EXT, S::WM, S::K0>(frames, frames_bytes, soff, slen, list[0], n0, flags, codes, csums, ext, hl, ql, stg);
+        if (n1) desc_class<S::G1, S::U1, COMPUTE, false, EXT, S::WM, S::K1>(frames, frames_bytes, soff, slen, list[1], n1, flags, codes, csums, ext, hl, ql, stg);
+        if (n2) desc_class<S::G2, S::U2, COMPUTE, true, EXT, S::WM>(frames, frames_bytes, soff, slen, list[2], n2, flags, codes, csums, ext, hl, ql, stg);
+    }
     __syncthreads();
     if (COMPUTE && S::STAGE && !(flags & GCS_CF_NO_INPLACE)) {
         // STAGE: the frames' sector-0 write-backs leave together, in frame
@@ -713,151 +715,6 @@ __device__ __forceinline__ void cf_issue(int base, int sub, int nchunks, bool co
     }
 }
 
-template <int G, int U, int OCC = 1>
-__global__ void __launch_bounds__(kBlock, OCC)
-k_copy_fill(uint8_t* __restrict__ frames, uint64_t frames_bytes,
-            const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens,
-            const uint8_t* __restrict__ src, uint64_t src_bytes,
-            const uint64_t* __restrict__ src_off, u32 n, uint8_t* __restrict__ out_code,
-            uint32_t* __restrict__ out_csum, u32 flags)
-{
-    static_assert(G >= 16, "the first G chunks must hold the longest header (134 B)");
-    // Frame chunks read up front: 0..5, enough to parse (the doff byte of the
-    // longest IP header, ts + 12 <= 86, lies in chunk 5).  Further frame
-    // chunks are read only where the plan keeps frame bytes; the rest of the
-    // frame's old contents is overwritten by the payload, so reading it would
-    // waste ~0.45 GB per 1M x 1500 B frames (PMC: 2.2 GB read for 1.6 GB used).
-    constexpr int kHdrLanes = 6;
-    // Speculation: mTCP's data segments carry ihl 5 and doff 8 (ip_out.c:143,
-    // tcp_out.c:22-61 with timestamps), so headers end at 66 and tot_len covers
-    // the frame.  Batch 0's payload loads are issued for that layout together
-    // with the header loads, and re-issued only if the parsed headers differ:
-    // one memory round trip per frame instead of two.
-    constexpr int kSpecHl = 66;
-    constexpr int FPB = kBlock / G;
-    const int sub = threadIdx.x & (G - 1);
-    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);
-    const uint64_t i = (uint64_t)blk * FPB + threadIdx.x / G;
-    if (i >= n)
-        return;
-    const uint64_t o = off[i];
-    const u32 len = lens[i];
-    const uint64_t po_any = src_off[i];                // loaded with off[i], not after the headers
-    const bool ok = (o & 15) == 0 && o <= frames_bytes && len <= frames_bytes - o;
-    uint8_t* f = frames + (ok ? o : 0);
-    const int64_t avail = ok ? (int64_t)(frames_bytes - o) : 0;
-    const int nchunks = ok ? (int)((len + 15) >> 4) : 0;
-    const uint4 z = make_uint4(0, 0, 0, 0);
-
-    // headers: frame chunk `sub` < kHdrLanes
-    const uint4 hv = (sub < kHdrLanes && sub < nchunks)
-                         ? load_chunk<true, false>(f + 16 * sub, avail - 16 * sub)
-                         : z;
-    // speculative batch 0: the guessed source range lies inside the source
-    const int te_g = (int)len;
-    const bool copy_g = ok && te_g >= kSpecHl && po_any <= src_bytes &&
-                        (uint64_t)(te_g - kSpecHl) <= src_bytes - po_any;
-    uint4 fr[U], pv[U];
-    int plan[U];
-    cf_issue<G, U>(0, sub, nchunks, copy_g, kSpecHl, te_g, src + (copy_g ? po_any : 0),
-                   copy_g ? (int64_t)(src_bytes - po_any) : 0, f, avail, hv, kHdrLanes, fr, pv,
-                   plan);
-    Hdr h;
-    h.d3 = group_bcast<G, 0>(hv.w);
-    h.d4 = group_bcast<G, 1>(hv.x);
-    h.d5 = group_bcast<G, 1>(hv.y);
-    const int ihl = (int)((h.d3 >> 16) & 15u);
-    const int ts = 14 + 4 * ihl;
-    const int tot = (int)bswap16(h.d4 & 0xFFFFu);
-    const int te = 14 + tot;
-    const int pd = ts + 12;                            // doff << 4 | res
-    const u32 db = group_sum<G>(sub == (pd >> 4) ? chunk_byte(hv, pd & 15) : 0u);
-    const int doff = (int)(db >> 4);
-    const int hl = ts + 4 * doff;
-    const bool copy = ok && len >= 34 && (h.d3 & 0xFFFFu) == 0x0008u && ihl >= 5 &&
-                      (h.d5 >> 24) == 6 && doff >= 5 && tot >= 4 * (ihl + doff) &&
-                      te <= (int)len;
-    const uint64_t plen = copy ? (uint64_t)(te - hl) : 0;
-    const uint64_t po = copy ? po_any : 0;
-    if (copy && !(po <= src_bytes && plen <= src_bytes - po)) {   // group-uniform
-        if (sub == 0) {
-            if (out_code)
-                out_code[i] = GCS_TX_BAD_DESC;
-            if (out_csum)
-                out_csum[i] = 0;
-        }
-        return;
-    }
-    const uint8_t* ps = src + po;                      // frame byte p <- ps[p - hl]
-    // payload loads must stay inside the source buffer: `src_room` bytes from ps
-    const int64_t src_room = copy ? (int64_t)(src_bytes - po) : 0;
-    // wrong guess (group-uniform): batch 0 again, for the parsed layout
-    if (copy != copy_g || (copy && (hl != kSpecHl || te != te_g)))
-        cf_issue<G, U>(0, sub, nchunks, copy, hl, te, ps, src_room, f, avail, hv, kHdrLanes, fr,
-                       pv, plan);
-
-    Acc a = {0u, 0u, 0u};
-    uint4 first[U];
-    for (int base = 0; base < nchunks; base += G * U) {   // group-uniform
-        uint4 v[U];
-        // 1: issue the loads of every chunk of the batch (batch 0: above)
-        if (base > 0)
-            cf_issue<G, U>(base, sub, nchunks, copy, hl, te, ps, src_room, f, avail, hv,
-                           kHdrLanes, fr, pv, plan);
-        // 2: assemble
-#pragma unroll
-        for (int j = 0; j < U; j++) {
-            const int cb = 16 * (base + j * G + sub);
-            uint4 x = z;
-            switch (plan[j]) {
-            case AS_FRAME: x = fr[j]; break;
-            case AS_ONE: x = pv[j]; break;
-            case AS_UP: x = blend(fr[j], bytes_up(pv[j], hl - cb), byte_mask(hl - cb, 16)); break;
-            case AS_TAIL: x = blend(fr[j], pv[j], byte_mask(0, te - cb)); break;
-            case AS_BYTES: {
-                u32 w[4] = {0u, 0u, 0u, 0u};
-                for (int k = 0; k < 16; k++) {
-                    const int p = cb + k;
-                    const u32 b = (p >= hl && p < te) ? (u32)ps[p - hl] : chunk_byte(fr[j], k);
-                    w[k >> 2] |= b << (8 * (k & 3));
-                }
-                x = make_uint4(w[0], w[1], w[2], w[3]);
-                break;
-            }
-            default: break;
-            }
-            v[j] = x;
-        }
-#pragma unroll
-        for (int j = 0; j < U; j++)
-            accum_chunk<true>(v[j], 16 * (base + j * G + sub), ts, te, a);
-        if (copy) {
-            // chunks 8.. go out now; the first line (with the check fields) in the epilogue
-#pragma unroll
-            for (int j = 0; j < U; j++) {
-                const int c = base + j * G + sub;
-                const int cb = 16 * c;
-                if (c < 8 || c >= nchunks || cb >= te)
-                    continue;
-                if (cb + 16 <= avail) {
-                    stg16<WM_SECTOR>(f + cb, v[j]);
-                } else {                                     // the buffer ends inside it
-                    for (int k = 0; k < 16 && cb + k < te; k++)
-                        f[cb + k] = (uint8_t)chunk_byte(v[j], k);
-                }
-            }
-        }
-        if (base == 0) {
-#pragma unroll
-            for (int j = 0; j < U; j++)
-                first[j] = v[j];
-        }
-    }
-    epilogue<G, U, true, WM_LINE_SC1>(h, a, f, len, avail, ok, sub, flags & ~GCS_CF_NO_INPLACE,
-                                      out_code ? out_code + i : nullptr,
-                                      out_csum ? out_csum + i : nullptr, true, first);
-}
-
 // Assemble destination chunks from a batch's loads (cf_issue's plans), in
 // place: x[j] becomes chunk base + j*G + sub of the filled frame.
 template <int G, int U>
@@ -889,16 +746,26 @@ __device__ __forceinline__ void cf_assemble(int base, int sub, int hl, int te, c
     }
 }
 
-// Copy + fill, register-lean form of k_copy_fill (same contract, same
-// results).  A frame's batch 0 (its first G*U chunks, the whole frame up to
-// 16*G*U bytes) is assembled IN the registers its frame chunks were loaded
-// into, folded there and handed to the epilogue as they are -- no separate
-// copy of the first batch kept across a batch loop.  Longer frames walk their
-// later batches first (no speculation for them), then batch 0.  ihl = 5 waves
-// fold with the constant-mask path (accum_fast5).
+// Frame chunks read up front: 0..5, enough to parse (the doff byte of the
+// longest IP header, ts + 12 <= 86, lies in chunk 5).  Further frame chunks are
+// read only where the plan keeps frame bytes; the rest of the frame's old
+// contents is overwritten by the payload (PMC: 2.2 -> 1.6 GB read per 1M x
+// 1500 B).  Speculation: mTCP's data segments carry ihl 5 and doff 8
+// (ip_out.c:143, tcp_out.c:22-61 with timestamps), so headers end at 66 and
+// tot_len covers the frame; batch 0's payload loads are issued for that layout
+// together with the header loads and re-issued only if the parsed headers
+// differ -- one memory round trip per frame instead of two.
+// Registers: batch 0 (the frame's first G*U chunks, the whole frame up to
+// 16*G*U bytes) is assembled IN the registers its loads landed in, folded
+// there and handed to the epilogue as it is; no copy of it is kept across a
+// batch loop.  Frames longer than one batch build their later batches first
+// (no speculation for them), then batch 0.  ihl = 5 waves fold with the
+// constant-mask path (accum_fast5).  1M x 1500 B: 706-711 -> 576-624 us
+// against the earlier form (88 VGPRs, first batch copied; kbench copy,
+// profiles/r02/kbench_copy_fill2*.log).
 template <int G, int U, int OCC = 1>
 __global__ void __launch_bounds__(kBlock, OCC)
-k_copy_fill2(uint8_t* __restrict__ frames, uint64_t frames_bytes,
+k_copy_fill(uint8_t* __restrict__ frames, uint64_t frames_bytes,
              const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens,
              const uint8_t* __restrict__ src, uint64_t src_bytes,
              const uint64_t* __restrict__ src_off, u32 n, uint8_t* __restrict__ out_code,
@@ -1380,308 +1247,6 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
     }
 }
 
-// k_gro with a register-lean phase D: each run's batches are built last to
-// first, assembled in the registers they were loaded into and folded with the
-// ihl = 5 constant masks; batch 0 stays in those registers for the epilogue
-// (no copy of it kept across the batch loop).
-template <int U, int W = kGroW, int OCC = 1>
-__global__ void __launch_bounds__(kBlock, OCC)
-k_gro2(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restrict__ off,
-      const uint16_t* __restrict__ lens, const uint8_t* __restrict__ verdict, u32 n, u32 window,
-      u32 max_len, uint8_t* __restrict__ out, uint64_t out_bytes, uint64_t* __restrict__ out_off,
-      uint16_t* __restrict__ out_len, uint32_t* __restrict__ head)
-{
-    static_assert(W <= kBlock, "one frame per thread");
-    constexpr int G = 64;
-    __shared__ __attribute__((aligned(16))) uint8_t hdr[W][kGroHdr];
-    __shared__ int pay[W];         // TCP payload bytes of a mergeable frame, else -1
-    __shared__ uint8_t cont[W];
-    __shared__ uint8_t dok[W];     // descriptor inside the input buffer
-    __shared__ uint32_t pref[W];   // payload offset of a member within its run
-    __shared__ uint16_t rhead[W];  // run head (window index) of each frame
-    __shared__ uint16_t run_t[W];  // runs: head index, member count, length, offset
-    __shared__ uint16_t run_n[W];
-    __shared__ uint32_t run_len[W];
-    __shared__ uint64_t run_off[W];
-    __shared__ int nruns;
-    __shared__ uint64_t soff[W];   // the window's descriptors: no dependent global loads in D
-    __shared__ uint16_t rn_at[W];  // per run head (window index): members, length, run index
-    __shared__ uint32_t rl_at[W];
-    __shared__ uint16_t ridx[W];
-    __shared__ uint32_t wsum[kBlock / 64][2];
-
-    const int t = threadIdx.x;
-    const uint64_t w0 = (uint64_t)blockIdx.x * window;
-    const int cnt = (int)min<uint64_t>(window, n - w0);
-    const uint4 z = make_uint4(0, 0, 0, 0);
-
-    // A: parse
-    if (t < cnt) {
-        const uint64_t o = off[w0 + t];
-        const u32 L = lens[w0 + t];
-        soff[t] = o;
-        const bool ok = (o & 15) == 0 && o <= in_bytes && L <= in_bytes - o;
-        const bool acc = ok && verdict[w0 + t] == GCS_V_ACCEPT;
-        dok[t] = ok;
-#pragma unroll
-        for (int c = 0; c < kGroHdr / 16; c++) {
-            const uint4 v = acc ? load_chunk<true, false>(in + o + 16 * c,
-                                                          (int64_t)(in_bytes - o) - 16 * c)
-                                : z;
-            uint32_t* d = reinterpret_cast<uint32_t*>(&hdr[t][16 * c]);
-            d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
-        }
-        const uint8_t* h = hdr[t];
-        int p = -1;
-        if (acc && (h[14] & 0x0F) == 5)
-            p = (int)lds_be16(h + 16) - 20 - 4 * (h[46] >> 4);
-        pay[t] = p;
-    }
-    __syncthreads();
-    // B: continuation
-    if (t < cnt)
-        cont[t] = t > 0 && gro_cont(hdr[t - 1], hdr[t], pay[t - 1], pay[t]);
-    __syncthreads();
-    // C: runs.  A chain is a maximal sequence of frames that each continue the
-    // previous one (cont); every frame of a chain is mergeable, so runs are
-    // chains cut greedily at max_len -- ref_gro_batch's walk, done by each
-    // chain's first thread over its own chain, in parallel.  Then one block
-    // scan gives every run its index and its 16 B-aligned output offset.
-    // (One thread walking the whole window took ~1/3 of the kernel.)
-    uint32_t rl = 0;                                   // this thread's run length if it heads one
-    bool rs = false;                                   // ... and whether it does
-    if (t < cnt && (t == 0 || !cont[t])) {
-        int cur = t;
-        u32 mlen = pay[t] > 0 ? 34 + 4 * (hdr[t][46] >> 4) + (u32)pay[t]
-                              : (dok[t] ? (u32)lens[w0 + t] : 0u);     // a bad descriptor: nothing
-        pref[t] = 0;
-        rhead[t] = (uint16_t)t;
-        rn_at[t] = 1;
-        for (int k = t + 1; k < cnt && cont[k]; k++) {
-            if (mlen + (u32)pay[k] <= max_len) {
-                pref[k] = mlen - (34 + 4 * (hdr[cur][46] >> 4));
-                mlen += (u32)pay[k];
-                rhead[k] = (uint16_t)cur;
-                rn_at[cur]++;
-                continue;
-            }
-            rl_at[cur] = mlen;                         // max_len cut: k heads a new run
-            cur = k;
-            mlen = 34 + 4 * (hdr[k][46] >> 4) + (u32)pay[k];
-            pref[k] = 0;
-            rhead[k] = (uint16_t)k;
-            rn_at[k] = 1;
-        }
-        rl_at[cur] = mlen;
-    }
-    __syncthreads();
-    if (t < cnt && rhead[t] == t) {
-        rs = true;
-        rl = rl_at[t];
-    }
-    // exclusive scans of (run starts, aligned run lengths) over the window
-    u32 xs = rs ? 1u : 0u, xl = rs ? (rl + 15u) & ~15u : 0u;
-    {
-        const int lane = t & 63, w = t >> 6;
-        u32 is = xs, il = xl;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const u32 os = __shfl_up(is, d, 64), ol = __shfl_up(il, d, 64);
-            if (lane >= d) {
-                is += os;
-                il += ol;
-            }
-        }
-        if (lane == 63) {
-            wsum[w][0] = is;
-            wsum[w][1] = il;
-        }
-        __syncthreads();
-        u32 bs = 0, bl = 0;
-        for (int q = 0; q < w; q++) {
-            bs += wsum[q][0];
-            bl += wsum[q][1];
-        }
-        xs = bs + is - xs;                             // exclusive
-        xl = bl + il - xl;
-        if (t == kBlock - 1)
-            nruns = (int)(bs + is);
-    }
-    const uint64_t o0 = cnt ? soff[0] : 0;
-    if (rs) {
-        run_t[xs] = (uint16_t)t;
-        run_n[xs] = (uint16_t)rn_at[t];
-        run_len[xs] = rl;
-        run_off[xs] = o0 + xl;
-        ridx[t] = (uint16_t)xs;
-    }
-    __syncthreads();
-    if (t < cnt) {
-        const int hk = rhead[t];
-        const int r = ridx[hk];
-        head[w0 + t] = (uint32_t)(w0 + hk);
-        out_off[w0 + t] = run_off[r];
-        out_len[w0 + t] = hk == t ? (uint16_t)run_len[r] : (uint16_t)0;
-    }
-
-    // D: build the runs, one wave per run
-    const int wave = t >> 6, sub = t & 63, nwaves = kBlock / 64;
-    for (int r = wave; r < nruns; r += nwaves) {       // wave-uniform
-        const int k0 = run_t[r], nm = run_n[r];
-        const u32 mlen = run_len[r];
-        const uint64_t oo = run_off[r];
-        uint8_t* m = out + oo;
-        const int64_t wlim = oo <= out_bytes ? (int64_t)(out_bytes - oo) : 0;
-        const uint64_t io = soff[k0];
-        const int nchunks = (int)((mlen + 15) >> 4);
-        if (nm == 1) {                                 // as it is
-            const int64_t avail = (int64_t)(in_bytes - io);
-            for (int c = sub; c < nchunks; c += G) {
-                const uint4 v = load_chunk<true, false>(in + io + 16 * c, avail - 16 * c);
-                if (16 * c + 16 <= wlim) {
-                    stg16<WM_SECTOR>(m + 16 * c, v);
-                } else {
-                    for (int k = 0; k < 16 && 16 * c + k < (int)mlen && 16 * c + k < wlim; k++)
-                        m[16 * c + k] = (uint8_t)chunk_byte(v, k);
-                }
-            }
-            continue;
-        }
-        const uint8_t* hh = hdr[k0];
-        const int hl = 34 + 4 * (hh[46] >> 4);
-        uint8_t psh = 0;
-        for (int k = k0; k < k0 + nm; k++)
-            psh |= hdr[k][47] & 0x08;
-        const int te = (int)mlen;                       // ts = 34: merged frames have ihl 5
-        Acc a = {0u, 0u, 0u};
-        const Mask5 msk = masks5<true>(sub);
-        const uint8_t* in_end = in + in_bytes;
-        uint4 x[U];
-        // batches last to first: batch 0 (headers, check fields) ends in x for the epilogue
-        for (int base = G * U * ((nchunks - 1) / (G * U)); base >= 0; base -= G * U) {
-            uint4 pb[U];
-            int plan[U], cut[U];
-            // 1: issue the loads of every chunk of the batch
-#pragma unroll
-            for (int j = 0; j < U; j++) {
-                const int c = base + j * G + sub;
-                const int cb = 16 * c;
-                int pl = AS_ZERO, ct = 0;
-                x[j] = z;
-                pb[j] = z;
-                if (c < nchunks && cb + 16 <= hl) {
-                    pl = AS_FRAME;                                 // head's headers (LDS)
-                } else if (c < nchunks && cb < hl) {
-                    const uint8_t* p0 = in + soff[k0] + hl;
-                    ct = hl - cb;                                  // header bytes in the chunk
-                    if (cb + 16 <= te && pay[k0] >= 16 - ct && p0 + 16 <= in_end) {
-                        pl = AS_UP;
-                        x[j] = ldg16u(p0);
-                    } else {
-                        pl = AS_BYTES;
-                    }
-                } else if (c < nchunks) {
-                    const u32 q = (u32)(cb - hl);                  // merged payload offset
-                    int lo2 = k0, hi2 = k0 + nm - 1;
-                    while (lo2 < hi2) {
-                        const int mid = (lo2 + hi2 + 1) >> 1;
-                        if (pref[mid] <= q) lo2 = mid; else hi2 = mid - 1;
-                    }
-                    const int sg = lo2;
-                    const int rem = (int)(pref[sg] + (u32)pay[sg] - q);   // bytes left in sg
-                    const int need = min(16, te - cb);
-                    const uint8_t* pq = in + soff[sg] + hl + (q - pref[sg]);
-                    if (rem >= need && pq + 16 <= in_end) {
-                        pl = AS_ONE;                               // one member (masked at te)
-                        x[j] = ldg16u(pq);
-                    } else if (sg + 1 < k0 + nm && pay[sg + 1] >= need - rem &&
-                               pq + 16 <= in_end && in + soff[sg + 1] + hl + 16 <= in_end) {
-                        pl = AS_TWO;                               // the end of sg, then sg+1
-                        ct = rem;
-                        x[j] = ldg16u(pq);
-                        pb[j] = ldg16u(in + soff[sg + 1] + hl);
-                    } else {
-                        pl = AS_BYTES;
-                    }
-                }
-                plan[j] = pl;
-                cut[j] = ct;
-            }
-            // 2: assemble in place
-#pragma unroll
-            for (int j = 0; j < U; j++) {
-                const int c = base + j * G + sub;
-                const int cb = 16 * c;
-                switch (plan[j]) {
-                case AS_FRAME:
-                    x[j] = *reinterpret_cast<const uint4*>(&hh[cb]);
-                    break;
-                case AS_UP:
-                    x[j] = blend(*reinterpret_cast<const uint4*>(&hh[cb]), bytes_up(x[j], cut[j]),
-                                 byte_mask(cut[j], 16));
-                    break;
-                case AS_TWO:
-                    x[j] = blend(x[j], bytes_up(pb[j], cut[j]), byte_mask(cut[j], 16));
-                    break;
-                case AS_BYTES: {
-                    u32 w[4] = {0u, 0u, 0u, 0u};
-                    int s2 = k0;
-                    for (int k = 0; k < 16; k++) {
-                        const int p = cb + k;
-                        u32 bb = 0;
-                        if (p < hl) {
-                            bb = hh[p];
-                        } else if (p < te) {
-                            const u32 qq = (u32)(p - hl);
-                            while (qq >= pref[s2] + (u32)pay[s2])
-                                s2++;
-                            bb = in[soff[s2] + hl + (qq - pref[s2])];
-                        }
-                        w[k >> 2] |= bb << (8 * (k & 3));
-                    }
-                    x[j] = make_uint4(w[0], w[1], w[2], w[3]);
-                    break;
-                }
-                default:
-                    break;
-                }
-                if (c < nchunks && cb + 16 > te)                    // nothing past the frame
-                    x[j] = blend(z, x[j], byte_mask(0, te - cb));
-                if (c == 1)                                        // tot_len (bytes 16-17)
-                    x[j].x = (x[j].x & 0xFFFF0000u) | bswap16((mlen - 14) & 0xFFFFu);
-                if (c == 2)                                        // flags (byte 47): PSH of any member
-                    x[j].w |= (u32)psh << 24;
-            }
-            if (base == 0)
-                accum_fast5<true, true>(x[0], sub, te, msk, a);
-            else
-                accum_fast5<true, false>(x[0], base + sub, te, msk, a);
-#pragma unroll
-            for (int j = 1; j < U; j++)
-                accum_fast5<true, false>(x[j], base + j * G + sub, te, msk, a);
-#pragma unroll
-            for (int j = 0; j < U; j++) {
-                const int c = base + j * G + sub;
-                const int cb = 16 * c;
-                if (c < 8 || c >= nchunks)
-                    continue;
-                if (cb + 16 <= wlim) {
-                    stg16<WM_SECTOR>(m + cb, x[j]);
-                } else {
-                    for (int k = 0; k < 16 && cb + k < te && cb + k < wlim; k++)
-                        m[cb + k] = (uint8_t)chunk_byte(x[j], k);
-                }
-            }
-        }
-        Hdr h;
-        h.d3 = group_bcast<G, 0>(x[0].w);
-        h.d4 = group_bcast<G, 1>(x[0].x);
-        h.d5 = group_bcast<G, 1>(x[0].y);
-        epilogue<G, U, true, WM_LINE_SC1>(h, a, m, mlen, wlim, true, sub, 0u, nullptr, nullptr,
-                                          true, x);
-    }
-}
-
 // TCPCalcChecksum(buf + off[i], len[i], saddr[i], daddr[i]), G lanes per item;
 // PSEUDO = false: ICMPChecksum(buf + off[i], len[i]) (icmp.c:18-42), the same
 // word loop and odd-byte rule without the pseudo header.
@@ -1975,7 +1540,9 @@ hipError_t launch_copy_fill(uint8_t* frames, uint64_t frames_bytes, const uint64
                             const uint64_t* src_off, u32 n, uint8_t* status, uint32_t* csums,
                             u32 flags, hipStream_t s)
 {
-    constexpr int G = 32, U = 3, FPB = kBlock / G;
+    // 16 lanes x 6 chunks per frame (124 VGPRs, 4 waves per SIMD, no spills):
+    // as fast as <32,3> at 6 waves, which spills (576-624 us per 1M x 1500 B)
+    constexpr int G = 16, U = 6, FPB = kBlock / G;
     hipLaunchKernelGGL((k_copy_fill<G, U>), dim3((n + FPB - 1) / FPB), dim3(kBlock), 0, s, frames,
                        frames_bytes, off, len, src, src_bytes, src_off, n, status, csums, flags);
     return hipGetLastError();

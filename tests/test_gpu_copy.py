@@ -98,6 +98,28 @@ def test_copy_fill_vs_oracle(torch_dev, ctx, O):
     assert (host(v)[rst == 0] == 0).all()
 
 
+def test_copy_fill_jumbo_vs_oracle(torch_dev, ctx, O):
+    """Frames longer than one batch of the kernel's lanes (> 1536 B, up to
+    9014 B jumbo frames): later batches are built before batch 0."""
+    t = torch_dev
+    n = 3000
+    rng = np.random.default_rng(91)
+    lens = rng.integers(1400, 9015, size=n).astype(np.uint16)
+    lens[::5] = 1536
+    lens[1::5] = 1537
+    buf, off, lens, src, src_off = segments(n, 91, lens=lens)
+    # payloads laid end to end in the source, every alignment
+    src_off[:] = np.cumsum(lens.astype(np.uint64)) - lens.astype(np.uint64)
+    src_off += rng.integers(0, 16, size=n).astype(np.uint64)
+    got, st, cs = run_copy(t, ctx, buf, off, lens, src, src_off)
+    ref = buf.copy()
+    rst, rcs = O.compute_copy_batch(ref, off, lens, src, src_off)
+    np.testing.assert_array_equal(st, rst)
+    np.testing.assert_array_equal(cs, rcs)
+    np.testing.assert_array_equal(got, ref)
+    assert (rst == 0).mean() > 0.95
+
+
 @pytest.mark.parametrize("payload", [0, 1, 2, 15, 16, 17, 31, 33, 100, 1434, 1448])
 @pytest.mark.parametrize("doff", [5, 8, 15])
 def test_copy_fill_payload_edges(torch_dev, ctx, O, payload, doff):

@@ -135,6 +135,33 @@ __global__ void k_hdr_desc(uint8_t* buf, const uint64_t* off, const uint16_t* le
 
 void run_variants(std::vector<Variant>& vs, hipStream_t s, int rounds);
 
+// IMIX read ceiling in the descriptor kernel's own block partition: block b
+// streams the packed region of descriptors [256b, 256b+256), [off[256b],
+// off[last] + len[last]), with U chunks per lane per round, every load
+// instruction of a wave covering 1 KiB; no arithmetic.
+template <int U>
+__global__ void __launch_bounds__(256) k_read_regions(const uint8_t* __restrict__ p,
+                                                      const uint64_t* __restrict__ off,
+                                                      const uint16_t* __restrict__ lens, u32 n,
+                                                      uint32_t* out)
+{
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);
+    const uint64_t f0 = (uint64_t)blk * 256, f1 = min<uint64_t>(f0 + 256, n) - 1;
+    const uint64_t a = off[f0] & ~15ull, b = off[f1] + lens[f1];
+    uint32_t acc = 0;
+    for (uint64_t base = a; base < b; base += 256ull * U * 16) {
+        uint4 v[U];
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            const uint64_t o = base + (uint64_t)(j * 256 + threadIdx.x) * 16;
+            v[j] = o + 16 <= b ? ldg16<true>(p + o) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < U; j++) acc += v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
+    }
+    if (acc == 0x9E3779B9u) out[0] = acc;
+}
+
 // C3: IMIX 64/576/1500 at 7:4:1, pslib 64 B packing, descriptor kernels.
 int imix_main(uint64_t n, int rounds)
 {
@@ -193,24 +220,22 @@ int imix_main(uint64_t n, int rounds)
                            std::string(TAG).find("no write") != std::string::npos           \
                                ? (u32)GCS_CF_NO_INPLACE : 0u);                              \
     }});
-    // round 2b: sector-0 write-backs staged in LDS and stored at block end in
-    // frame order (STAGE) vs in each list pass's epilogue
-    MIXED(true, 6, "6 shipped (epilogue sectors sc1)", 4, 1, 16, 3, 32, 3)
-    MIXED(true, 6, "6 epilogue sectors nt", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT)
-    MIXED(true, 6, "6 STAGE nt", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true)
-    MIXED(true, 7, "7 STAGE nt", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true)
-    MIXED(true, 5, "5 STAGE nt", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true)
-    MIXED(true, 6, "6 STAGE sc0 sc1", 4, 1, 16, 3, 32, 3, WM_SECTOR_SC01, 256, true, 1, 1, true)
-    MIXED(true, 6, "6 STAGE nt unordered", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, false, 1, 1, true)
-    MIXED(true, 6, "6 STAGE nt K0=2", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 2, 1, true)
+    // round 2b: staged sector write-back (shipped: STAGE nt)
+    MIXED(true, 6, "6 epilogue sectors sc1 (round 1)", 4, 1, 16, 3, 32, 3)
+    MIXED(true, 6, "6 STAGE nt (shipped)", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true)
     MIXED(true, 6, "6 no write-back", 4, 1, 16, 3, 32, 3)
-    MIXED(false, 6, "6 verify shipped", 4, 1, 16, 3, 32, 3)
     vs.push_back({"verify  desc (launch_verify_desc)", vb, [&](hipStream_t st) {
         CK(launch_verify_desc(rx, total, doff, dlen, (u32)n, v1, 0u, st));
     }});
     vs.push_back({"compute desc (launch_compute_desc)", cb, [&](hipStream_t st) {
         CK(launch_compute_desc(tx, total, doff, dlen, (u32)n, nullptr, nullptr, 0u, st));
     }});
+#define RREG(U_)                                                                          \
+    vs.push_back({"read-ceiling block regions one-shot U=" #U_, (double)total, [&](hipStream_t st) { \
+        hipLaunchKernelGGL((k_read_regions<U_>), dim3((n + 255) / 256), dim3(256), 0, st, rx,  \
+                           doff, dlen, (u32)n, sink);                                           \
+    }});
+    RREG(2) RREG(4) RREG(8)
     vs.push_back({"read-ceiling uint4 NT (whole packed buffer)", (double)total,
                   [&](hipStream_t st) {
         hipLaunchKernelGGL((k_read<true>), dim3(cus * 8), dim3(256), 0, st, (const uint4*)rx,
@@ -222,6 +247,37 @@ int imix_main(uint64_t n, int rounds)
     size_t bad = 0;
     for (auto b : h) bad += b != 0;
     std::printf("non-accept verdicts: %zu (expect 0)\n", bad);
+    // every verify variant on a corrupted copy of rx: verdicts equal launch_verify_desc's
+    {
+        uint8_t* rxc;
+        CK(hipMalloc(&rxc, total));
+        CK(hipMemcpy(rxc, rx, total, hipMemcpyDeviceToDevice));
+        std::vector<uint8_t> hb(total);
+        CK(hipMemcpy(hb.data(), rxc, total, hipMemcpyDeviceToHost));
+        uint64_t y = 0x1234567;
+        for (uint64_t i = 0; i < n; i += 97) {
+            y ^= y << 13; y ^= y >> 7; y ^= y << 17;
+            hb[off[i] + y % len[i]] ^= (uint8_t)(1u << (y % 8));
+        }
+        CK(hipMemcpy(rxc, hb.data(), total, hipMemcpyHostToDevice));
+        uint8_t* keep = rx;
+        rx = rxc;
+        CK(launch_verify_desc(rx, total, doff, dlen, (u32)n, v1, 0u, s));
+        std::vector<uint8_t> ref(n), got(n);
+        CK(hipMemcpy(ref.data(), v1, n, hipMemcpyDeviceToHost));
+        size_t drops = 0;
+        for (auto b : ref) drops += b != 0;
+        for (auto& v : vs) {
+            if (v.name.rfind("verify", 0) != 0)
+                continue;
+            CK(hipMemset(v1, 0xEE, n));
+            v.run(s);
+            CK(hipMemcpy(got.data(), v1, n, hipMemcpyDeviceToHost));
+            std::printf("check %-40s verdicts on %zu corrupted frames: %s\n", v.name.c_str(), drops,
+                        got == ref ? "equal" : "DIFFER");
+        }
+        rx = keep;
+    }
     // every compute variant alone on freshly zeroed check fields: verify accepts all
     for (auto& v : vs) {
         if (v.name.rfind("compute", 0) != 0 || v.name.find("no write") != std::string::npos)
@@ -329,6 +385,8 @@ int tx_main(uint64_t n, int rounds)
     TXV(32, 3, true, WM_LINE_SC1, 0u, "128B line sc1")
     TXV(32, 3, true, WM_CHUNK_SC1, 0u, "16B chunks sc1")
     TXV(32, 3, true, WM_SECTOR_SC01, 0u, "64B sector sc0 sc1")
+    TXV(32, 3, true, WM_LINE_NT, 0u, "128B line nt")
+    TXV(32, 3, true, WM_LINE, 0u, "128B line plain")
     TXV(16, 6, true, WM_SECTOR_SC1, 0u, "64B sector sc1")
     TXV(64, 2, true, WM_SECTOR_SC1, 0u, "64B sector sc1")
     TXV(8, 12, true, WM_SECTOR_SC1, 0u, "64B sector sc1")
@@ -346,6 +404,26 @@ int tx_main(uint64_t n, int rounds)
     STEPV(WM_SECTOR, "64B sector plain")
     STEPV(WM_SECTOR_SC01, "64B sector sc0 sc1")
     STEPV(WM_SECTOR_NT, "64B sector nt")
+    STEPV(WM_LINE_NT, "128B line nt")
+    STEPV(WM_LINE, "128B line plain")
+    // TX and RX batches on two streams at once (independent batches)
+    hipStream_t s2;
+    hipEvent_t ev_fork, ev_join;
+    CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    CK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+    CK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+    vs.push_back({"step TX || RX on two streams (shipped kernels)", cbytes + vbytes, [&](hipStream_t st) {
+        CK(hipEventRecord(ev_fork, st));
+        CK(hipStreamWaitEvent(s2, ev_fork, 0));
+        CK(launch_verify_fixed(rx, stride, L, (u32)n, v1, 0u, s2));
+        CK(launch_compute_fixed(tx, stride, L, (u32)n, nullptr, nullptr, 0u, st));
+        CK(hipEventRecord(ev_join, s2));
+        CK(hipStreamWaitEvent(st, ev_join, 0));
+    }});
+    vs.push_back({"step TX then RX, one stream (shipped kernels)", cbytes + vbytes, [&](hipStream_t st) {
+        CK(launch_compute_fixed(tx, stride, L, (u32)n, nullptr, nullptr, 0u, st));
+        CK(launch_verify_fixed(rx, stride, L, (u32)n, v1, 0u, st));
+    }});
     vs.push_back({"step RX then TX (sector sc1)", cbytes + vbytes, [&](hipStream_t st) {
         hipLaunchKernelGGL((k_fixed<32, 3, false, false, true, WM_SECTOR_SC1, true>),
                            dim3((n + 7) / 8), dim3(256), 0, st, rx, stride, L, (u32)n, v1,
@@ -554,13 +632,12 @@ int copy_main(uint64_t n, int rounds)
                             nullptr, 0u, st_));
     }});
 #define CF2(G_, U_, O_)                                                                      \
-    vs.push_back({"fused copy + fill2 <" #G_ "," #U_ "> occ " #O_, bytes, [&](hipStream_t st_) { \
-        hipLaunchKernelGGL((k_copy_fill2<G_, U_, O_>), dim3((n + 256 / G_ - 1) / (256 / G_)),  \
+    vs.push_back({"fused copy + fill <" #G_ "," #U_ "> occ " #O_, bytes, [&](hipStream_t st_) { \
+        hipLaunchKernelGGL((k_copy_fill<G_, U_, O_>), dim3((n + 256 / G_ - 1) / (256 / G_)),  \
                            dim3(256), 0, st_, tx, n * stride, off, lens, src, n * plen + 64, soff, \
                            (u32)n, st, nullptr, 0u);                                           \
     }});
-    CF2(32, 3, 6) CF2(32, 3, 7) CF2(16, 6, 1) CF2(16, 6, 5) CF2(16, 6, 6) CF2(32, 4, 1)
-    CF2(32, 4, 5) CF2(16, 7, 1)
+    CF2(32, 3, 6) CF2(16, 6, 1) CF2(16, 6, 4) CF2(32, 3, 5)
     uint8_t *asrc, *cdst;                     // copy ceilings write cdst, never tx
     CK(hipMalloc(&asrc, n * stride));
     CK(hipMalloc(&cdst, n * stride));
@@ -577,14 +654,6 @@ int copy_main(uint64_t n, int rounds)
     vs.push_back({"  copy frames G=128 U=1 (2 waves/frame), 1434", cpb, [&](hipStream_t st_) {
         hipLaunchKernelGGL((k_copy_frames<false, 128, 1>), dim3((n + 1) / 2), dim3(256), 0, st_,
                            cdst, src, (uint64_t)plen, (u32)n);
-    }});
-    vs.push_back({"fused copy + fill <64,2>", bytes, [&](hipStream_t st_) {
-        hipLaunchKernelGGL((k_copy_fill<64, 2, 1>), dim3((n + 3) / 4), dim3(256), 0, st_, tx,
-                           n * stride, off, lens, src, n * plen + 64, soff, (u32)n, st, nullptr, 0u);
-    }});
-    vs.push_back({"fused copy + fill <64,2> occ 8", bytes, [&](hipStream_t st_) {
-        hipLaunchKernelGGL((k_copy_fill<64, 2, 8>), dim3((n + 3) / 4), dim3(256), 0, st_, tx,
-                           n * stride, off, lens, src, n * plen + 64, soff, (u32)n, st, nullptr, 0u);
     }});
     vs.push_back({"  copy frames, src stride 1536 (aligned)", cpb, [&](hipStream_t st_) {
         hipLaunchKernelGGL((k_copy_frames<false>), dim3((n + 7) / 8), dim3(256), 0, st_, cdst, asrc,
@@ -606,12 +675,6 @@ int copy_main(uint64_t n, int rounds)
                   [&](hipStream_t st_) {
         CK(hipMemcpyAsync(cdst, asrc, n * stride, hipMemcpyDeviceToDevice, st_));
     }});
-#define CFO(O_)                                                                              \
-    vs.push_back({"fused copy + fill, occupancy " #O_, bytes, [&](hipStream_t st_) {          \
-        hipLaunchKernelGGL((k_copy_fill<32, 3, O_>), dim3((n + 7) / 8), dim3(256), 0, st_, tx,  \
-                           n * stride, off, lens, src, n * plen + 64, soff, (u32)n, st, nullptr, 0u); \
-    }});
-    CFO(6) CFO(8)
     vs.push_back({"hipMemcpy2DAsync payloads + fill", bytes, [&](hipStream_t st_) {
         CK(hipMemcpy2DAsync(tx + hl, stride, src, plen, plen, n, hipMemcpyDeviceToDevice, st_));
         CK(launch_compute_desc(tx, n * stride, off, lens, (u32)n, st, nullptr, 0u, st_));
@@ -720,12 +783,6 @@ int lro_main(uint64_t n, int rounds)
                            off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd);  \
     }});
     GROO(2, 64, 6)
-#define GRO2(U_, W_, O_)                                                                     \
-    vs.push_back({"k_gro2<" #U_ "," #W_ "," #O_ "> (window 64, max 16384)", bytes, [&](hipStream_t st) { \
-        hipLaunchKernelGGL((k_gro2<U_, W_, O_>), dim3((n + 63) / 64), dim3(256), 0, st, in, n * stride, \
-                           off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd);  \
-    }});
-    GRO2(2, 64, 6) GRO2(2, 64, 8) GRO2(3, 64, 1) GRO2(3, 64, 6) GRO2(4, 64, 1) GRO2(4, 64, 5)
     vs.push_back({"verify (launch_verify_desc) for scale", (double)n * (L + 1), [&](hipStream_t st) {
         CK(launch_verify_desc(in, n * stride, off, lens, (u32)n, vd, 0u, st));
     }});
