@@ -404,8 +404,33 @@ int tx_main(uint64_t n, int rounds)
     STEPV(WM_SECTOR, "64B sector plain")
     STEPV(WM_SECTOR_SC01, "64B sector sc0 sc1")
     STEPV(WM_SECTOR_NT, "64B sector nt")
-    STEPV(WM_LINE_NT, "128B line nt")
-    STEPV(WM_LINE, "128B line plain")
+    // large batches: one launch vs launches of <= 1M frames with line write-back
+#define SPLITV(PER_, WM_, TAG)                                                               \
+    vs.push_back({std::string("compute <32,3> in launches of ") + #PER_ + " frames, " + TAG, cbytes, \
+                  [&](hipStream_t st) {                                                      \
+        for (uint64_t f0 = 0; f0 < n; f0 += PER_) {                                          \
+            const uint64_t m = std::min<uint64_t>(PER_, n - f0);                             \
+            hipLaunchKernelGGL((k_fixed<32, 3, true, false, true, WM_, true>), dim3((m + 7) / 8), \
+                               dim3(256), 0, st, tx + f0 * stride, stride, L, (u32)m, nullptr, \
+                               nullptr, 0u);                                                 \
+        }                                                                                    \
+    }});
+    SPLITV(1048576, WM_LINE_SC1, "128B line sc1")
+    SPLITV(524288, WM_LINE_SC1, "128B line sc1")
+    SPLITV(1048576, WM_SECTOR_SC1, "64B sector sc1")
+    vs.push_back({"step TX+RX shipped launchers", cbytes + vbytes, [&](hipStream_t st) {
+        CK(launch_compute_fixed(tx, stride, L, (u32)n, nullptr, nullptr, 0u, st));
+        CK(launch_verify_fixed(rx, stride, L, (u32)n, v1, 0u, st));
+    }});
+    vs.push_back({"step TX in 1M line launches + RX", cbytes + vbytes, [&](hipStream_t st) {
+        for (uint64_t f0 = 0; f0 < n; f0 += 1048576) {
+            const uint64_t m = std::min<uint64_t>(1048576, n - f0);
+            hipLaunchKernelGGL((k_fixed<32, 3, true, false, true, WM_LINE_SC1, true>), dim3((m + 7) / 8),
+                               dim3(256), 0, st, tx + f0 * stride, stride, L, (u32)m, nullptr,
+                               nullptr, 0u);
+        }
+        CK(launch_verify_fixed(rx, stride, L, (u32)n, v1, 0u, st));
+    }});
     // TX and RX batches on two streams at once (independent batches)
     hipStream_t s2;
     hipEvent_t ev_fork, ev_join;
