@@ -338,6 +338,23 @@ def _launch_ms(torch, fn, reps=20, warm=3):
     return e0.elapsed_time(e1) / reps
 
 
+def c2_max_frame(ctx, torch, n=1 << 20, L=1514):
+    """C2 at mTCP's largest frame (1500 B of IP MTU + 14 B Ethernet header,
+    SURVEY §8d): same stride 1536, TX fill and RX verify per launch."""
+    from mtcp_amd import synth
+    stream = torch.cuda.current_stream().cuda_stream
+    buf, stride = synth.fixed_frames_device(n, L, stride=1536, seed=0x5EA)
+    v = torch.empty(n, dtype=torch.uint8, device="cuda")
+    cms = _launch_ms(torch, lambda: ctx.compute_fixed(buf, stride, L, n, stream=stream))
+    vms = _launch_ms(torch, lambda: ctx.verify_fixed(buf, stride, L, n, v, stream=stream))
+    assert int((v != 0).sum()) == 0
+    return {"workload": f"{n} x {L}B frames, stride {stride}, TX fill and RX verify per launch",
+            "compute_ms": cms, "verify_ms": vms,
+            "step_gpkt_per_s": 2 * n / (cms + vms) / 1e6,
+            "compute_frac_peak": n * (L + 4) / (cms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "verify_frac_peak": n * (L + 1) / (vms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+
+
 def c3_imix(ctx, torch, n=4 << 20):
     """C3 side measurement: 4M IMIX frames (64/576/1500 at 7:4:1, pslib 64 B
     packing), descriptor batch in HBM, TX fill and RX verify per launch."""
@@ -647,6 +664,8 @@ def main():
             torch.cuda.empty_cache()
             line["c1_64B"] = c1_small_frames(ctx, torch)
             line["c1_64B_8M"] = c1_small_frames(ctx, torch, n=8 << 20)
+            line["c2_1514B"] = c2_max_frame(ctx, torch)
+            torch.cuda.empty_cache()
             line["c3_imix"] = c3_imix(ctx, torch)
             torch.cuda.empty_cache()
             line["rows_8f"] = rows_8f(ctx, torch)
