@@ -479,3 +479,57 @@ def test_c4_shard_properties(torch_dev, ctx, O):
     ctx.sync()
     got = t.nonzero(v).flatten().cpu().numpy()
     np.testing.assert_array_equal(got, bad)
+
+
+def test_c3_imix_full_size(torch_dev, ctx, O):
+    """C3 at its BASELINE size, 4M IMIX frames packed at 64 B (1.5 GB generated
+    in HBM as bench.py does), through the descriptor kernel: the fill's status
+    is OK everywhere and verify then accepts all; a fill is idempotent; 4,096
+    sampled frames match the oracle bit for bit (checks and whole filled
+    frames); seeded corruptions are exactly the drops."""
+    t = torch_dev
+    n = 4 << 20
+    lens = synth.imix_lengths(n, seed=0xC3)
+    d, doff, dlen, total = synth.packed_frames_device(lens, seed=0xC3)
+    off = doff.cpu().numpy().view(np.uint64)
+    idx = np.sort(np.random.default_rng(3).choice(n, 4096, replace=False))
+    # the sampled frames, unfilled, repacked for the oracle
+    s_len = lens[idx]
+    s_off, s_total = synth.packed_offsets(s_len)
+    sample = np.zeros(s_total + 64, dtype=np.uint8)
+    host_all = d.cpu().numpy()
+    for k, i in enumerate(idx):
+        sample[int(s_off[k]):int(s_off[k]) + int(s_len[k])] = \
+            host_all[int(off[i]):int(off[i]) + int(s_len[k])]
+    del host_all
+    st = t.zeros(n, dtype=t.uint8, device="cuda")
+    cs = t.zeros(n, dtype=t.int32, device="cuda")
+    ctx.compute(d, doff, dlen, n, st, cs)
+    v = t.zeros(n, dtype=t.uint8, device="cuda")
+    ctx.verify(d, doff, dlen, n, v)
+    ctx.sync()
+    assert int((st != 0).sum()) == 0 and int((v != 0).sum()) == 0
+    ref = sample.copy()
+    rst, rcs = O.compute_batch(ref, s_off, s_len)
+    assert (rst == 0).all()
+    np.testing.assert_array_equal(host(cs).view(np.uint32)[idx], rcs)
+    filled = d.cpu().numpy()
+    for k, i in enumerate(idx):
+        np.testing.assert_array_equal(filled[int(off[i]):int(off[i]) + int(s_len[k])],
+                                      ref[int(s_off[k]):int(s_off[k]) + int(s_len[k])])
+    before = d.clone()
+    ctx.compute(d, doff, dlen, n)                                      # idempotent
+    ctx.sync()
+    assert t.equal(d, before)
+    del before
+    # corruptions: one byte in [14, len) of every 997th frame plus a seeded set
+    rng = np.random.default_rng(33)
+    bad = np.unique(np.concatenate([np.arange(5, n, 997), rng.choice(n, 3000, replace=False)]))
+    pos = (rng.random(len(bad)) * (lens[bad].astype(np.int64) - 14)).astype(np.int64) + 14
+    flip = rng.integers(1, 256, len(bad))
+    flat = t.from_numpy(off[bad].astype(np.int64) + pos).cuda()
+    d[flat] ^= t.from_numpy(flip.astype(np.uint8)).cuda()
+    ctx.verify(d, doff, dlen, n, v)
+    ctx.sync()
+    got = t.nonzero(v).flatten().cpu().numpy()
+    np.testing.assert_array_equal(got, bad)
