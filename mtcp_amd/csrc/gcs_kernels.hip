@@ -397,8 +397,9 @@ hipError_t launch_burst_server(ServerMailbox* mb, uint32_t done_seq, uint64_t id
 // keeps K = 1 (profiles/r02/kbench_imix_K.log; other class shapes:
 // kbench_imix_shapes2.log).
 template <int G0_, int U0_, int G1_, int U1_, int G2_, int U2_, int WM_ = kWM, int F_ = kBlock,
-          bool ORDERED_ = true, int K0_ = 1, int K1_ = 1, bool STAGE_ = false>
+          bool ORDERED_ = true, int K0_ = 1, int K1_ = 1, bool STAGE_ = false, bool NT_ = kNT>
 struct DescShape {
+    static constexpr bool NT = NT_;
     static constexpr int G0 = G0_, U0 = U0_, G1 = G1_, U1 = U1_, G2 = G2_, U2 = U2_, WM = WM_;
     static constexpr int F = F_;
     static constexpr bool ORDERED = ORDERED_;
@@ -412,12 +413,14 @@ struct DescShape {
 // stages each frame's sector 0 in LDS and stores the block's sectors together
 // at its end, in frame order, non-temporal: 4M IMIX 390 -> 377-379 us (in the
 // epilogues: sc1 390, nt 411; staged: sc1 409, sc0 sc1 410;
-// profiles/r02/kbench_imix_stage*.log).
+// profiles/r02/kbench_imix_stage*.log).  The fill loads its frames with the
+// default (temporal) policy, 377-379 -> 371-373 us; the verify keeps NT loads
+// (temporal: 319-320 vs 276-279 us; kbench_imix_temporal*.log).
 template <bool COMPUTE>
 using DescShip = DescShape<4, 1, 16, 3, 32, 3, COMPUTE ? WM_SECTOR_NT : kWM, kBlock, true, 1, 1,
-                           COMPUTE>;
+                           COMPUTE, !COMPUTE>;
 
-template <int G, int U, bool COMPUTE, bool LOOP, bool EXT, int WM, int K = 1>
+template <int G, int U, bool COMPUTE, bool LOOP, bool EXT, int WM, int K = 1, bool NT = kNT>
 __device__ __forceinline__ void desc_class(uint8_t* __restrict__ frames, uint64_t frames_bytes,
                                            const uint64_t* soff, const uint16_t* slen,
                                            const uint16_t* list, int count, u32 flags,
@@ -444,7 +447,7 @@ __device__ __forceinline__ void desc_class(uint8_t* __restrict__ frames, uint64_
             tk[k] = active ? t : -1;
             const uint64_t o = soff[t];                  // LDS: no dependent global load
             const int nch = active ? (int)((slen[t] + 15u) >> 4) : 0;
-            load_first<G, U, true, kNT>(frames + o, nch, (int64_t)(frames_bytes - o), sub, v[k]);
+            load_first<G, U, true, NT>(frames + o, nch, (int64_t)(frames_bytes - o), sub, v[k]);
         }
 #pragma unroll
         for (int k = 0; k < K; k++) {
@@ -452,7 +455,7 @@ __device__ __forceinline__ void desc_class(uint8_t* __restrict__ frames, uint64_
             const int t = active ? tk[k] : list[0];
             const uint64_t o = soff[t];                  // descriptor validated in phase 0
             uint8_t* f = frames + o;
-            frame_body<G, U, COMPUTE, LOOP, true, kNT, WM, EXT>(
+            frame_body<G, U, COMPUTE, LOOP, true, NT, WM, EXT>(
                 v[k], f, f, slen[t], (int64_t)(frames_bytes - o), true, sub, flags, codes + t,
                 COMPUTE ? csums + t : nullptr, active, xframe_of(t),
                 stage ? reinterpret_cast<uint8_t*>(stage + 4 * t) : nullptr);
@@ -541,9 +544,9 @@ __device__ __forceinline__ void desc_mixed(uint8_t* __restrict__ frames, uint64_
         uint32_t* hl = EXT && !COMPUTE ? hashes : nullptr;
         uint16_t* ql = EXT && !COMPUTE ? queues : nullptr;
         uint4* stg = COMPUTE && S::STAGE ? stage : nullptr;
-        if (n0) desc_class<S::G0, S::U0, COMPUTE, false, EXT, S::WM, S::K0>(frames, frames_bytes, soff, slen, list[0], n0, flags, codes, csums, ext, hl, ql, stg);
-        if (n1) desc_class<S::G1, S::U1, COMPUTE, false, EXT, S::WM, S::K1>(frames, frames_bytes, soff, slen, list[1], n1, flags, codes, csums, ext, hl, ql, stg);
-        if (n2) desc_class<S::G2, S::U2, COMPUTE, true, EXT, S::WM>(frames, frames_bytes, soff, slen, list[2], n2, flags, codes, csums, ext, hl, ql, stg);
+        if (n0) desc_class<S::G0, S::U0, COMPUTE, false, EXT, S::WM, S::K0, S::NT>(frames, frames_bytes, soff, slen, list[0], n0, flags, codes, csums, ext, hl, ql, stg);
+        if (n1) desc_class<S::G1, S::U1, COMPUTE, false, EXT, S::WM, S::K1, S::NT>(frames, frames_bytes, soff, slen, list[1], n1, flags, codes, csums, ext, hl, ql, stg);
+        if (n2) desc_class<S::G2, S::U2, COMPUTE, true, EXT, S::WM, 1, S::NT>(frames, frames_bytes, soff, slen, list[2], n2, flags, codes, csums, ext, hl, ql, stg);
     }
     __syncthreads();
     if (COMPUTE && S::STAGE && !(flags & GCS_CF_NO_INPLACE)) {

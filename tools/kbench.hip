@@ -224,6 +224,11 @@ int imix_main(uint64_t n, int rounds)
     MIXED(true, 6, "6 epilogue sectors sc1 (round 1)", 4, 1, 16, 3, 32, 3)
     MIXED(true, 6, "6 STAGE nt (shipped)", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true)
     MIXED(true, 6, "6 no write-back", 4, 1, 16, 3, 32, 3)
+    // temporal frame loads: a 128 B line split between frames of two classes
+    // (64 B packing) may stay in L2 for the second pass
+    MIXED(false, 6, "6 verify NT loads (shipped)", 4, 1, 16, 3, 32, 3)
+    MIXED(false, 6, "6 verify temporal loads", 4, 1, 16, 3, 32, 3, kWM, 256, true, 1, 1, false, false)
+    MIXED(true, 6, "6 STAGE nt, temporal loads", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true, false)
     vs.push_back({"verify  desc (launch_verify_desc)", vb, [&](hipStream_t st) {
         CK(launch_verify_desc(rx, total, doff, dlen, (u32)n, v1, 0u, st));
     }});
