@@ -1,6 +1,6 @@
 /*
- * asan_driver.c -- host-side AddressSanitizer run of libmtcp_gpucsum's host
- * code (TEST ONLY; tests/plugin/Makefile target `asan`, run on the GPU box by
+ * asan_driver.c -- host-side sanitizer run (ASan + UBSan, or TSan) of the host
+ * code (TEST ONLY; built by tests/plugin/Makefile.asan, run on the GPU box by
  * tests/test_host_asan.py).  GPU-side sanitizers are not available on this
  * pool, so the device code runs uninstrumented; everything the host does --
  * gcs_api.cpp's staging slots, gather pool and burst server, the plugin
@@ -14,7 +14,7 @@
  *   4  the plugin decorating the synthetic NIC module under mini_mtcp's RX and
  *      TX loops, against the bare module (software folds)
  *   5  argument errors come back as status codes
- * Prints one line per part and "ASAN DRIVER OK" at the end; exits non-zero on
+ * Prints one line per part and "HOST DRIVER OK" at the end; exits non-zero on
  * a mismatch (ASan aborts on its own on a memory error).
  */
 #include <stdint.h>
@@ -323,9 +323,9 @@ int main(void)
 	part_plugin();
 	part_errors();
 	if (g_fail) {
-		printf("ASAN DRIVER FAILED\n");
+		printf("HOST DRIVER FAILED\n");
 		return 1;
 	}
-	printf("ASAN DRIVER OK\n");
+	printf("HOST DRIVER OK\n");
 	return 0;
 }
