@@ -463,6 +463,56 @@ __device__ __forceinline__ void desc_class(uint8_t* __restrict__ frames, uint64_
     }
 }
 
+// End of a descriptor block: the staged sector-0 write-backs, then the block's
+// per-frame outputs from LDS as coalesced stores.
+template <class S, bool COMPUTE, bool EXT>
+__device__ __forceinline__ void desc_tail(uint8_t* __restrict__ frames, uint64_t frames_bytes,
+                                          uint64_t f0, u32 n, const uint64_t* soff,
+                                          const uint16_t* slen, const uint8_t* codes,
+                                          const uint32_t* csums, const uint32_t* hashes,
+                                          const uint16_t* queues, const uint4* stage,
+                                          uint8_t* __restrict__ out_code,
+                                          uint32_t* __restrict__ out_csum, u32 flags,
+                                          const Ext& ext)
+{
+    constexpr int F = S::F;
+    const int t = threadIdx.x;
+    const uint64_t i = f0 + t;
+    if (COMPUTE && S::STAGE && !(flags & GCS_CF_NO_INPLACE)) {
+        // STAGE: the frames' sector-0 write-backs leave together, in frame
+        // order, 16 B per lane: four lanes per sector, so adjacent sectors
+        // (two packed 64 B frames) are one whole 128 B line of one store
+        // instruction.  A chunk goes out under exactly the epilogue's
+        // conditions: a status that fills, inside the frame and the buffer.
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int q = r * kBlock + t, ft = q >> 2, c = q & 3;
+            if (ft >= F || f0 + ft >= n)
+                continue;
+            const u32 st = codes[ft];
+            const bool wip = st == GCS_TX_OK || st == GCS_TX_IP_ONLY || st == GCS_TX_BAD_TCPLEN ||
+                             (EXT && (st == GCS_TX_ICMP_OK || st == GCS_TX_BAD_ICMPLEN));
+            if (!wip || 16 * c >= (int)slen[ft])
+                continue;
+            const uint64_t o = soff[ft] + 16 * c;
+            if (o + 16 <= frames_bytes)
+                stg16<S::WM>(frames + o, stage[q]);
+        }
+    }
+    if (t < F && i < n) {
+        if (out_code)
+            out_code[i] = codes[t];
+        if (COMPUTE && out_csum)
+            out_csum[i] = csums[t];
+        if (EXT && !COMPUTE) {
+            if (ext.hash)
+                ext.hash[i] = hashes[t];
+            if (ext.queue)
+                ext.queue[i] = queues[t];
+        }
+    }
+}
+
 template <class S, bool COMPUTE, bool XCD, bool EXT>
 __device__ __forceinline__ void desc_mixed(uint8_t* __restrict__ frames, uint64_t frames_bytes,
                                            const uint64_t* __restrict__ off,
@@ -549,39 +599,8 @@ __device__ __forceinline__ void desc_mixed(uint8_t* __restrict__ frames, uint64_
         if (n2) desc_class<S::G2, S::U2, COMPUTE, true, EXT, S::WM, 1, S::NT>(frames, frames_bytes, soff, slen, list[2], n2, flags, codes, csums, ext, hl, ql, stg);
     }
     __syncthreads();
-    if (COMPUTE && S::STAGE && !(flags & GCS_CF_NO_INPLACE)) {
-        // STAGE: the frames' sector-0 write-backs leave together, in frame
-        // order, 16 B per lane: four lanes per sector, so adjacent sectors
-        // (two packed 64 B frames) are one whole 128 B line of one store
-        // instruction.  A chunk goes out under exactly the epilogue's
-        // conditions: a status that fills, inside the frame and the buffer.
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int q = r * kBlock + t, ft = q >> 2, c = q & 3;
-            if (ft >= F || f0 + ft >= n)
-                continue;
-            const u32 st = codes[ft];
-            const bool wip = st == GCS_TX_OK || st == GCS_TX_IP_ONLY || st == GCS_TX_BAD_TCPLEN ||
-                             (EXT && (st == GCS_TX_ICMP_OK || st == GCS_TX_BAD_ICMPLEN));
-            if (!wip || 16 * c >= (int)slen[ft])
-                continue;
-            const uint64_t o = soff[ft] + 16 * c;
-            if (o + 16 <= frames_bytes)
-                stg16<S::WM>(frames + o, stage[q]);
-        }
-    }
-    if (t < F && i < n) {
-        if (out_code)
-            out_code[i] = codes[t];
-        if (COMPUTE && out_csum)
-            out_csum[i] = csums[t];
-        if (EXT && !COMPUTE) {
-            if (ext.hash)
-                ext.hash[i] = hashes[t];
-            if (ext.queue)
-                ext.queue[i] = queues[t];
-        }
-    }
+    desc_tail<S, COMPUTE, EXT>(frames, frames_bytes, f0, n, soff, slen, codes, csums, hashes, queues,
+                               stage, out_code, out_csum, flags, ext);
 }
 
 template <class S, bool COMPUTE, bool XCD, int OCC = 1>

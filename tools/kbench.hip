@@ -162,6 +162,502 @@ __global__ void __launch_bounds__(256) k_read_regions(const uint8_t* __restrict_
     if (acc == 0x9E3779B9u) out[0] = acc;
 }
 
+// ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
+// One global_load_lds_dwordx4: lane l's 16 B from src land at LDS byte
+// lds_dst + 16*l (lds_dst wave-uniform).  M0 is written and restored inside
+// the statement (cdna_hip_programming.md §5.7: the LDS-DMA recipe).
+template <bool NT>
+__device__ __forceinline__ void glds16(const uint8_t* src, u32 lds_dst)
+{
+    u32 keep;
+    if constexpr (NT)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                     "global_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(src), "s"(lds_dst) : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                     "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(src), "s"(lds_dst) : "memory");
+}
+
+// s_waitcnt vmcnt(N) alone (gfx9 encoding: vmcnt in [3:0] and [15:14]).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt()
+{
+    static_assert(N >= 0 && N < 64, "vmcnt");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+    asm volatile("" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------
+// MEASURED, NOT SHIPPED ("IMIX one frame per lane").
+// Descriptor batches, one frame per lane out of LDS (C3 IMIX).  A one-wave
+// block takes F consecutive descriptors.  When their frames lie within CAP
+// bytes [A, B16) of the buffer (packed batches: pslib.c:132-156), the wave
+// moves that region into LDS with LDS-DMA (global_load_lds_dwordx4, 1 KiB per
+// instruction, every byte read once and coalesced), then each lane folds ONE
+// whole frame out of LDS: no group reductions, no header broadcasts, so the
+// fold costs a few instructions per 16 B chunk instead of the group kernels'
+// per-frame fixed cost, which bounds the list kernel on small frames.  Chunks
+// 0..5 (every header byte of any ihl) are read first and go through the exact
+// masks and the shared TX/RX epilogue; later chunks are summed in a per-lane
+// rotated order so that lanes whose frames sit at equal offsets mod 256 B do
+// not read the same LDS banks together.  A TX fill patches sector 0 of its
+// frame inside the LDS region, and the wave stores the F sectors in frame
+// order at the end (four lanes per sector, nt), as the staged list kernel
+// does.  Blocks whose frames do not fit (sparse or unordered descriptors) fold
+// each lane's frame from global memory instead (correct, slower).
+template <int F_, int CAP_, bool LNT_, int WM_>
+struct LaneShape {
+    static constexpr int F = F_;          // frames per block (<= 64: one wave)
+    static constexpr int CAP = CAP_;      // LDS region bytes
+    static constexpr bool LNT = LNT_;     // non-temporal region loads
+    static constexpr int WM = WM_;        // TX write-back mode
+    static_assert(F <= 64 && CAP % 1024 == 0, "one wave; whole DMA instructions");
+};
+
+// Chunks >= 6 of a frame: the TCP segment's interior, or its tail at te
+// (ts <= 74 < 96, so no header field lies here).
+__device__ __forceinline__ void accum_body(uint4 v, int cb, int ts, int te, Acc& a)
+{
+    if (cb + 16 <= te) {
+        a.tcp = sad4(v, a.tcp);
+    } else if (cb < te) {
+        a.tcp = sad(v.x & region_mask(cb, ts, te), a.tcp);
+        a.tcp = sad(v.y & region_mask(cb + 4, ts, te), a.tcp);
+        a.tcp = sad(v.z & region_mask(cb + 8, ts, te), a.tcp);
+        a.tcp = sad(v.w & region_mask(cb + 12, ts, te), a.tcp);
+    }
+}
+
+template <class L, bool COMPUTE, bool EXT, bool FROM_LDS>
+__device__ __forceinline__ void lane_frame(const uint8_t* src, uint8_t* __restrict__ f, u32 len,
+                                           int64_t avail, bool active, u32 flags,
+                                           uint8_t* out_code, uint32_t* out_csum,
+                                           const XFrame& xf, uint8_t* stage)
+{
+    constexpr int H = 6;                               // header chunks (96 B)
+    const int nch = active ? (int)((len + 15) >> 4) : 0;
+    auto rd = [&](int c) -> uint4 {
+        if (FROM_LDS)
+            return *reinterpret_cast<const uint4*>(src + 16 * c);
+        return load_chunk<true, L::LNT>(f + 16 * c, avail - 16 * c);
+    };
+    uint4 v[H];
+#pragma unroll
+    for (int c = 0; c < H; c++)
+        v[c] = c < nch ? rd(c) : make_uint4(0, 0, 0, 0);
+    Hdr h;
+    h.d3 = v[0].w;
+    h.d4 = v[1].x;
+    h.d5 = v[1].y;
+    const int ts = 14 + 4 * (int)((h.d3 >> 16) & 15u);
+    const int te = 14 + (int)bswap16(h.d4 & 0xFFFFu);
+    Acc a = {0u, 0u, 0u};
+#pragma unroll
+    for (int c = 0; c < H; c++)
+        accum_chunk<COMPUTE>(v[c], 16 * c, ts, te, a);
+    const int rest = nch - H;
+    if (rest > 0) {
+        int idx = (int)(threadIdx.x & 63) % rest;      // rotated start
+        for (int j = 0; j < rest; j += 4) {
+            uint4 w[4];
+            int cb[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const bool ok = j + u < rest;
+                cb[u] = 16 * (H + idx);
+                w[u] = ok ? rd(H + idx) : make_uint4(0, 0, 0, 0);
+                if (!ok)
+                    cb[u] = 1 << 30;                   // beyond te: contributes nothing
+                idx = idx + 1 == rest ? 0 : idx + 1;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                accum_body(w[u], cb[u], ts, te, a);
+        }
+    }
+    epilogue<1, H, COMPUTE, L::WM, EXT>(h, a, f, len, avail, true, 0, flags, out_code,
+                                        COMPUTE ? out_csum : nullptr, active, v, xf, stage);
+}
+
+template <class L, bool COMPUTE, bool XCD, bool EXT>
+__device__ __forceinline__ void desc_lane(uint8_t* __restrict__ frames, uint64_t frames_bytes,
+                                          const uint64_t* __restrict__ off,
+                                          const uint16_t* __restrict__ lens, u32 n,
+                                          uint8_t* __restrict__ out_code,
+                                          uint32_t* __restrict__ out_csum, u32 flags,
+                                          const Ext& ext)
+{
+    constexpr int F = L::F;
+    __shared__ __attribute__((aligned(16))) uint8_t region[L::CAP];
+    __shared__ uint8_t codes[F];
+    __shared__ uint32_t ro_s[F];
+    __shared__ uint16_t len_s[F];
+    const uint32_t blk = XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint64_t f0 = (uint64_t)blk * F;
+    const int lane = threadIdx.x;
+    const uint64_t i = f0 + lane;
+    const bool in = lane < F && i < n;
+    uint64_t o = 0;
+    u32 len = 0;
+    bool ok = false;
+    if (in) {
+        o = off[i];
+        len = lens[i];
+        ok = (o & 15) == 0 && o <= frames_bytes && len <= frames_bytes - o;
+    }
+    // the block's region: [min off, max end) over its valid frames
+    uint64_t lo = ok ? o : ~0ull, hi = ok ? ((o + len + 15) & ~15ull) : 0ull;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t l2 = __shfl_xor(lo, d, 64), h2 = __shfl_xor(hi, d, 64);
+        lo = l2 < lo ? l2 : lo;
+        hi = h2 > hi ? h2 : hi;
+    }
+    const bool lds = hi > lo && hi - lo <= (uint64_t)L::CAP && hi <= frames_bytes;
+    XFrame xf{};
+    if constexpr (EXT)
+        xf = XFrame{{ext.key[0], ext.key[1], ext.key[2], ext.key[3]},
+                    ext.hash && in ? ext.hash + i : nullptr, ext.queue && in ? ext.queue + i : nullptr,
+                    ext.nq, ext.nq_magic, ext.endian, nullptr};
+    uint8_t* code_p = codes + lane;
+    uint32_t csum = 0;
+    if (in && !ok) {
+        codes[lane] = COMPUTE ? GCS_TX_BAD_DESC : GCS_V_BAD_DESC;
+        if (EXT && !COMPUTE) {
+            if (xf.hash) *xf.hash = 0;
+            if (xf.queue) *xf.queue = 0xFFFF;
+        }
+    }
+    if (lds) {
+        // LDS-DMA of [lo, hi): 1 KiB per instruction; sources past hi clamped
+        // to its last chunk (hi <= frames_bytes)
+        const u32 base = (u32)(uintptr_t)region;
+        const int nins = (int)((hi - lo + 1023) >> 10);
+        for (int q = 0; q < nins; q++) {
+            const uint64_t g = lo + 1024ull * q + 16ull * lane;
+            glds16<L::LNT>(frames + (g < hi ? g : hi - 16),
+                           __builtin_amdgcn_readfirstlane(base + 1024u * (u32)q));
+        }
+        wait_vmcnt<0>();
+        const u32 ro = (u32)(o - lo);
+        ro_s[lane] = ro;
+        len_s[lane] = (uint16_t)len;
+        lane_frame<L, COMPUTE, EXT, true>(region + ro, frames + o, len,
+                                          (int64_t)(frames_bytes - o), ok, flags, code_p, &csum,
+                                          xf, COMPUTE ? region + ro : nullptr);
+        if (COMPUTE && !(flags & GCS_CF_NO_INPLACE)) {
+            // sector 0 of every frame from the LDS region, in frame order:
+            // four lanes per sector, so two packed 64 B frames are one line
+#pragma unroll
+            for (int r = 0; r < 4 * F / 64; r++) {
+                const int q = r * 64 + lane, ft = q >> 2, c = q & 3;
+                if (f0 + ft >= n)
+                    continue;
+                const u32 st = codes[ft];
+                const bool wip = st == GCS_TX_OK || st == GCS_TX_IP_ONLY ||
+                                 st == GCS_TX_BAD_TCPLEN ||
+                                 (EXT && (st == GCS_TX_ICMP_OK || st == GCS_TX_BAD_ICMPLEN));
+                if (!wip || 16 * c >= (int)len_s[ft])
+                    continue;
+                const u32 rc = ro_s[ft] + 16 * c;
+                stg16<L::WM>(frames + lo + rc, *reinterpret_cast<const uint4*>(region + rc));
+            }
+        }
+    } else {
+        lane_frame<L, COMPUTE, EXT, false>(nullptr, frames + o, len, (int64_t)(frames_bytes - o),
+                                           ok, flags, code_p, &csum, xf, nullptr);
+    }
+    if (in) {
+        if (out_code)
+            out_code[i] = codes[lane];
+        if (COMPUTE && out_csum)
+            out_csum[i] = ok ? csum : 0u;
+    }
+}
+
+template <class L, bool COMPUTE, bool XCD, int OCC = 1>
+__global__ void __launch_bounds__(64, OCC)
+k_desc_lane(uint8_t* __restrict__ frames, uint64_t frames_bytes,
+            const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens, u32 n,
+            uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags)
+{
+    desc_lane<L, COMPUTE, XCD, false>(frames, frames_bytes, off, lens, n, out_code, out_csum,
+                                      flags, Ext{});
+}
+
+template <class L, bool COMPUTE, bool XCD, int OCC = 1>
+__global__ void __launch_bounds__(64, OCC)
+k_desc_lane_x(uint8_t* __restrict__ frames, uint64_t frames_bytes,
+              const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens, u32 n,
+              uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags, Ext ext)
+{
+    desc_lane<L, COMPUTE, XCD, true>(frames, frames_bytes, off, lens, n, out_code, out_csum,
+                                     flags, ext);
+}
+
+// ---------------------------------------------------------------------------
+// MEASURED, NOT SHIPPED ("IMIX through an LDS ring").
+// Packed descriptor batches through an LDS ring (C3 IMIX; PSIO's chunk layout,
+// pslib.c:132-156, frames back to back in offset order).  The list kernel above
+// loads every frame with its own lane group, so a block's HBM reads come in
+// 12 dependent trips of 1-3 KiB per wave.  Here a block streams its frames'
+// region [A, B) instead, in windows of W bytes: every wave moves 1 KiB
+// contiguous per LDS-DMA instruction straight into an RS-slot LDS ring, NIF
+// windows ahead.  The frames are then folded out of the ring by the same
+// per-frame code (frame_body), in the same size classes, a frame at the window
+// where it ENDS: it starts at most one window earlier (len <= 1536 < W), so
+// windows k-1 and k hold it, while k+1..k+NIF are in flight.  Each
+// wave takes whole wave-trips (64/G frames of one class) of the window in turn,
+// so the four waves share a window's classes.  Blocks whose frames are not
+// packed in offset order, are longer than 1536 B, or span more than
+// kRingMaxWin windows take the list passes instead (block-uniform).
+constexpr int kRingMaxWin = 64;
+
+template <int W_, int NIF_, bool LNT_, int RS_ = 4, int PROBE_ = 0>
+struct RingShape {
+    static constexpr int PROBE = PROBE_;               // A/B only: 1 = no fold, 2 = no DMA
+    static constexpr int W = W_;                       // bytes per window (power of 2)
+    static constexpr int NIF = NIF_;                   // windows in flight (LDS-DMA)
+    static constexpr bool LNT = LNT_;                  // non-temporal window loads
+    static constexpr int RS = RS_;                     // ring slots (power of 2)
+    static constexpr int NL = W / (16 * kBlock);       // 16 B DMAs per thread per window
+    static_assert((W & (W - 1)) == 0 && NL >= 1 && W >= 2048, "window");
+    static_assert((RS & (RS - 1)) == 0 && RS >= NIF + 2, "slots: k-1, k, k+1..k+NIF");
+};
+
+template <class S, int G, int U, bool COMPUTE, bool EXT, int RB>
+__device__ __forceinline__ void ring_trip(uint8_t* __restrict__ frames, uint64_t frames_bytes,
+                                          uint64_t A, const uint4* ring, const uint64_t* soff,
+                                          const uint16_t* slen, const uint16_t* list, int start,
+                                          int end, u32 flags, uint8_t* codes, uint32_t* csums,
+                                          const Ext& ext, uint32_t* hashes, uint16_t* queues,
+                                          uint4* stage)
+{
+    const int lane = threadIdx.x & 63, g = lane / G, sub = lane & (G - 1);
+    const int idx = start + g;
+    const bool active = idx < end;
+    const int t = list[active ? idx : start];
+    const u32 ro = (u32)(soff[t] - A), len = slen[t];
+    const int nch = active ? (int)((len + 15) >> 4) : 0;
+    uint4 v[U];
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+        const int c = j * G + sub;
+        const u32 x = ro + 16u * (u32)c;               // window x/W sits in slot (x/W) % RS
+        v[j] = c < nch ? ring[(x & (u32)(RB - 1)) >> 4] : make_uint4(0, 0, 0, 0);
+    }
+    const XFrame xf = EXT ? XFrame{{ext.key[0], ext.key[1], ext.key[2], ext.key[3]},
+                                   hashes ? hashes + t : nullptr, queues ? queues + t : nullptr,
+                                   ext.nq, ext.nq_magic, ext.endian, nullptr}
+                          : XFrame{};
+    uint8_t* f = frames + A + ro;
+    frame_body<G, U, COMPUTE, false, true, true, S::WM, EXT>(
+        v, f, f, len, (int64_t)(frames_bytes - A - ro), true, sub, flags, codes + t,
+        COMPUTE ? csums + t : nullptr, active, xf,
+        stage ? reinterpret_cast<uint8_t*>(stage + 4 * t) : nullptr);
+}
+
+template <class S, class R, bool COMPUTE, bool XCD, bool EXT>
+__device__ __forceinline__ void desc_ring(uint8_t* __restrict__ frames, uint64_t frames_bytes,
+                                          const uint64_t* __restrict__ off,
+                                          const uint16_t* __restrict__ lens, u32 n,
+                                          uint8_t* __restrict__ out_code,
+                                          uint32_t* __restrict__ out_csum, u32 flags,
+                                          const Ext& ext)
+{
+    constexpr int F = kBlock, W = R::W, NL = R::NL, NIF = R::NIF, NW = kBlock / 64;
+    static_assert(((R::RS * W) & (R::RS * W - 1)) == 0, "ring bytes: power of 2");
+    static_assert(S::F == kBlock && S::ORDERED && S::K0 == 1 && S::K1 == 1, "ring shape");
+    __shared__ uint64_t soff[F];
+    __shared__ uint16_t slen[F];
+    __shared__ uint16_t list[3][F];
+    __shared__ int wcnt[3][NW];
+    __shared__ uint16_t pos[3][kRingMaxWin + 1];
+    __shared__ int ring_ok;
+    __shared__ uint8_t codes[F];
+    __shared__ uint32_t csums[COMPUTE ? F : 1];
+    __shared__ uint32_t hashes[EXT && !COMPUTE ? F : 1];
+    __shared__ uint16_t queues[EXT && !COMPUTE ? F : 1];
+    __shared__ uint4 stage[COMPUTE && S::STAGE ? 4 * F : 1];
+    __shared__ uint4 ring[R::RS * W / 16];
+    const uint32_t blk = XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint64_t f0 = (uint64_t)blk * F;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int nin = (int)min<uint64_t>(F, n - f0);     // frames of this block
+    if (t == 0)
+        ring_ok = 1;
+    // phase 0: validate and classify (as desc_mixed)
+    const uint64_t i = f0 + t;
+    int cls = -1;
+    if (t < nin) {
+        const uint64_t o = off[i];
+        const u32 len = lens[i];
+        const bool ok = (o & 15) == 0 && o <= frames_bytes && len <= frames_bytes - o;
+        if (!ok) {
+            codes[t] = COMPUTE ? GCS_TX_BAD_DESC : GCS_V_BAD_DESC;
+            if (COMPUTE)
+                csums[t] = 0;
+            if (EXT && !COMPUTE) {
+                hashes[t] = 0;
+                queues[t] = 0xFFFF;
+            }
+        } else {
+            soff[t] = o;
+            slen[t] = (uint16_t)len;
+            cls = len <= (u32)S::T0 ? 0 : (len <= (u32)S::T1 ? 1 : 2);
+        }
+    }
+    const uint64_t below = (1ull << lane) - 1;
+    uint64_t m[3];
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        m[c] = __ballot(cls == c);
+        if (lane == 0)
+            wcnt[c][w] = __popcll(m[c]);
+    }
+    __syncthreads();
+    // class lists in frame order; per-class counts before this frame
+    int cum[3], tot[3];
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        int base = 0, all = 0;
+#pragma unroll
+        for (int ww = 0; ww < NW; ww++) {
+            base += ww < w ? wcnt[c][ww] : 0;
+            all += wcnt[c][ww];
+        }
+        cum[c] = base + __popcll(m[c] & below);
+        tot[c] = all;
+    }
+    if (cls >= 0)
+        list[cls][cum[cls]] = (uint16_t)t;
+    // ring mode: every frame valid, <= 1536 B, packed in offset order
+    if (t < nin) {
+        bool rok = cls >= 0 && slen[t] <= (u32)(16 * S::G2 * S::U2);
+        if (rok && t > 0)
+            rok = soff[t - 1] + slen[t - 1] <= soff[t];
+        if (!rok)
+            ring_ok = 0;
+    }
+    __syncthreads();
+    const uint64_t A = soff[0] & ~15ull;
+    int nwin = 0;
+    if (ring_ok) {
+        // the window loads read whole chunks up to B16: it must lie in the buffer
+        const uint64_t B = soff[nin - 1] + slen[nin - 1];
+        const uint64_t span = (B - A + W - 1) / W;
+        if (((B + 15) & ~15ull) <= frames_bytes && B > A)
+            nwin = span > (uint64_t)kRingMaxWin ? 0 : (int)span;
+    }
+    if (nwin == 0) {
+        // the list passes over global memory
+        uint32_t* hl = EXT && !COMPUTE ? hashes : nullptr;
+        uint16_t* ql = EXT && !COMPUTE ? queues : nullptr;
+        uint4* stg = COMPUTE && S::STAGE ? stage : nullptr;
+        if (tot[0]) desc_class<S::G0, S::U0, COMPUTE, false, EXT, S::WM, 1, S::NT>(frames, frames_bytes, soff, slen, list[0], tot[0], flags, codes, csums, ext, hl, ql, stg);
+        if (tot[1]) desc_class<S::G1, S::U1, COMPUTE, false, EXT, S::WM, 1, S::NT>(frames, frames_bytes, soff, slen, list[1], tot[1], flags, codes, csums, ext, hl, ql, stg);
+        if (tot[2]) desc_class<S::G2, S::U2, COMPUTE, true, EXT, S::WM, 1, S::NT>(frames, frames_bytes, soff, slen, list[2], tot[2], flags, codes, csums, ext, hl, ql, stg);
+    } else {
+        // window of each frame = the window holding its last byte; pos[c][k] =
+        // class-c frames ending before window k (lists are in window order)
+        auto win_of = [&](int ft) {
+            const uint64_t e = soff[ft] + slen[ft];
+            const uint64_t last = e > soff[ft] ? e - 1 : soff[ft];
+            return (int)((last - A) / W);
+        };
+        if (t < nin) {
+            const int wt = win_of(t), wp = t ? win_of(t - 1) : -1;
+            for (int k = wp + 1; k <= wt; k++)
+#pragma unroll
+                for (int c = 0; c < 3; c++)
+                    pos[c][k] = (uint16_t)cum[c];
+            if (t == nin - 1)
+                for (int k = wt + 1; k <= nwin; k++)
+#pragma unroll
+                    for (int c = 0; c < 3; c++)
+                        pos[c][k] = (uint16_t)tot[c];
+        }
+        // The windows travel by LDS-DMA (global_load_lds_dwordx4: 1 KiB per
+        // wave instruction straight into the ring slot, no VGPRs), issued in
+        // asm so that hipcc neither counts nor drains them: window k+NIF is
+        // issued before window k is folded, and the wait before the barrier
+        // that publishes window k+1 leaves the later NL*(NIF-1) DMAs in flight
+        // (vmcnt counts in issue order; stores the fold may issue after them
+        // only make the wait stricter).  Sources past the region are clamped
+        // to its last chunk (B16 <= frames_bytes), so every window issues the
+        // same NL DMAs and the count holds to the end.
+        const uint64_t Bl = ((soff[nin - 1] + slen[nin - 1] + 15) & ~15ull) - 16;
+        const u32 ring_lds = (u32)(uintptr_t)ring;
+        auto issue = [&](int k) {
+#pragma unroll
+            for (int j = 0; j < NL; j++) {
+                const uint64_t g = A + (uint64_t)k * W + 16ull * (j * kBlock + t);
+                const u32 dst = __builtin_amdgcn_readfirstlane(
+                    ring_lds + (u32)((k % R::RS) * W + (j * kBlock + w * 64) * 16));
+                if (R::PROBE != 2)
+                    glds16<R::LNT>(frames + (g < Bl ? g : Bl), dst);
+            }
+        };
+        uint32_t* hl = EXT && !COMPUTE ? hashes : nullptr;
+        uint16_t* ql = EXT && !COMPUTE ? queues : nullptr;
+        uint4* stg = COMPUTE && S::STAGE ? stage : nullptr;
+        constexpr int RB = R::RS * W;
+        auto process = [&](int k) {
+            const int b0 = pos[0][k], e0 = pos[0][k + 1], b1 = pos[1][k], e1 = pos[1][k + 1],
+                      b2 = pos[2][k], e2 = pos[2][k + 1];
+            constexpr int P0 = 64 / S::G0, P1 = 64 / S::G1, P2 = 64 / S::G2;
+            const int t0 = (e0 - b0 + P0 - 1) / P0, t1 = (e1 - b1 + P1 - 1) / P1,
+                      t2 = (e2 - b2 + P2 - 1) / P2;
+            for (int q = w; q < t0 + t1 + t2; q += NW) {       // wave-uniform
+                if (q < t0)
+                    ring_trip<S, S::G0, S::U0, COMPUTE, EXT, RB>(frames, frames_bytes, A, ring, soff, slen, list[0], b0 + P0 * q, e0, flags, codes, csums, ext, hl, ql, stg);
+                else if (q < t0 + t1)
+                    ring_trip<S, S::G1, S::U1, COMPUTE, EXT, RB>(frames, frames_bytes, A, ring, soff, slen, list[1], b1 + P1 * (q - t0), e1, flags, codes, csums, ext, hl, ql, stg);
+                else
+                    ring_trip<S, S::G2, S::U2, COMPUTE, EXT, RB>(frames, frames_bytes, A, ring, soff, slen, list[2], b2 + P2 * (q - t0 - t1), e2, flags, codes, csums, ext, hl, ql, stg);
+            }
+        };
+        // prologue: windows 0..NIF-1 in flight, wait for window 0
+        for (int k = 0; k < NIF; k++)
+            issue(k);
+        wait_vmcnt<NL * (NIF - 1)>();
+        __syncthreads();
+        for (int k = 0; k < nwin; k++) {
+            issue(k + NIF);          // into the slot of window k+NIF-RS <= k-2: free
+            if (R::PROBE != 1)
+                process(k);          // windows k-1 and k
+            wait_vmcnt<NL * (NIF - 1)>();
+            __syncthreads();         // window k+1 published; windows <= k-1 free
+        }
+        wait_vmcnt<0>();             // the clamped DMAs past the end land before the block ends
+    }
+    __syncthreads();
+    desc_tail<S, COMPUTE, EXT>(frames, frames_bytes, f0, n, soff, slen, codes, csums, hashes, queues,
+                               stage, out_code, out_csum, flags, ext);
+}
+
+template <class S, class R, bool COMPUTE, bool XCD, int OCC = 1>
+__global__ void __launch_bounds__(kBlock, OCC)
+k_desc_ring(uint8_t* __restrict__ frames, uint64_t frames_bytes,
+            const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens, u32 n,
+            uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags)
+{
+    desc_ring<S, R, COMPUTE, XCD, false>(frames, frames_bytes, off, lens, n, out_code, out_csum,
+                                         flags, Ext{});
+}
+
+template <class S, class R, bool COMPUTE, bool XCD, int OCC = 1>
+__global__ void __launch_bounds__(kBlock, OCC)
+k_desc_ring_x(uint8_t* __restrict__ frames, uint64_t frames_bytes,
+              const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens, u32 n,
+              uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags, Ext ext)
+{
+    desc_ring<S, R, COMPUTE, XCD, true>(frames, frames_bytes, off, lens, n, out_code, out_csum,
+                                        flags, ext);
+}
 // C3: IMIX 64/576/1500 at 7:4:1, pslib 64 B packing, descriptor kernels.
 int imix_main(uint64_t n, int rounds)
 {
@@ -229,6 +725,40 @@ int imix_main(uint64_t n, int rounds)
     MIXED(false, 6, "6 verify NT loads (shipped)", 4, 1, 16, 3, 32, 3)
     MIXED(false, 6, "6 verify temporal loads", 4, 1, 16, 3, 32, 3, kWM, 256, true, 1, 1, false, false)
     MIXED(true, 6, "6 STAGE nt, temporal loads", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true, false)
+    // round 2c: the block's packed region streamed through an LDS ring
+#define RINGP(C_, OCC_, TAG, W_, NIF_, LNT_, PR_, ...)                                     \
+    vs.push_back({std::string(C_ ? "compute" : "verify ") + " ring " + TAG,                 \
+                  C_ ? cb : vb, [&](hipStream_t st) {                                      \
+        using S_ = DescShape<__VA_ARGS__>;                                                  \
+        using R_ = RingShape<W_, NIF_, LNT_, 4, PR_>;                                       \
+        hipLaunchKernelGGL((k_desc_ring<S_, R_, C_, true, OCC_>), dim3((n + 255) / 256),    \
+                           dim3(256), 0, st, C_ ? tx : rx, total, doff, dlen, (u32)n,       \
+                           C_ ? nullptr : v1, nullptr, 0u);                                 \
+    }});
+#define RING(C_, OCC_, TAG, W_, NIF_, LNT_, ...) RINGP(C_, OCC_, TAG, W_, NIF_, LNT_, 0, __VA_ARGS__)
+    if (getenv("KB_RING")) {
+    RING(false, 4, "W8K NIF2 occ4", 8192, 2, true, 4, 1, 16, 3, 32, 3)
+    RINGP(false, 4, "W8K NIF2 occ4 PROBE no fold", 8192, 2, true, 1, 4, 1, 16, 3, 32, 3)
+    RINGP(false, 4, "W8K NIF2 occ4 PROBE no DMA", 8192, 2, true, 2, 4, 1, 16, 3, 32, 3)
+    RINGP(false, 4, "W16K NIF2 occ4 PROBE no fold", 16384, 2, true, 1, 4, 1, 16, 3, 32, 3)
+    RING(true, 2, "W8K NIF2 occ2 temporal", 8192, 2, false, 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true, false)
+    RINGP(true, 2, "W8K NIF2 occ2 PROBE no DMA", 8192, 2, false, 2, 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true, false)
+    }
+    // round 2d: one frame per lane out of an LDS copy of the block's region
+#define LANE(C_, TAG, F_, CAP_, LNT_)                                                      \
+    vs.push_back({std::string(C_ ? "compute" : "verify ") + " lane " + TAG,                 \
+                  C_ ? cb : vb, [&](hipStream_t st) {                                      \
+        using L_ = LaneShape<F_, CAP_, LNT_, WM_SECTOR_NT>;                                 \
+        hipLaunchKernelGGL((k_desc_lane<L_, C_, true>), dim3((n + F_ - 1) / F_), dim3(64),  \
+                           0, st, C_ ? tx : rx, total, doff, dlen, (u32)n,                  \
+                           C_ ? nullptr : v1, nullptr, 0u);                                 \
+    }});
+    LANE(false, "F64 CAP32K nt", 64, 32768, true)
+    LANE(false, "F32 CAP16K nt", 32, 16384, true)
+    LANE(false, "F64 CAP32K temporal", 64, 32768, false)
+    LANE(true, "F64 CAP32K temporal", 64, 32768, false)
+    LANE(true, "F64 CAP32K nt", 64, 32768, true)
+    LANE(true, "F32 CAP16K temporal", 32, 16384, false)
     vs.push_back({"verify  desc (launch_verify_desc)", vb, [&](hipStream_t st) {
         CK(launch_verify_desc(rx, total, doff, dlen, (u32)n, v1, 0u, st));
     }});
