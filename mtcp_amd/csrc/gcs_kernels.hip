@@ -397,9 +397,11 @@ hipError_t launch_burst_server(ServerMailbox* mb, uint32_t done_seq, uint64_t id
 // keeps K = 1 (profiles/r02/kbench_imix_K.log; other class shapes:
 // kbench_imix_shapes2.log).
 template <int G0_, int U0_, int G1_, int U1_, int G2_, int U2_, int WM_ = kWM, int F_ = kBlock,
-          bool ORDERED_ = true, int K0_ = 1, int K1_ = 1, bool STAGE_ = false, bool NT_ = kNT>
+          bool ORDERED_ = true, int K0_ = 1, int K1_ = 1, bool STAGE_ = false, bool NT_ = kNT,
+          int RELOAD_ = 0>
 struct DescShape {
     static constexpr bool NT = NT_;
+    static constexpr int RELOAD = RELOAD_;   // A/B: re-read each staged sector before its store
     static constexpr int G0 = G0_, U0 = U0_, G1 = G1_, U1 = U1_, G2 = G2_, U2 = U2_, WM = WM_;
     static constexpr int F = F_;
     static constexpr bool ORDERED = ORDERED_;
@@ -484,9 +486,13 @@ __device__ __forceinline__ void desc_tail(uint8_t* __restrict__ frames, uint64_t
         // (two packed 64 B frames) are one whole 128 B line of one store
         // instruction.  A chunk goes out under exactly the epilogue's
         // conditions: a status that fills, inside the frame and the buffer.
+        bool go[4];
+        uint64_t ob[4];
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             const int q = r * kBlock + t, ft = q >> 2, c = q & 3;
+            go[r] = false;
+            ob[r] = 0;
             if (ft >= F || f0 + ft >= n)
                 continue;
             const u32 st = codes[ft];
@@ -494,10 +500,22 @@ __device__ __forceinline__ void desc_tail(uint8_t* __restrict__ frames, uint64_t
                              (EXT && (st == GCS_TX_ICMP_OK || st == GCS_TX_BAD_ICMPLEN));
             if (!wip || 16 * c >= (int)slen[ft])
                 continue;
-            const uint64_t o = soff[ft] + 16 * c;
-            if (o + 16 <= frames_bytes)
-                stg16<S::WM>(frames + o, stage[q]);
+            ob[r] = soff[ft] + 16 * c;
+            go[r] = ob[r] + 16 <= frames_bytes;
         }
+        if constexpr (S::RELOAD != 0) {
+            // A/B probe: bring each sector's line into L2 right before its store
+            u32 keep = 0;
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+                if (go[r])
+                    keep ^= ldg16<S::RELOAD == 2>(frames + ob[r]).x;
+            asm volatile("" : : "v"(keep));
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+            if (go[r])
+                stg16<S::WM>(frames + ob[r], stage[r * kBlock + t]);
     }
     if (t < F && i < n) {
         if (out_code)

@@ -119,7 +119,28 @@ struct Variant {
     double bytes;                       // algorithmic bytes per launch
     std::function<void(hipStream_t)> run;
     std::vector<float> ms;
+    std::function<void(hipStream_t)> prep = nullptr;   // untimed, before each timed launch
 };
+
+// Zero both check fields (bytes 24-25, 50-51) of every fixed-stride frame: a
+// TX batch as mTCP hands it over (ip_out.c:153, tcp_out.c:323), so the next
+// fill writes new bytes instead of the values already there.
+__global__ void k_zero_checks(uint8_t* f, uint64_t n, uint64_t stride)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        *reinterpret_cast<uint16_t*>(f + i * stride + 24) = 0;
+        *reinterpret_cast<uint16_t*>(f + i * stride + 50) = 0;
+    }
+}
+__global__ void k_zero_checks_desc(uint8_t* f, const uint64_t* off, const uint16_t* len, uint64_t n)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && len[i] >= 52) {
+        *reinterpret_cast<uint16_t*>(f + off[i] + 24) = 0;
+        *reinterpret_cast<uint16_t*>(f + off[i] + 50) = 0;
+    }
+}
 
 __global__ void k_hdr_desc(uint8_t* buf, const uint64_t* off, const uint16_t* lens, uint64_t n)
 {
@@ -188,6 +209,53 @@ __device__ __forceinline__ void wait_vmcnt()
     static_assert(N >= 0 && N < 64, "vmcnt");
     __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
     asm volatile("" ::: "memory");
+}
+
+// IMIX fill ceiling: k_read_regions' stream of the block's packed region, then
+// the staged fill's write-back pattern with no fold -- sector 0 of each of the
+// block's 256 frames, in frame order, four lanes per sector, nt stores of the
+// bytes already there (re-read, mostly from L2 / MALL: LNT = false keeps the
+// stream's lines cached).  What a fill that reads every byte once and writes
+// one sector per frame costs on this batch.
+template <int U, bool LNT, bool RNT = false, bool FLIP = false>
+__global__ void __launch_bounds__(256) k_fill_ceiling(uint8_t* __restrict__ p,
+                                                      const uint64_t* __restrict__ off,
+                                                      const uint16_t* __restrict__ lens, u32 n,
+                                                      uint32_t* out)
+{
+    __shared__ uint64_t soff[256];
+    __shared__ uint16_t slen[256];
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);
+    const uint64_t f0 = (uint64_t)blk * 256, f1 = min<uint64_t>(f0 + 256, n) - 1;
+    if (f0 + threadIdx.x < n) {
+        soff[threadIdx.x] = off[f0 + threadIdx.x];
+        slen[threadIdx.x] = lens[f0 + threadIdx.x];
+    }
+    const uint64_t a = off[f0] & ~15ull, b = off[f1] + lens[f1];
+    uint32_t acc = 0;
+    for (uint64_t base = a; base < b; base += 256ull * U * 16) {
+        uint4 v[U];
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            const uint64_t o = base + (uint64_t)(j * 256 + threadIdx.x) * 16;
+            v[j] = o + 16 <= b ? ldg16<LNT>(p + o) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < U; j++) acc += v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int q = r * 256 + threadIdx.x, ft = q >> 2, c = q & 3;
+        if (f0 + ft >= n || 16 * c >= (int)slen[ft])
+            continue;
+        uint8_t* s = p + soff[ft] + 16 * c;
+        uint4 w = ldg16<RNT>(s);
+        if (FLIP && c == 1)
+            w.z ^= 0x00000001u;                      // byte 24 (iph->check): new data each run
+        stg16<WM_SECTOR_NT>(s, w);
+    }
+    if (acc == 0x9E3779B9u) out[0] = acc;
 }
 
 // ---------------------------------------------------------------------------
@@ -725,6 +793,22 @@ int imix_main(uint64_t n, int rounds)
     MIXED(false, 6, "6 verify NT loads (shipped)", 4, 1, 16, 3, 32, 3)
     MIXED(false, 6, "6 verify temporal loads", 4, 1, 16, 3, 32, 3, kWM, 256, true, 1, 1, false, false)
     MIXED(true, 6, "6 STAGE nt, temporal loads", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true, false)
+    // fresh IMIX TX batches: check fields zeroed (untimed) before every launch
+    vs.push_back({"compute desc (launch_compute_desc) FRESH checks", cb, [&](hipStream_t st) {
+        CK(launch_compute_desc(tx, total, doff, dlen, (u32)n, nullptr, nullptr, 0u, st));
+    }});
+    vs.back().prep = [&](hipStream_t st) {
+        hipLaunchKernelGGL(k_zero_checks_desc, dim3((n + 255) / 256), dim3(256), 0, st, tx, doff, dlen, n);
+    };
+    vs.push_back({"compute mixed no write-back FRESH checks", cb, [&](hipStream_t st) {
+        CK(launch_compute_desc(tx, total, doff, dlen, (u32)n, nullptr, nullptr, (u32)GCS_CF_NO_INPLACE, st));
+    }});
+    vs.back().prep = vs[vs.size() - 2].prep;
+    // round 2e: re-read each staged sector (line into L2) right before its store
+    MIXED(true, 6, "6 STAGE nt, temporal loads, RELOAD temporal", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true, false, 1)
+    MIXED(true, 6, "6 STAGE nt, temporal loads, RELOAD nt", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true, false, 2)
+    MIXED(true, 6, "6 STAGE nt, nt loads, RELOAD temporal", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true, true, 1)
+    MIXED(true, 6, "6 STAGE sc1, temporal loads, RELOAD temporal", 4, 1, 16, 3, 32, 3, WM_SECTOR_SC1, 256, true, 1, 1, true, false, 1)
     // round 2c: the block's packed region streamed through an LDS ring
 #define RINGP(C_, OCC_, TAG, W_, NIF_, LNT_, PR_, ...)                                     \
     vs.push_back({std::string(C_ ? "compute" : "verify ") + " ring " + TAG,                 \
@@ -753,12 +837,14 @@ int imix_main(uint64_t n, int rounds)
                            0, st, C_ ? tx : rx, total, doff, dlen, (u32)n,                  \
                            C_ ? nullptr : v1, nullptr, 0u);                                 \
     }});
+    if (getenv("KB_LANE")) {
     LANE(false, "F64 CAP32K nt", 64, 32768, true)
     LANE(false, "F32 CAP16K nt", 32, 16384, true)
     LANE(false, "F64 CAP32K temporal", 64, 32768, false)
     LANE(true, "F64 CAP32K temporal", 64, 32768, false)
     LANE(true, "F64 CAP32K nt", 64, 32768, true)
     LANE(true, "F32 CAP16K temporal", 32, 16384, false)
+    }
     vs.push_back({"verify  desc (launch_verify_desc)", vb, [&](hipStream_t st) {
         CK(launch_verify_desc(rx, total, doff, dlen, (u32)n, v1, 0u, st));
     }});
@@ -771,6 +857,21 @@ int imix_main(uint64_t n, int rounds)
                            doff, dlen, (u32)n, sink);                                           \
     }});
     RREG(2) RREG(4) RREG(8)
+#define FCEIL(U_, LNT_)                                                                   \
+    vs.push_back({"fill-ceiling region stream + sector nt U=" #U_ " LNT=" #LNT_, cb,           \
+                  [&](hipStream_t st) {                                                    \
+        hipLaunchKernelGGL((k_fill_ceiling<U_, LNT_>), dim3((n + 255) / 256), dim3(256), 0,   \
+                           st, tx, doff, dlen, (u32)n, sink);                              \
+    }});
+    FCEIL(4, false) FCEIL(4, true)
+    vs.push_back({"fill-ceiling ... LNT=true RNT, data changed", cb, [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_fill_ceiling<4, true, true, true>), dim3((n + 255) / 256), dim3(256), 0,
+                           st, tx, doff, dlen, (u32)n, sink);
+    }});
+    vs.push_back({"fill-ceiling region stream + sector nt U=4 LNT=true RNT", cb, [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_fill_ceiling<4, true, true>), dim3((n + 255) / 256), dim3(256), 0,
+                           st, tx, doff, dlen, (u32)n, sink);
+    }});
     vs.push_back({"read-ceiling uint4 NT (whole packed buffer)", (double)total,
                   [&](hipStream_t st) {
         hipLaunchKernelGGL((k_read<true>), dim3(cus * 8), dim3(256), 0, st, (const uint4*)rx,
@@ -933,6 +1034,36 @@ int tx_main(uint64_t n, int rounds)
         hipLaunchKernelGGL((k_fixed<32, 3, false, false, true, WM_SECTOR_SC1, true>),          \
                            dim3((n + 7) / 8), dim3(256), 0, st, rx, stride, L, (u32)n, v1,     \
                            nullptr, 0u);                                                      \
+    }});
+    // fresh TX batches: the check fields zeroed (untimed) before every launch
+    auto zero_tx = [&](hipStream_t st) {
+        hipLaunchKernelGGL(k_zero_checks, dim3((n + 255) / 256), dim3(256), 0, st, tx, n, stride);
+    };
+#define TXF(WM_, TAG)                                                                         \
+    vs.push_back({std::string("compute <32,3> FRESH checks, ") + TAG, cbytes, [&](hipStream_t st) { \
+        hipLaunchKernelGGL((k_fixed<32, 3, true, false, true, WM_, true>), dim3((n + 7) / 8),   \
+                           dim3(256), 0, st, tx, stride, L, (u32)n, nullptr, nullptr, 0u);    \
+    }});                                                                                      \
+    vs.back().prep = zero_tx;
+    TXF(WM_LINE_SC1, "128B line sc1 (shipped <= 1M)")
+    TXF(WM_SECTOR_SC1, "64B sector sc1")
+    TXF(WM_SECTOR_NT, "64B sector nt")
+    TXF(WM_LINE_NT, "128B line nt")
+    vs.push_back({"compute <32,3> FRESH checks, pure fold (no write-back)", cbytes, [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_fixed<32, 3, true, false, true, WM_SECTOR_SC1, true>), dim3((n + 7) / 8),
+                           dim3(256), 0, st, tx, stride, L, (u32)n, nullptr, nullptr,
+                           (u32)GCS_CF_NO_INPLACE);
+    }});
+    vs.back().prep = zero_tx;
+    vs.push_back({"zero checks kernel alone", (double)n * 4, [&](hipStream_t st) { zero_tx(st); }});
+    vs.push_back({"step TX+RX FRESH checks, launch_compute_fixed + verify", cbytes + vbytes, [&](hipStream_t st) {
+        CK(launch_compute_fixed(tx, stride, L, (u32)n, nullptr, nullptr, 0u, st));
+        CK(launch_verify_fixed(rx, stride, L, (u32)n, v1, 0u, st));
+    }});
+    vs.back().prep = zero_tx;
+    vs.push_back({"step TX+RX refill (bench), launch_compute_fixed + verify", cbytes + vbytes, [&](hipStream_t st) {
+        CK(launch_compute_fixed(tx, stride, L, (u32)n, nullptr, nullptr, 0u, st));
+        CK(launch_verify_fixed(rx, stride, L, (u32)n, v1, 0u, st));
     }});
     STEPV(WM_SECTOR_SC1, "64B sector sc1 (shipped)")
     STEPV(WM_LINE_SC1, "128B line sc1")
@@ -1410,6 +1541,8 @@ void run_variants(std::vector<Variant>& vs, hipStream_t s, int rounds)
         for (auto& v : vs) {
             for (int w = 0; w < 3; w++) v.run(s);
             for (int r = 0; r < rounds; r++) {
+                if (v.prep)
+                    v.prep(s);
                 scrub(s);
                 CK(hipEventRecord(e0, s));
                 v.run(s);
@@ -1424,6 +1557,8 @@ void run_variants(std::vector<Variant>& vs, hipStream_t s, int rounds)
     }
     for (int r = 0; r < rounds; r++) {
         for (auto& v : vs) {
+            if (v.prep)
+                v.prep(s);
             scrub(s);
             CK(hipEventRecord(e0, s));
             v.run(s);
@@ -1695,6 +1830,8 @@ int main(int argc, char** argv)
         for (auto& v : vs) {
             for (int w = 0; w < 3; w++) v.run(s);
             for (int r = 0; r < rounds; r++) {
+                if (v.prep)
+                    v.prep(s);
                 scrub(s);
                 CK(hipEventRecord(e0, s));
                 v.run(s);
@@ -1709,6 +1846,8 @@ int main(int argc, char** argv)
     }
     for (int r = 0; r < rounds; r++) {
         for (auto& v : vs) {
+            if (v.prep)
+                v.prep(s);
             scrub(s);
             CK(hipEventRecord(e0, s));
             v.run(s);
