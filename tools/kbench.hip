@@ -1526,6 +1526,14 @@ int lro_main(uint64_t n, int rounds)
 
 void run_variants(std::vector<Variant>& vs, hipStream_t s, int rounds)
 {
+    // KB_ONLY=<substring>: time only the matching variants (profiling runs)
+    if (const char* only = std::getenv("KB_ONLY")) {
+        std::vector<Variant> keep;
+        for (auto& v : vs)
+            if (v.name.find(only) != std::string::npos)
+                keep.push_back(v);
+        vs.swap(keep);
+    }
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
