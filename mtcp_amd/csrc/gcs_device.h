@@ -624,6 +624,10 @@ __device__ __forceinline__ void epilogue(const Hdr& h, Acc a, uint8_t* __restric
             }
         } else {
             const int nchunks = (int)((len + 15) >> 4);
+            // the buffer-end test in 32 bits (chunks c < 8 here): no 64-bit
+            // invariant for it stays live across k_gro's batch loop (5 -> 3
+            // spilled VGPRs there; the same speed)
+            const int wl = wlim > 256 ? 256 : (int)wlim;
             const int ctcp = (int)(ts + 16) >> 4;            // chunk holding tcph->check
             const int cicmp = (int)(ts + 2) >> 4;            // chunk holding icmph->checksum
 #pragma unroll
@@ -642,7 +646,7 @@ __device__ __forceinline__ void epilogue(const Hdr& h, Acc a, uint8_t* __restric
                                          (wicmp && (c >> 2) == (cicmp >> 2)));
                 if (!take)
                     continue;
-                if (16 * c + 16 > wlim) {                    // chunk crosses the buffer end
+                if (16 * c + 16 > wl) {                      // chunk crosses the buffer end
                     if (has_ip)
                         *reinterpret_cast<uint16_t*>(f + 24) = (uint16_t)ipc;
                     if (has_tcp)

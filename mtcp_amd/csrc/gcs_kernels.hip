@@ -17,7 +17,8 @@ constexpr bool kNT = true;
 constexpr int kWM = WM_SECTOR_SC1;
 // XCD-contiguous frame ranges (xcd_block below): TX+RX step 491 -> 485 us.
 constexpr bool kXCD = true;
-// k_desc_mixed register budget: 6 waves per SIMD (<= 80 VGPRs, no spills).
+// k_desc_mixed register budget: 6 waves per SIMD (80 VGPRs; one 8-byte value goes to
+// scratch around the list passes: a store and a reload per thread, outside the loops).
 // 4M IMIX frames: verify 349 -> 316 us against the unbounded 89-94 VGPRs (5
 // waves); 8 waves spills and takes 385 us.
 constexpr int kDescOcc = 6;
