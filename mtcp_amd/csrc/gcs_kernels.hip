@@ -4,6 +4,8 @@
 #include "gcs_device.h"
 #include "gcs_internal.h"
 
+#include <cstdlib>
+
 namespace gcs {
 
 constexpr int kBlock = 256;
@@ -1395,6 +1397,17 @@ k_ip_fn(const uint8_t* __restrict__ buf, uint64_t buf_bytes, const uint64_t* __r
 // its neighbour's bytes.)
 constexpr uint64_t kLineWbBytes = 128ull << 20;
 
+// GCS_TX_LINE_WB_MB overrides kLineWbBytes (MB of lines per launch; 0 = sector
+// write-back only): an A/B knob for the bench step, read once.
+static uint64_t line_wb_bytes()
+{
+    static const uint64_t v = [] {
+        const char* e = std::getenv("GCS_TX_LINE_WB_MB");
+        return e ? (uint64_t)std::strtoull(e, nullptr, 10) << 20 : kLineWbBytes;
+    }();
+    return v;
+}
+
 template <int G, int U, bool COMPUTE, bool LOOP, bool EXT, int K = 1, int WM = kWM>
 static hipError_t launch_fixed_wm(uint8_t* frames, uint64_t stride, u32 frame_len, u32 n,
                                   uint8_t* code, uint32_t* csum, u32 flags, const Ext& ext,
@@ -1417,7 +1430,7 @@ static hipError_t launch_fixed(uint8_t* frames, uint64_t stride, u32 frame_len, 
                                hipStream_t s)
 {
     if constexpr (COMPUTE && G >= 8)
-        if (stride % 128 == 0 && (uint64_t)n * 128 <= kLineWbBytes)
+        if (stride % 128 == 0 && (uint64_t)n * 128 <= line_wb_bytes())
             return launch_fixed_wm<G, U, COMPUTE, LOOP, EXT, K, WM_LINE_SC1>(
                 frames, stride, frame_len, n, code, csum, flags, ext, s);
     return launch_fixed_wm<G, U, COMPUTE, LOOP, EXT, K>(frames, stride, frame_len, n, code, csum,
