@@ -792,6 +792,11 @@ int imix_main(uint64_t n, int rounds)
     // (64 B packing) may stay in L2 for the second pass
     MIXED(false, 6, "6 verify NT loads (shipped)", 4, 1, 16, 3, 32, 3)
     MIXED(false, 6, "6 verify temporal loads", 4, 1, 16, 3, 32, 3, kWM, 256, true, 1, 1, false, false)
+    // descriptors per block: the three class passes walk a smaller region
+    MIXED(false, 6, "6 verify F=128", 4, 1, 16, 3, 32, 3, kWM, 128, true, 1, 1, false, true)
+    MIXED(false, 6, "6 verify F=64", 4, 1, 16, 3, 32, 3, kWM, 64, true, 1, 1, false, true)
+    MIXED(true, 6, "6 STAGE nt, temporal loads F=128", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 128, true, 1, 1, true, false)
+    MIXED(true, 6, "6 STAGE nt, temporal loads F=64", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 64, true, 1, 1, true, false)
     MIXED(true, 6, "6 STAGE nt, temporal loads", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true, false)
     // fresh IMIX TX batches: check fields zeroed (untimed) before every launch
     vs.push_back({"compute desc (launch_compute_desc) FRESH checks", cb, [&](hipStream_t st) {
