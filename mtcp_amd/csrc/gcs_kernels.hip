@@ -410,7 +410,8 @@ struct DescShape {
     static constexpr bool ORDERED = ORDERED_;
     static constexpr int K0 = K0_, K1 = K1_;
     static constexpr bool STAGE = STAGE_;
-    static_assert(F <= kBlock, "one descriptor per thread");
+    static constexpr int R = (F + kBlock - 1) / kBlock;   // descriptors per thread
+    static_assert(F <= kBlock || F % kBlock == 0, "whole descriptors per thread");
     static constexpr int T0 = 16 * G0 * U0, T1 = 16 * G1 * U1;
 };
 
@@ -480,19 +481,18 @@ __device__ __forceinline__ void desc_tail(uint8_t* __restrict__ frames, uint64_t
                                           uint32_t* __restrict__ out_csum, u32 flags,
                                           const Ext& ext)
 {
-    constexpr int F = S::F;
+    constexpr int F = S::F, NR = 4 * S::R;            // stage rounds: 4 chunks per frame
     const int t = threadIdx.x;
-    const uint64_t i = f0 + t;
     if (COMPUTE && S::STAGE && !(flags & GCS_CF_NO_INPLACE)) {
         // STAGE: the frames' sector-0 write-backs leave together, in frame
         // order, 16 B per lane: four lanes per sector, so adjacent sectors
         // (two packed 64 B frames) are one whole 128 B line of one store
         // instruction.  A chunk goes out under exactly the epilogue's
         // conditions: a status that fills, inside the frame and the buffer.
-        bool go[4];
-        uint64_t ob[4];
+        bool go[NR];
+        uint64_t ob[NR];
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
+        for (int r = 0; r < NR; r++) {
             const int q = r * kBlock + t, ft = q >> 2, c = q & 3;
             go[r] = false;
             ob[r] = 0;
@@ -510,26 +510,31 @@ __device__ __forceinline__ void desc_tail(uint8_t* __restrict__ frames, uint64_t
             // A/B probe: bring each sector's line into L2 right before its store
             u32 keep = 0;
 #pragma unroll
-            for (int r = 0; r < 4; r++)
+            for (int r = 0; r < NR; r++)
                 if (go[r])
                     keep ^= ldg16<S::RELOAD == 2>(frames + ob[r]).x;
             asm volatile("" : : "v"(keep));
         }
 #pragma unroll
-        for (int r = 0; r < 4; r++)
+        for (int r = 0; r < NR; r++)
             if (go[r])
                 stg16<S::WM>(frames + ob[r], stage[r * kBlock + t]);
     }
-    if (t < F && i < n) {
-        if (out_code)
-            out_code[i] = codes[t];
-        if (COMPUTE && out_csum)
-            out_csum[i] = csums[t];
-        if (EXT && !COMPUTE) {
-            if (ext.hash)
-                ext.hash[i] = hashes[t];
-            if (ext.queue)
-                ext.queue[i] = queues[t];
+#pragma unroll
+    for (int r = 0; r < S::R; r++) {
+        const int ft = r * kBlock + t;
+        const uint64_t i = f0 + ft;
+        if (ft < F && i < n) {
+            if (out_code)
+                out_code[i] = codes[ft];
+            if (COMPUTE && out_csum)
+                out_csum[i] = csums[ft];
+            if (EXT && !COMPUTE) {
+                if (ext.hash)
+                    ext.hash[i] = hashes[ft];
+                if (ext.queue)
+                    ext.queue[i] = queues[ft];
+            }
         }
     }
 }
@@ -547,7 +552,8 @@ __device__ __forceinline__ void desc_mixed(uint8_t* __restrict__ frames, uint64_
     __shared__ uint16_t slen[F];
     __shared__ uint16_t list[3][F];
     __shared__ int cnt[3];
-    __shared__ int wcnt[3][kBlock / 64];
+    constexpr int R = S::R, NW = kBlock / 64;
+    __shared__ int wcnt[3][R * NW];
     __shared__ uint8_t codes[F];
     __shared__ uint32_t csums[COMPUTE ? F : 1];
     __shared__ uint32_t hashes[EXT && !COMPUTE ? F : 1];
@@ -559,53 +565,66 @@ __device__ __forceinline__ void desc_mixed(uint8_t* __restrict__ frames, uint64_
     if (t < 3)
         cnt[t] = 0;
     __syncthreads();
-    // phase 0: validate and classify
-    const uint64_t i = f0 + t;
-    int cls = -1;
-    if (t < F && i < n) {
-        const uint64_t o = off[i];
-        const u32 len = lens[i];
-        const bool ok = (o & 15) == 0 && o <= frames_bytes && len <= frames_bytes - o;
-        if (!ok) {
-            codes[t] = COMPUTE ? GCS_TX_BAD_DESC : GCS_V_BAD_DESC;
-            if (COMPUTE)
-                csums[t] = 0;
-            if (EXT && !COMPUTE) {
-                hashes[t] = 0;
-                queues[t] = 0xFFFF;
+    // phase 0: validate and classify (R descriptors per thread: frames t, t+256, ..)
+    int cls[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const int ft = r * kBlock + t;
+        const uint64_t i = f0 + ft;
+        cls[r] = -1;
+        if (ft < F && i < n) {
+            const uint64_t o = off[i];
+            const u32 len = lens[i];
+            const bool ok = (o & 15) == 0 && o <= frames_bytes && len <= frames_bytes - o;
+            if (!ok) {
+                codes[ft] = COMPUTE ? GCS_TX_BAD_DESC : GCS_V_BAD_DESC;
+                if (COMPUTE)
+                    csums[ft] = 0;
+                if (EXT && !COMPUTE) {
+                    hashes[ft] = 0;
+                    queues[ft] = 0xFFFF;
+                }
+            } else {
+                soff[ft] = o;
+                slen[ft] = (uint16_t)len;
+                cls[r] = len <= (u32)S::T0 ? 0 : (len <= (u32)S::T1 ? 1 : 2);
+                if (!S::ORDERED)
+                    list[cls[r]][atomicAdd(&cnt[cls[r]], 1)] = (uint16_t)ft;
             }
-        } else {
-            soff[t] = o;
-            slen[t] = (uint16_t)len;
-            cls = len <= (u32)S::T0 ? 0 : (len <= (u32)S::T1 ? 1 : 2);
-            if (!S::ORDERED)
-                list[cls][atomicAdd(&cnt[cls], 1)] = (uint16_t)t;
         }
     }
     if (S::ORDERED) {
-        // per wave and class: ballot, then the lane's rank among its class
+        // per (descriptor round, wave) and class: ballot, then the lane's rank
+        // among its class; lists come out in frame order
         const int lane = t & 63, w = t >> 6;
         const uint64_t below = (1ull << lane) - 1;
-        int rank = 0;
+        int rank[R];
 #pragma unroll
-        for (int c = 0; c < 3; c++) {
-            const uint64_t m = __ballot(cls == c);
-            if (lane == 0)
-                wcnt[c][w] = __popcll(m);
-            if (cls == c)
-                rank = __popcll(m & below);
+        for (int r = 0; r < R; r++) {
+            rank[r] = 0;
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                const uint64_t m = __ballot(cls[r] == c);
+                if (lane == 0)
+                    wcnt[c][r * NW + w] = __popcll(m);
+                if (cls[r] == c)
+                    rank[r] = __popcll(m & below);
+            }
         }
         __syncthreads();
-        if (cls >= 0) {
-            int base = 0;
-            for (int ww = 0; ww < w; ww++)
-                base += wcnt[cls][ww];
-            list[cls][base + rank] = (uint16_t)t;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            if (cls[r] >= 0) {
+                int base = 0;
+                for (int k = 0; k < r * NW + w; k++)
+                    base += wcnt[cls[r]][k];
+                list[cls[r]][base + rank[r]] = (uint16_t)(r * kBlock + t);
+            }
         }
         if (t < 3) {
             int tot = 0;
-            for (int ww = 0; ww < kBlock / 64; ww++)
-                tot += wcnt[t][ww];
+            for (int k = 0; k < R * NW; k++)
+                tot += wcnt[t][k];
             cnt[t] = tot;
         }
     }

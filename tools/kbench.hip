@@ -793,6 +793,9 @@ int imix_main(uint64_t n, int rounds)
     MIXED(false, 6, "6 verify NT loads (shipped)", 4, 1, 16, 3, 32, 3)
     MIXED(false, 6, "6 verify temporal loads", 4, 1, 16, 3, 32, 3, kWM, 256, true, 1, 1, false, false)
     // descriptors per block: the three class passes walk a smaller region
+    MIXED(false, 6, "6 verify F=512", 4, 1, 16, 3, 32, 3, kWM, 512, true, 1, 1, false, true)
+    MIXED(true, 6, "6 STAGE nt, temporal loads F=512", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 512, true, 1, 1, true, false)
+    MIXED(true, 5, "5 STAGE nt, temporal loads F=512", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 512, true, 1, 1, true, false)
     MIXED(false, 6, "6 verify F=128", 4, 1, 16, 3, 32, 3, kWM, 128, true, 1, 1, false, true)
     MIXED(false, 6, "6 verify F=64", 4, 1, 16, 3, 32, 3, kWM, 64, true, 1, 1, false, true)
     MIXED(true, 6, "6 STAGE nt, temporal loads F=128", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 128, true, 1, 1, true, false)
