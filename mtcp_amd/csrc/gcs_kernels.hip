@@ -386,8 +386,9 @@ hipError_t launch_burst_server(ServerMailbox* mb, uint32_t done_seq, uint64_t id
 // a dependent global load before its frame loads: 4M IMIX frames, verify
 // 316 -> 269 us, fill 407 -> 364 us.  Wider shapes (U = 6 or 9 per lane)
 // spill at 6 waves per SIMD and lose (kbench imix).
-// F = descriptors per block (<= kBlock): fewer per block means more, shorter
-// blocks -- a smaller tail when large frames make every block long.
+// F = descriptors per block: <= kBlock (one per thread) or R * kBlock (R per
+// thread).  256 measured best on C3 (128: verify 319-336 us, 512: 273 us but
+// the fill's LDS stage then allows 3 blocks per CU; kbench_imix_F*_blocked.log).
 // ORDERED: the class lists keep frame order (wave ballot + prefix count)
 // instead of atomicAdd arrival order, so the groups of one list instruction
 // work on neighbouring frames: a wave's 64 B-class loads and sector stores
