@@ -50,6 +50,10 @@
  *               MTU frame; a longer frame is an LRO chain, the same size rule
  *               tcp_ring_buffer.c:18 applies) are not read by the GPU: they are
  *               left to the inner module's own checks, as the NIC did them.
+ *               set_inner selects it by itself when the inner module IS mTCP's
+ *               dpdk_module_func (weak reference): a DPDK build without
+ *               ENABLELRO never delivers a frame over 1518 B (jumbo frames off,
+ *               dpdk_module.c:112-135), so the rule only ever sees LRO chains.
  * Not supported: an inner get_rptr that is not idempotent per index, e.g.
  * DPDK built with IP_DEFRAG (dpdk_module.c:527-529 reassembles on each call);
  * a frame whose pointer or length changes between the burst's verify and
@@ -118,7 +122,8 @@ typedef struct io_module_func {
 extern io_module_func gpucsum_module_func;
 
 /* Set the inner module the decorator wraps.  Call before load_module().
- * Resets the inner caps (GPUCSUM_INNER_TX_EAGER if inner is netmap_module_func). */
+ * Resets the inner caps: GPUCSUM_INNER_TX_EAGER if inner is netmap_module_func,
+ * GPUCSUM_INNER_RX_CHAINED if it is dpdk_module_func, else none. */
 int gpucsum_set_inner(io_module_func *inner);
 /* The inner module (NULL if none): for mTCP's module-identity checks, e.g. the
  * ENABLELRO gather test at tcp_ring_buffer.c:18. */
@@ -129,6 +134,8 @@ io_module_func *gpucsum_get_inner(void);
 /* Shape of the inner module; call after gpucsum_set_inner, before init_handle.
  * rx_seg_max: longest single-segment frame (0 = 1514). */
 int gpucsum_set_inner_caps(uint32_t caps, uint32_t rx_seg_max);
+/* The caps in force (after set_inner's own choice or set_inner_caps). */
+uint32_t gpucsum_get_inner_caps(void);
 
 #define GPUCSUM_MAX_IFS    16     /* MAX_DEVICES, io_engine/include/ps.h:4 */
 #define GPUCSUM_MAX_BURST  8192   /* frames per GPU batch: a larger recv_pkts burst is

@@ -150,7 +150,11 @@ int gcs_ctx_set_burst_server(gcs_ctx *ctx, int on);
  * the offsets are 16 B-aligned and increasing, the frames go to the GPU with
  * one DMA per staging slot and no host copy.  Otherwise they are gathered
  * into the context's pinned staging (environment GCS_GATHER_THREADS threads,
- * default 8, for large batches). */
+ * default 8, for large batches).
+ * gcs_host_register: regions are process-wide, at most 64 GiB each, and may
+ * not overlap (GCS_EINVAL).  gcs_host_unregister takes the pointer that was
+ * registered; no batch reading the region may be in flight on any context
+ * (calls are synchronous, so: none running on another thread). */
 int gcs_host_alloc(void **p, uint64_t bytes);
 int gcs_host_free(void *p);
 int gcs_host_register(void *p, uint64_t bytes);

@@ -269,6 +269,10 @@ class BurstServer {
         e = std::getenv("GCS_SERVER_LIFE_US");
         life_ticks_ = (uint64_t)((e ? std::atof(e) : 2000.0) * ticks_per_us);
         prof_ = std::getenv("GCS_SERVER_PROF") != nullptr;
+        // test-only (tests/test_gpu_host.py): start the request numbers near a
+        // 16-bit tag or 32-bit wrap instead of after 65k real bursts
+        if (const char* s = std::getenv("GCS_SERVER_SEQ_START"))
+            seq_ = (uint32_t)std::strtoul(s, nullptr, 0);
         return GCS_OK;
     }
 
@@ -291,7 +295,13 @@ class BurstServer {
             int rc = launch(seq_);
             if (rc) return rc;
         }
-        const uint32_t q = ++seq_;
+        // The records carry q's low 16 bits, and cleared records read as tag
+        // 0: a request whose tag would be 0 could look complete before the
+        // grid has read it, so those numbers are never posted (this also
+        // skips 0 itself when seq_ wraps).
+        uint32_t q = ++seq_;
+        if ((q & 0xFFFFu) == 0)
+            q = ++seq_;
         const uint64_t tag = (uint64_t)(q & 0xFFFFu) << 48;
         const auto tw = std::chrono::steady_clock::now();
         std::memset(mb_->rec, 0, n * sizeof(uint64_t));   // no record of an older request
@@ -743,6 +753,12 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
                                             /*in_place=*/compute);
                 if (rc) return rc;
             } else {
+                if (ctx->server) {
+                    // a resident grid on a shared hardware queue would hold this
+                    // launch back until its idle or lifetime exit
+                    int rc = ctx->server->stop();
+                    if (rc) return rc;
+                }
                 if (compute)
                     HIP_TRY(gcs::launch_compute_desc_spread(reg.dev, reg.bytes, s.m_off, s.m_len,
                                                             n, s.m_code, s.m_csum, 0u, s.stream));
@@ -1043,15 +1059,27 @@ try {
     return GCS_OK;
 } GCS_CATCH
 
+// Regions are process-wide.  The burst server's request carries a region's
+// size in 16 B units as a u32, hence the 64 GiB limit.  hipHostRegister maps
+// the pages for every device of the process (one address space), so the
+// device view is valid whichever device the calling thread has current.
 int gcs_host_register(void* p, uint64_t bytes)
 try {
-    if (!p || bytes == 0)
+    if (!p || bytes == 0 || bytes / 16 > 0xFFFFFFFFull)
         return GCS_EINVAL;
+    uint8_t* const host = static_cast<uint8_t*>(p);
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    for (const auto& r : g_regions)
+        if (host < r.host + r.bytes && r.host < host + bytes)
+            return GCS_EINVAL;                        // overlaps a registered region
     HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterMapped));
     uint8_t* dev = nullptr;
-    HIP_TRY(hipHostGetDevicePointer((void**)&dev, p, 0));
-    std::lock_guard<std::mutex> lk(g_reg_mu);
-    g_regions.push_back(RegRegion{static_cast<uint8_t*>(p), bytes, dev});
+    hipError_t e = hipHostGetDevicePointer((void**)&dev, p, 0);
+    if (e != hipSuccess) {
+        (void)hipHostUnregister(p);
+        return hip_fail(e, "hipHostGetDevicePointer");
+    }
+    g_regions.push_back(RegRegion{host, bytes, dev});
     return GCS_OK;
 } GCS_CATCH
 

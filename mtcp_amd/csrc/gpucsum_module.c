@@ -65,6 +65,11 @@ struct gthr {
 /* mTCP's netmap module, when the decorator is linked into mTCP (weak: absent
  * from other programs).  Its get_wptr transmits, netmap_module.c:149-160. */
 extern io_module_func netmap_module_func __attribute__((weak));
+/* ... and its DPDK module.  Without ENABLELRO it receives no frame longer than
+ * 1518 B (jumbo frames off, max_rx_pkt_len = ETHER_MAX_LEN, dpdk_module.c:
+ * 112-135), so any longer frame is an LRO chain (BUF_SIZE 16384, :44-48)
+ * and RX_CHAINED is safe to assume for it either way. */
+extern io_module_func dpdk_module_func __attribute__((weak));
 
 static io_module_func *g_inner;
 static uint32_t g_caps;
@@ -79,7 +84,11 @@ int gpucsum_set_inner(io_module_func *inner)
 	if (!inner || inner == &gpucsum_module_func)
 		return GCS_EINVAL;
 	g_inner = inner;
-	g_caps = (&netmap_module_func && inner == &netmap_module_func) ? GPUCSUM_INNER_TX_EAGER : 0;
+	g_caps = 0;
+	if (&netmap_module_func && inner == &netmap_module_func)
+		g_caps = GPUCSUM_INNER_TX_EAGER;
+	if (&dpdk_module_func && inner == &dpdk_module_func)
+		g_caps = GPUCSUM_INNER_RX_CHAINED;
 	g_seg_max = GPUCSUM_DEFAULT_SEG_MAX;
 	return GCS_OK;
 }
@@ -97,6 +106,11 @@ int gpucsum_set_inner_caps(uint32_t caps, uint32_t rx_seg_max)
 	g_caps = caps;
 	g_seg_max = rx_seg_max ? rx_seg_max : GPUCSUM_DEFAULT_SEG_MAX;
 	return GCS_OK;
+}
+
+uint32_t gpucsum_get_inner_caps(void)
+{
+	return g_caps;
 }
 
 static struct gthr *lookup(struct mtcp_thread_context *ctx)

@@ -103,3 +103,30 @@ def test_product_does_not_link_oracle():
     assert "oracle" not in out and "ref_mtcp" not in out
     syms = exported_symbols(gpucsum.LIB_PATH)
     assert not any(s.startswith(("ref_", "refx_", "TCPCalcChecksum")) for s in syms)
+
+
+def test_set_inner_picks_caps_for_mtcp_modules(tmp_path):
+    """gpucsum_set_inner recognises mTCP's own modules through weak references:
+    netmap's get_wptr transmits (TX_EAGER, netmap_module.c:149-160); DPDK frames
+    over one MTU frame are ENABLELRO chains (RX_CHAINED, dpdk_module.c:44-48,
+    112-135).  The modules are defined in an -rdynamic executable, as a linked
+    mTCP exports them; no GPU call is made."""
+    exe = str(tmp_path / "inner_caps")
+    subprocess.run(["gcc", "-O1", "-rdynamic", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "plugin", "inner_caps.c"),
+                    "-L", os.path.dirname(gpucsum.LIB_PATH), "-lmtcp_gpucsum",
+                    "-Wl,-rpath," + os.path.dirname(gpucsum.LIB_PATH), "-o", exe], check=True)
+    out = subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()
+    got = dict(zip(out[0::2], map(int, out[1::2])))
+    assert got == {"dpdk": 2, "netmap": 1, "other": 0, "set": 2}
+
+
+def test_host_register_rejects_bad_regions():
+    """Regions of 64 GiB or more cannot be described to the burst server
+    (ServerReqB.bytes16 is a u32) and are refused before any HIP call."""
+    L = gpucsum.lib()
+    buf = C.create_string_buffer(64)
+    EINVAL = gpucsum.K["GCS_EINVAL"]
+    assert L.gcs_host_register(None, 64) == EINVAL
+    assert L.gcs_host_register(buf, 0) == EINVAL
+    assert L.gcs_host_register(buf, 64 << 30) == EINVAL

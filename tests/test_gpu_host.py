@@ -233,3 +233,42 @@ def test_registered_rooms_in_place(torch_dev, server):
                 assert (v[[1, 17, 40]] != 0).all()
     finally:
         gpucsum.check(L.gcs_host_unregister(mb.ctypes.data))
+
+
+@pytest.mark.parametrize("start", [0xFFFF - 3, 0x2FFFF - 2, 0xFFFFFFFF - 4])
+def test_burst_server_request_tags_wrap(torch_dev, monkeypatch, start):
+    """The per-frame records carry the request number's low 16 bits, and a
+    cleared record reads as tag 0: a request tagged 0 would complete at once,
+    before the grid read it (every 65536th burst).  Requests are
+    numbered across the 16-bit tag boundary and the 32-bit wrap here, on the
+    staged paths that complete on the records alone (RX verify, TX fill into
+    staging); every burst must equal the oracle."""
+    monkeypatch.setenv("GCS_SERVER_SEQ_START", str(start))
+    O = Oracle()
+    with gpucsum.Context(0, max_frames=1024, max_bytes=4 << 20) as c:
+        c.set_burst_server(True)
+        for k, (buf, off, lens) in enumerate(bursts(5, 64, 700)):
+            b1 = buf.copy()
+            st, cs = c.compute_host(b1, off, lens)
+            ref = buf.copy()
+            rst, rcs = O.compute_batch(ref, off, lens)
+            np.testing.assert_array_equal(st, rst)
+            np.testing.assert_array_equal(cs, rcs)
+            np.testing.assert_array_equal(b1, ref)
+            bad = synth.corrupt(ref, off, lens, frac_log2=2, seed=k)
+            v = c.verify_host(ref.copy(), off, lens)
+            np.testing.assert_array_equal(v, O.verify_batch(ref.copy(), off, lens))
+            assert (v[bad] != 0).all()
+
+
+def test_host_register_refuses_overlap(torch_dev):
+    L = gpucsum.lib()
+    rooms = np.zeros(3 * 4096, dtype=np.uint8)
+    base = (-rooms.ctypes.data) % 4096
+    a = rooms.ctypes.data + base
+    gpucsum.check(L.gcs_host_register(a, 4096))
+    try:
+        assert L.gcs_host_register(a, 4096) == gpucsum.K["GCS_EINVAL"]
+        assert L.gcs_host_register(a + 2048, 4096) == gpucsum.K["GCS_EINVAL"]
+    finally:
+        gpucsum.check(L.gcs_host_unregister(a))
