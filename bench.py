@@ -437,6 +437,58 @@ def rows_8f(ctx, torch, n=1 << 20, L=1500):
     return out
 
 
+def tx_write_mode(n, stride):
+    """The TX fill's write-back for a fixed-stride batch, as the library picks
+    it (gcs_kernels.hip launch_fixed): whole 128 B lines while n x 128 B fits
+    GCS_TX_LINE_WB_MB (default 128 MiB, inside the Infinity Cache), else the
+    64 B sectors holding the check fields."""
+    mb = int(os.environ.get("GCS_TX_LINE_WB_MB", "128"))
+    return "line" if stride % 128 == 0 and n * 128 <= (mb << 20) else "sector"
+
+
+def c2_sector_wb(ctx, torch, tx, stride, L, n):
+    """The C2 TX fill with sector write-back forced (GCS_CF_SECTOR_WB): what
+    the headline's fill costs without the whole-line write-back its 1M-frame
+    batch qualifies for."""
+    stream = torch.cuda.current_stream().cuda_stream
+    flag = gpucsum_K()["GCS_CF_SECTOR_WB"]
+    ms = _launch_ms(torch, lambda: ctx.compute_fixed(tx, stride, L, n, flags=flag, stream=stream))
+    line_ms = _launch_ms(torch, lambda: ctx.compute_fixed(tx, stride, L, n, stream=stream))
+    return {"workload": f"{n} x {L}B TX fill, stride {stride}, per launch",
+            "sector_compute_ms": ms,
+            "sector_frac_peak": n * (L + 4) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "line_compute_ms": line_ms,
+            "line_frac_peak": n * (L + 4) / (line_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+
+
+def c4_shard(ctx, torch, steps, warmup, settle_s, n=4 << 20, L=1500):
+    """The N > 1 per-GPU workload on this one GPU: a C4 shard of 4M x 1500 B
+    frames, the same TX + RX step, settle, warmup and timing as the main line
+    (time_steps), so a SCALE curve's per-GPU rate can be read against it."""
+    tx, rx, stride, nbad = make_batches(ctx, n, L, 0x6D746370, torch)
+    el, txl, rxl, verdict = time_steps(ctx, tx, rx, stride, L, n, steps, warmup, 1, torch,
+                                       settle_s)
+    bad = int((verdict != 0).sum())
+    assert bad == nbad, (bad, nbad)
+    tms, rms = float(np.mean(txl)), float(np.mean(rxl))
+    kname, kms, kb = (("compute", tms, n * (L + 4)) if tms >= rms else
+                      ("verify", rms, n * (L + 1)))
+    prow = pmc_row(f"{kname}_fixed_{L}_{n}")
+    del tx, rx
+    return {"workload": f"C4 shard: {n} x {L}B frames, TX compute + RX verify per step",
+            "gpkt_per_s": 2 * n * steps / el / 1e9, "ms_per_step": el / steps * 1e3,
+            "compute_ms": tms, "verify_ms": rms,
+            "tx_write_mode": tx_write_mode(n, stride),
+            "roofline": {"kernel": kname, "achieved": kb / (kms * 1e-3) / 1e9,
+                         "frac": kb / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "traffic": prow["hbm_bytes_per_launch"] if prow else None,
+                         "traffic_source": (f"profiles/pmc_summary.json configs[{kname}_fixed_"
+                                            f"{L}_{n}]" if prow else None)},
+            "verify_frac": n * (L + 1) / (rms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "compute_frac": n * (L + 4) / (tms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "corrupted_frames_detected": bad}
+
+
 def gpucsum_K():
     from mtcp_amd import gpucsum
     return gpucsum.K
@@ -640,6 +692,7 @@ def main():
             "traffic_source": (f"profiles/pmc_summary.json configs[{kname}_fixed_{L}_{n}]"
                                if prow else None),
             "bytes_per_launch_algorithmic": kbytes, "avg_launch_ms": kms,
+            "tx_write_mode": tx_write_mode(n, stride),
         },
         "kernels_ms": {"compute": tx_ms, "verify": rx_ms,
                        "compute_first_last": [tx_list[0], tx_list[-1]],
@@ -660,7 +713,12 @@ def main():
             line["cpu_baseline"] = cpu_baseline(tx, rx, stride, L, args.cpu_seconds,
                                                 args.cpu_sample, torch)
         if not args.no_extras:
+            line["c2_sector_wb"] = c2_sector_wb(ctx, torch, tx, stride, L, n)
+            sec = line["c2_sector_wb"]
+            line["roofline"]["sector_wb_frac"] = sec["sector_frac_peak"]
             del tx, rx
+            torch.cuda.empty_cache()
+            line["c4_shard"] = c4_shard(ctx, torch, args.steps, args.warmup, args.settle_s)
             torch.cuda.empty_cache()
             line["c1_64B"] = c1_small_frames(ctx, torch)
             line["c1_64B_8M"] = c1_small_frames(ctx, torch, n=8 << 20)

@@ -116,6 +116,10 @@ extern "C" {
                                      ICMPOutput does (icmp.c:57-69: checksum = 0, then
                                      ICMPChecksum over the whole message); csums[] then
                                      holds ip | icmp << 16                             */
+#define GCS_CF_SECTOR_WB    0x4u  /* fixed-stride fills: write back only the 64 B sectors
+                                     holding the check fields, never whole 128 B lines
+                                     (the line write-back is chosen by batch size,
+                                     DESIGN.md §4 "TX write-back"; a measurement knob) */
 
 typedef struct gcs_ctx gcs_ctx;
 

@@ -211,6 +211,33 @@ __device__ __forceinline__ uint4 load_chunk(const uint8_t* p, int64_t avail)
     return v;
 }
 
+// One global_load_lds_dwordx4 (LDS-DMA): lane l's 16 B from src land at LDS
+// byte lds_dst + 16*l, lds_dst wave-uniform; no VGPR destination.  M0 is
+// written and restored inside the statement (cdna_hip_programming.md §5.7,
+// the LDS-DMA recipe).  hipcc does not count asm loads: wait with wait_vmcnt.
+template <bool NT>
+__device__ __forceinline__ void glds16(const uint8_t* src, u32 lds_dst)
+{
+    u32 keep;
+    if constexpr (NT)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                     "global_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(src), "s"(lds_dst) : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                     "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(src), "s"(lds_dst) : "memory");
+}
+
+// s_waitcnt vmcnt(N) alone (gfx9 encoding: vmcnt in [3:0] and [15:14]).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt()
+{
+    static_assert(N >= 0 && N < 64, "vmcnt");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+    asm volatile("" ::: "memory");
+}
+
 // ---------------------------------------------------------------------------
 // per-frame work for one group of G lanes
 

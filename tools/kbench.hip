@@ -185,31 +185,7 @@ __global__ void __launch_bounds__(256) k_read_regions(const uint8_t* __restrict_
 
 // ---------------------------------------------------------------------------
 // ---------------------------------------------------------------------------
-// One global_load_lds_dwordx4: lane l's 16 B from src land at LDS byte
-// lds_dst + 16*l (lds_dst wave-uniform).  M0 is written and restored inside
-// the statement (cdna_hip_programming.md §5.7: the LDS-DMA recipe).
-template <bool NT>
-__device__ __forceinline__ void glds16(const uint8_t* src, u32 lds_dst)
-{
-    u32 keep;
-    if constexpr (NT)
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                     "global_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep) : "v"(src), "s"(lds_dst) : "memory");
-    else
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                     "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep) : "v"(src), "s"(lds_dst) : "memory");
-}
-
-// s_waitcnt vmcnt(N) alone (gfx9 encoding: vmcnt in [3:0] and [15:14]).
-template <int N>
-__device__ __forceinline__ void wait_vmcnt()
-{
-    static_assert(N >= 0 && N < 64, "vmcnt");
-    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
-    asm volatile("" ::: "memory");
-}
+// glds16 / wait_vmcnt: gcs_device.h
 
 // IMIX fill ceiling: k_read_regions' stream of the block's packed region, then
 // the staged fill's write-back pattern with no fold -- sector 0 of each of the
@@ -853,6 +829,41 @@ int imix_main(uint64_t n, int rounds)
     LANE(true, "F64 CAP32K nt", 64, 32768, true)
     LANE(true, "F32 CAP16K temporal", 32, 16384, false)
     }
+    // round 3: class-split blocks (k_desc_part): one class of one tile per block
+#define PART(C_, OCC_, TAG, NT_, WM_, ...)                                                 \
+    vs.push_back({std::string(C_ ? "compute" : "verify ") + " part " + TAG,                 \
+                  C_ ? cb : vb, [&](hipStream_t st) {                                      \
+        using P_ = PartShape<__VA_ARGS__>;                                                  \
+        hipLaunchKernelGGL((k_desc_part<P_, C_, false, WM_, NT_, OCC_>), part_grid<P_>((u32)n), \
+                           dim3(256), 0, st, C_ ? tx : rx, total, doff, dlen, (u32)n,       \
+                           C_ ? nullptr : v1, nullptr, 0u, Ext{});                          \
+    }});
+    if (getenv("KB_PART")) {   // measured r03: 339-435 us verify (per-block fixed costs)
+    PART(false, 6, "768/256k2/96k2/128 occ6", true, kWM, 768, 256, 2, 96, 2, 128)
+    PART(false, 6, "768/256k2/128k2/192 occ6", true, kWM, 768, 256, 2, 128, 2, 192)
+    PART(true, 6, "768/256k2/96k2/128 occ6 sector nt", false, WM_SECTOR_NT, 768, 256, 2, 96, 2, 128)
+    }
+    // round 3: a block's whole region through LDS (k_desc_region)
+#define REGION(C_, TAG, WM_, ...)                                                          \
+    vs.push_back({std::string(C_ ? "compute" : "verify ") + " region " + TAG,               \
+                  C_ ? cb : vb, [&](hipStream_t st) {                                      \
+        using R_ = RegionShape<__VA_ARGS__>;                                                \
+        hipLaunchKernelGGL((k_desc_region<R_, C_, false, WM_>), dim3((n + R_::F - 1) / R_::F), \
+                           dim3(256), 0, st, C_ ? tx : rx, total, doff, dlen, (u32)n,       \
+                           C_ ? nullptr : v1, nullptr, 0u, Ext{});                          \
+    }});
+    REGION(false, "F64 CAP32K G4 nt", kWM, 64, 32768, 4, true)
+    REGION(false, "F64 CAP32K G8 nt", kWM, 64, 32768, 8, true)
+    REGION(false, "F64 CAP32K G16 nt", kWM, 64, 32768, 16, true)
+    REGION(false, "F48 CAP24K G4 nt", kWM, 48, 24576, 4, true)
+    REGION(false, "F96 CAP40K G4 nt", kWM, 96, 40960, 4, true)
+    REGION(false, "F128 CAP56K G4 nt", kWM, 128, 57344, 4, true)
+    REGION(false, "F64 CAP32K G4 temporal", kWM, 64, 32768, 4, false)
+    REGION(true, "F64 CAP32K G4 nt, sector nt", WM_SECTOR_NT, 64, 32768, 4, true)
+    REGION(true, "F64 CAP32K G4 temporal, sector nt", WM_SECTOR_NT, 64, 32768, 4, false)
+    REGION(true, "F64 CAP32K G4 nt, sector sc1", WM_SECTOR_SC1, 64, 32768, 4, true)
+    REGION(true, "F96 CAP40K G4 nt, sector nt", WM_SECTOR_NT, 96, 40960, 4, true)
+    REGION(true, "F64 CAP32K G8 nt, sector nt", WM_SECTOR_NT, 64, 32768, 8, true)
     vs.push_back({"verify  desc (launch_verify_desc)", vb, [&](hipStream_t st) {
         CK(launch_verify_desc(rx, total, doff, dlen, (u32)n, v1, 0u, st));
     }});
@@ -1537,9 +1548,20 @@ void run_variants(std::vector<Variant>& vs, hipStream_t s, int rounds)
     // KB_ONLY=<substring>: time only the matching variants (profiling runs)
     if (const char* only = std::getenv("KB_ONLY")) {
         std::vector<Variant> keep;
+        // '|' separates alternatives
+        std::vector<std::string> alts;
+        for (std::string a = only; ; ) {
+            const size_t p = a.find('|');
+            alts.push_back(a.substr(0, p));
+            if (p == std::string::npos) break;
+            a = a.substr(p + 1);
+        }
         for (auto& v : vs)
-            if (v.name.find(only) != std::string::npos)
-                keep.push_back(v);
+            for (auto& a : alts)
+                if (v.name.find(a) != std::string::npos) {
+                    keep.push_back(v);
+                    break;
+                }
         vs.swap(keep);
     }
     hipEvent_t e0, e1;
