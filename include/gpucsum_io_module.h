@@ -54,10 +54,18 @@
  *               dpdk_module_func (weak reference): a DPDK build without
  *               ENABLELRO never delivers a frame over 1518 B (jumbo frames off,
  *               dpdk_module.c:112-135), so the rule only ever sees LRO chains.
- * Not supported: an inner get_rptr that is not idempotent per index, e.g.
- * DPDK built with IP_DEFRAG (dpdk_module.c:527-529 reassembles on each call);
- * a frame whose pointer or length changes between the burst's verify and
- * mTCP's get_rptr is dropped and counted in rx_rptr_changed.
+ *   GPUCSUM_INNER_RX_ONCE (IP_DEFRAG)  the inner get_rptr is not idempotent
+ *               per index: DPDK built with IP_DEFRAG feeds each fragment to its
+ *               reassembly table on every call (dpdk_module.c:474-513, 527-529).
+ *               The decorator then calls it exactly once per index, in
+ *               recv_pkts, and serves mTCP's get_rptr from what that call
+ *               returned: a reassembled datagram is verified like any frame, an
+ *               absorbed fragment (NULL) is an inner drop.  Not together with
+ *               RX_CHAINED: ENABLELRO's gather reads the inner's cur_rx_m, which
+ *               follows the last get_rptr call (dpdk_module.c:543-545, 856).
+ * Without RX_ONCE, a frame whose pointer or length changes between the
+ * burst's verify and mTCP's get_rptr is dropped and counted in
+ * rx_rptr_changed.
  *
  * RSS check (optional): with RSS configured (gpucsum_set_rss,
  * or GPUCSUM_RSS_QUEUES=<n> [GPUCSUM_RSS_I40E=1] in the environment) each RX
@@ -131,6 +139,8 @@ io_module_func *gpucsum_get_inner(void);
 
 #define GPUCSUM_INNER_TX_EAGER   0x1u  /* get_wptr may transmit / reuse earlier buffers */
 #define GPUCSUM_INNER_RX_CHAINED 0x2u  /* get_rptr may return multi-segment (LRO) frames */
+#define GPUCSUM_INNER_RX_ONCE    0x4u  /* get_rptr is not idempotent (IP_DEFRAG): call it
+                                          once per index; not with RX_CHAINED */
 /* Shape of the inner module; call after gpucsum_set_inner, before init_handle.
  * rx_seg_max: longest single-segment frame (0 = 1514). */
 int gpucsum_set_inner_caps(uint32_t caps, uint32_t rx_seg_max);

@@ -100,8 +100,11 @@ io_module_func *gpucsum_get_inner(void)
 
 int gpucsum_set_inner_caps(uint32_t caps, uint32_t rx_seg_max)
 {
-	if (!g_inner || (caps & ~(GPUCSUM_INNER_TX_EAGER | GPUCSUM_INNER_RX_CHAINED)) ||
-	    rx_seg_max > 65535)
+	const uint32_t known = GPUCSUM_INNER_TX_EAGER | GPUCSUM_INNER_RX_CHAINED |
+	                       GPUCSUM_INNER_RX_ONCE;
+
+	if (!g_inner || (caps & ~known) || rx_seg_max > 65535 ||
+	    ((caps & GPUCSUM_INNER_RX_ONCE) && (caps & GPUCSUM_INNER_RX_CHAINED)))
 		return GCS_EINVAL;
 	g_caps = caps;
 	g_seg_max = rx_seg_max ? rx_seg_max : GPUCSUM_DEFAULT_SEG_MAX;
@@ -367,7 +370,8 @@ static int32_t gpucsum_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
 	if (rx_reserve(r, (uint32_t)n))
 		die("RX burst arrays", GCS_ENOMEM);
 	/* One pass over the inner burst to learn every frame's address.  get_rptr
-	 * is called again per index when mTCP walks the burst (below). */
+	 * is called again per index when mTCP walks the burst (below), except
+	 * with RX_ONCE, where this is the inner's only call. */
 	for (i = 0; i < n; i++) {
 		r->len[i] = 0;
 		r->ptr[i] = g_inner->get_rptr(ctx, ifidx, i, &r->len[i]);
@@ -414,6 +418,15 @@ static uint8_t *gpucsum_get_rptr(struct mtcp_thread_context *ctx, int ifidx, int
 
 	if (!r || index < 0 || index >= r->n)
 		return g_inner->get_rptr(ctx, ifidx, index, len);
+	if (g_caps & GPUCSUM_INNER_RX_ONCE) {
+		/* the burst pass's call was the inner's one call for this index */
+		if (GCS_V_IS_ERROR(r->verdict[index])) {
+			g->st.rx_errors++;
+			return NULL;
+		}
+		*len = r->len[index];
+		return r->ptr[index];
+	}
 	if (r->verdict[index] == V_INNER) {
 		g->st.rx_inner++;
 		p = g_inner->get_rptr(ctx, ifidx, index, len);

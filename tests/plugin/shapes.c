@@ -13,6 +13,14 @@
  *             assigns the next 64 B-aligned offset; send_pkts may send only
  *             part of the chunk (ps_send_chunk_buf), the rest stays queued;
  *             dev_ioctl NULL (:399).
+ *   dfshape   DPDK with a working IP_DEFRAG (dpdk_module.c:474-513, 527-529):
+ *             get_rptr feeds a fragment to the reassembly table on EVERY call;
+ *             a fragment that does not complete its datagram gives NULL, the
+ *             completing one the reassembled datagram (contiguous here), and a
+ *             fragment fed twice starts a new table entry (NULL).  The
+ *             reference dereferences the NULL of an absorbed fragment at
+ *             dpdk_module.c:530 (*len = m->pkt_len); this shape returns it, as
+ *             a fixed module would.
  *   lroshape  DPDK built with ENABLELRO (dpdk_module.c:399-548, 805-928): RX
  *             mbufs, some of them chains (NIC LRO), *len = pkt_len of the
  *             chain; get_rptr records cur_rx_m (:543-545) and returns NULL for
@@ -279,6 +287,77 @@ io_module_func psshape_module_func = {
 	.load_module = nop_load, .init_handle = nop_init, .link_devices = nop_link,
 	.release_pkt = nop_release, .get_wptr = ps_get_wptr, .send_pkts = ps_send,
 	.get_rptr = ps_get_rptr, .recv_pkts = ps_recv, .select = nop_select,
+	.destroy_handle = nop_destroy, .dev_ioctl = NULL,
+};
+
+/* ---- DPDK + IP_DEFRAG shape -------------------------------------------- */
+
+static struct {
+	uint8_t *frag;          /* per wire frame: 0 plain, 1 absorbed, 2 completes a datagram */
+	uint8_t *whole;         /* per wire frame: its reassembled datagram (frag 2), ROOM each */
+	uint16_t *whole_len;
+	uint8_t *fed;           /* the fragment went to the table already */
+	uint32_t refeeds;
+} DF;
+
+int dfshape_reset(const uint8_t *buf, const uint64_t *off, const uint16_t *len, uint32_t n,
+                  uint32_t burst, const uint8_t *frag, const uint8_t *wbuf,
+                  const uint64_t *woff, const uint16_t *wlen)
+{
+	uint32_t i;
+
+	free(DF.frag);
+	free(DF.whole);
+	free(DF.whole_len);
+	free(DF.fed);
+	memset(&DF, 0, sizeof(DF));
+	DF.frag = calloc(n ? n : 1, 1);
+	DF.whole = calloc(n ? n : 1, ROOM);
+	DF.whole_len = calloc(n ? n : 1, sizeof(uint16_t));
+	DF.fed = calloc(n ? n : 1, 1);
+	if (!DF.frag || !DF.whole || !DF.whole_len || !DF.fed)
+		return -1;
+	for (i = 0; i < n; i++) {
+		DF.frag[i] = frag[i];
+		if (frag[i] == 2) {
+			if (wlen[i] > ROOM)
+				return -1;
+			memcpy(DF.whole + (uint64_t)i * ROOM, wbuf + woff[i], wlen[i]);
+			DF.whole_len[i] = wlen[i];
+		}
+	}
+	return wire_reset() || rx_load(buf, off, len, n, burst);
+}
+
+uint32_t dfshape_refeeds(void) { return DF.refeeds; }
+
+static uint8_t *df_get_rptr(struct mtcp_thread_context *c, int ifidx, int index, uint16_t *len)
+{
+	uint32_t i = R.cur_first + (uint32_t)index;
+	(void)c; (void)ifidx;
+	if (DF.frag[i] == 0) {
+		*len = R.len[i];
+		return R.bufs + (uint64_t)i * ROOM;
+	}
+	if (DF.fed[i]) {                        /* fed again: a fresh, incomplete entry */
+		DF.refeeds++;
+		*len = 0;
+		return NULL;
+	}
+	DF.fed[i] = 1;
+	if (DF.frag[i] == 1) {
+		*len = 0;
+		return NULL;
+	}
+	*len = DF.whole_len[i];
+	return DF.whole + (uint64_t)i * ROOM;
+}
+
+/* RX only: the tests drive no TX through it (the netmap shape's TX is reused) */
+io_module_func dfshape_module_func = {
+	.load_module = nop_load, .init_handle = nop_init, .link_devices = nop_link,
+	.release_pkt = nop_release, .get_wptr = nm_get_wptr, .send_pkts = nm_send,
+	.get_rptr = df_get_rptr, .recv_pkts = nm_recv, .select = nop_select,
 	.destroy_handle = nop_destroy, .dev_ioctl = NULL,
 };
 

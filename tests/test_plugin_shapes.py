@@ -16,7 +16,7 @@ from oracle_lib import Oracle
 from test_plugin import GStats, Stats, load, tx_frames, vtab, H, P  # noqa: F401
 
 MINI_ACCEPT, MINI_ERROR, MINI_RELEASE, MINI_NOT_TCP, MINI_NON_IP, MINI_NULL = range(6)
-TX_EAGER, RX_CHAINED = 0x1, 0x2
+TX_EAGER, RX_CHAINED, RX_ONCE = 0x1, 0x2, 0x4
 vp = C.c_void_p
 
 
@@ -28,6 +28,8 @@ def S(H, P):  # noqa: F811
     H.psshape_partial_sends.restype = C.c_uint32
     H.lroshape_reset.argtypes = [vp, vp, vp, vp, vp, vp, C.c_uint32, C.c_uint32]
     H.lroshape_gathers.restype = C.c_uint32
+    H.dfshape_reset.argtypes = [vp, vp, vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp]
+    H.dfshape_refeeds.restype = C.c_uint32
     H.shape_wire_count.restype = C.c_uint32
     H.shape_wire_frame.argtypes = [C.c_uint32, vp]
     H.mini_send.argtypes = [vp, vp, C.c_int]
@@ -84,7 +86,9 @@ class Decorated:
 
 def test_caps_api(S, P):  # noqa: F811
     assert P.gpucsum_set_inner(vtab(S, "nmshape_module_func")) == 0
-    assert P.gpucsum_set_inner_caps(0x4, 0) != 0            # unknown cap
+    assert P.gpucsum_set_inner_caps(0x8, 0) != 0            # unknown cap
+    assert P.gpucsum_set_inner_caps(RX_ONCE | RX_CHAINED, 0) != 0   # cur_rx_m (LRO gather)
+    assert P.gpucsum_set_inner_caps(RX_ONCE, 0) == 0
     assert P.gpucsum_set_inner_caps(TX_EAGER, 70000) != 0   # seg_max > 65535
     assert P.gpucsum_set_inner_caps(TX_EAGER | RX_CHAINED, 0) == 0
     assert P.gpucsum_get_inner() == vtab(S, "nmshape_module_func")
@@ -314,6 +318,74 @@ def test_lro_gathers_the_right_frame(S, P, burst):  # noqa: F811
         ihl = int(buf[o + 14]) & 15
         hl = 14 + 4 * ihl + 4 * (int(buf[o + 14 + 4 * ihl + 12]) >> 4)
         np.testing.assert_array_equal(pay_hw[k], buf[o + hl:o + L])
+
+
+def defrag_wire(n, seed):
+    """An RX wire for an IP_DEFRAG port: plain frames (some corrupted), absorbed
+    fragments and completing fragments, each of the latter with the datagram
+    the reassembly table hands back (some of those corrupted too)."""
+    rng = np.random.default_rng(seed)
+    buf, off, lens = synth.packed_frames(synth.imix_lengths(n, seed=seed), seed=seed + 1)
+    Oracle().compute_batch(buf, off, lens)
+    synth.corrupt(buf, off, lens, frac_log2=3, seed=seed + 2)
+    u = rng.random(n)
+    frag = np.where(u < 0.15, 1, np.where(u < 0.25, 2, 0)).astype(np.uint8)
+    wb, wo, wl = synth.packed_frames(synth.imix_lengths(n, seed=seed + 3), seed=seed + 4)
+    Oracle().compute_batch(wb, wo, wl)
+    synth.corrupt(wb, wo, wl, frac_log2=2, seed=seed + 5)
+    return buf, off, lens, frag, wb, wo, wl
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("burst", [64, 9])
+def test_defrag_inner_called_once(S, P, burst):  # noqa: F811
+    """DPDK with IP_DEFRAG (dpdk_module.c:474-513, 527-529): get_rptr feeds a
+    fragment to the reassembly table on every call.  With RX_ONCE the
+    decorator calls it once per index and mTCP sees exactly what the inner
+    module alone gives it: the same dispositions, rx_errors and reassembled
+    datagrams verified on the GPU.  Without it the burst pass's call consumes
+    each completing fragment and mTCP's own call re-feeds it (a NULL)."""
+    n = 900
+    buf, off, lens, frag, wb, wo, wl = defrag_wire(n, 90)
+    args = (buf.ctypes.data, off.ctypes.data, lens.ctypes.data, n, burst, frag.ctypes.data,
+            wb.ctypes.data, wo.ctypes.data, wl.ctypes.data)
+
+    def run(iom, ctx):
+        assert S.dfshape_reset(*args) == 0
+        st = Stats()
+        disp = np.zeros(n, np.uint8)
+        assert S.mini_rx_loop(iom, ctx, 0, C.byref(st), disp.ctypes.data, n) == n
+        return st, disp, S.dfshape_refeeds()
+
+    ctx = C.create_string_buffer(64)
+    st_sw, disp_sw, rf_sw = run(vtab(S, "dfshape_module_func"), C.addressof(ctx))
+    assert rf_sw == 0
+    d = Decorated(S, P, "dfshape_module_func", RX_ONCE)
+    try:
+        st_hw, disp_hw, rf_hw = run(d.iom, d.ctx)
+        gst = d.stats()
+    finally:
+        d.close()
+    # a frame the GPU rejects is a NULL from get_rptr, as DPDK's hardware check
+    # gives it (dpdk_module.c:536-542): both count as rx_errors (core.c:794-799)
+    err = lambda x: np.isin(x, [MINI_ERROR, MINI_NULL])  # noqa: E731
+    np.testing.assert_array_equal(err(disp_sw), err(disp_hw))
+    np.testing.assert_array_equal(disp_sw == MINI_ACCEPT, disp_hw == MINI_ACCEPT)
+    assert (st_sw.rx_errors, st_sw.accepted, st_sw.released) == \
+           (st_hw.rx_errors, st_hw.accepted, st_hw.released)
+    assert rf_hw == 0 and gst.rx_rptr_changed == 0
+    done = frag == 2
+    assert (disp_hw[done] == MINI_ACCEPT).sum() > 0 and err(disp_hw[done]).sum() > 0
+    # the default (idempotent inner) mode: completing fragments are lost
+    d = Decorated(S, P, "dfshape_module_func", 0)
+    try:
+        st_x, disp_x, rf_x = run(d.iom, d.ctx)
+        gx = d.stats()
+    finally:
+        d.close()
+    # every completing fragment the GPU accepted was fed again by mTCP's call
+    assert rf_x == gx.rx_rptr_changed > 0
+    assert (disp_x[done] == MINI_NULL).all() and st_x.accepted < st_sw.accepted
 
 
 @pytest.mark.gpu
