@@ -16,7 +16,12 @@
  *   RX loop       core.c:785-801: recv_pkts, get_rptr per index, NULL ->
  *                 rx_errors, else ProcessPacket (eth_in.c:9-60)
  *   TX            SendTCPPacketStandalone (tcp_out.c:135-217) per segment,
- *                 send_pkts every `burst` segments (core.c:846-848)
+ *                 send_pkts every `burst` segments (core.c:846-848); and the
+ *                 data path: SendTCPPacket -> IPOutput (tcp_out.c:223-357,
+ *                 ip_out.c:106-175) over established tcp_streams with their
+ *                 send/recv variables, timestamps and payload copy.  timer.c
+ *                 is compiled in too: SendTCPPacket puts a stream with
+ *                 payload on the RTO list (AddtoRTOList, tcp_out.c:350).
  *
  * Everything beyond the checksum path stays out of reach: ProcessTCPPacket's
  * first call after its checksum prefix is StreamHTSearch (tcp_in.c:1251),
@@ -33,6 +38,8 @@
 #include "mtcp.h"
 #include "eth_in.h"
 #include "tcp_out.h"
+#include "timer.h"
+#include "tcp_in.h"
 
 struct mtcp_config CONFIG;
 
@@ -170,4 +177,88 @@ int refs_tx_tcp(struct io_module_func *iom, struct mtcp_thread_context *ctx, uin
 	}
 	iom->send_pkts(ctx, 0);
 	return (int)n;
+}
+
+/* mTCP's data path: SendTCPPacket (tcp_out.c:223-357) -> IPOutput
+ * (ip_out.c:106-175) -> EthernetOutput over `ns` established streams, as
+ * FlushTCPSendingBuffer / SendControlPacket call it.  Stream j: the tuple in
+ * network order, snd_nxt / rcv_nxt, the receive window and the peer's last
+ * timestamp (echoed in every segment's TS option, tcp_out.c:62-70), MSS 1460
+ * (so payloads up to 1448 B with the 12 B timestamp option).  Segment k goes
+ * out on stream sidx[k] with flags[k] and payload bytes pay_off/pay_len;
+ * cur_ts advances by one per send round.  Returns segments written, or -1 on a
+ * NULL get_wptr that a send round does not cure (tcp_out.c:799-802 retries). */
+int refs_tx_stream(struct io_module_func *iom, struct mtcp_thread_context *ctx, uint32_t ns,
+                   const uint32_t *saddr, const uint16_t *sport, const uint32_t *daddr,
+                   const uint16_t *dport, const uint32_t *snd_nxt, const uint32_t *rcv_nxt,
+                   const uint32_t *rcv_wnd, const uint32_t *ts_recent, uint32_t n,
+                   const uint16_t *sidx, const uint8_t *flags, const uint8_t *payload,
+                   const uint64_t *pay_off, const uint16_t *pay_len, uint32_t burst)
+{
+	tcp_stream *st;
+	struct tcp_send_vars *sv;
+	struct tcp_recv_vars *rv;
+	uint32_t j, k;
+	int ret = (int)n;
+
+	refs_bind(iom, ctx, 7000);
+	refs_mgr.rto_store = InitRTOHashstore();
+	st = calloc(ns, sizeof(*st));
+	sv = calloc(ns, sizeof(*sv));
+	rv = calloc(ns, sizeof(*rv));
+	if (!refs_mgr.rto_store || !st || !sv || !rv) {
+		ret = -1;
+		goto out;
+	}
+	for (j = 0; j < ns; j++) {
+		st[j].sndvar = &sv[j];
+		st[j].rcvvar = &rv[j];
+		st[j].id = j;
+		st[j].saddr = saddr[j];
+		st[j].daddr = daddr[j];
+		st[j].sport = sport[j];
+		st[j].dport = dport[j];
+		st[j].state = TCP_ST_ESTABLISHED;
+		st[j].on_rto_idx = -1;
+		st[j].snd_nxt = snd_nxt[j];
+		st[j].rcv_nxt = rcv_nxt[j];
+		sv[j].iss = snd_nxt[j];
+		sv[j].snd_una = snd_nxt[j];
+		sv[j].mss = TCP_DEFAULT_MSS;
+		sv[j].eff_mss = TCP_DEFAULT_MSS - TCP_OPT_TIMESTAMP_LEN - 2;
+		sv[j].wscale_mine = TCP_DEFAULT_WSCALE;
+		sv[j].nif_out = -1;           /* IPOutput routes it (ip_out.c:114-118) */
+		sv[j].ip_id = (uint16_t)(0x1234 + 97 * j);
+		sv[j].rto = TCP_INITIAL_RTO;
+		rv[j].rcv_wnd = rcv_wnd[j];
+		rv[j].ts_recent = ts_recent[j];
+	}
+	for (k = 0; k < n; k++) {
+		tcp_stream *s = &st[sidx[k] < ns ? sidx[k] : 0];
+		uint8_t *pl = (uint8_t *)payload + pay_off[k];
+		int rc = SendTCPPacket(&refs_mgr, s, refs_mgr.cur_ts, flags[k], pl, pay_len[k]);
+		if (rc == -2) {
+			iom->send_pkts(ctx, 0);
+			refs_mgr.cur_ts++;
+			rc = SendTCPPacket(&refs_mgr, s, refs_mgr.cur_ts, flags[k], pl, pay_len[k]);
+		}
+		if (rc < 0) {
+			ret = -1;
+			goto out;
+		}
+		if (burst && (k + 1) % burst == 0) {
+			iom->send_pkts(ctx, 0);
+			refs_mgr.cur_ts++;
+		}
+	}
+	iom->send_pkts(ctx, 0);
+out:
+	free(st);
+	free(sv);
+	free(rv);
+	if (refs_mgr.rto_store) {
+		free(refs_mgr.rto_store);
+		refs_mgr.rto_store = NULL;
+	}
+	return ret;
 }

@@ -9,7 +9,8 @@
  *                    which records the frame as accepted.
  *   thread_printf    the TRACE_* logger (debug.h:241): output dropped.
  *   everything else  aborts: reaching it would mean the harness left the
- *                    checksum path.
+ *                    checksum path.  (timer.c's list functions are the
+ *                    reference's own, compiled in: SendTCPPacket calls them.)
  */
 #include <setjmp.h>
 #include <stdio.h>
@@ -37,9 +38,6 @@ void thread_printf(void *mtcp, FILE *f, const char *fmt, ...)
 	void name(void) { fprintf(stderr, "ref_stack: trap %s reached\n", #name); abort(); }
 
 TRAP(AddEpollEvent)
-TRAP(AddtoRTOList)
-TRAP(AddtoTimeoutList)
-TRAP(AddtoTimewaitList)
 TRAP(CreateTCPStream)
 TRAP(DestroyTCPStream)
 TRAP(ListenerHTSearch)
@@ -50,9 +48,5 @@ TRAP(RaiseCloseEvent)
 TRAP(RaiseErrorEvent)
 TRAP(RaiseReadEvent)
 TRAP(RaiseWriteEvent)
-TRAP(RemoveFromRTOList)
-TRAP(RemoveFromTimewaitList)
 TRAP(SBRemove)
 TRAP(StreamEnqueue)
-TRAP(UpdateRetransmissionTimer)
-TRAP(UpdateTimeoutList)

@@ -40,6 +40,7 @@ def R():
     L.refs_config.argtypes = [u32]
     L.refs_rx_loop.argtypes = [vp, vp, C.c_int, vp, u32, C.POINTER(C.c_uint64)]
     L.refs_tx_tcp.argtypes = [vp, vp, u32] + [vp] * 11 + [u32]
+    L.refs_tx_stream.argtypes = [vp, vp, u32] + [vp] * 8 + [u32] + [vp] * 5 + [u32]
     L.refs_config(MY_IP)
     return L
 
@@ -121,8 +122,71 @@ def run_tx(H, R, iom, ctx, a, burst):
     return tx_wire(H)
 
 
+def stream_args(n, seed, ns=8):
+    """mTCP's data path: n segments over ns established streams, ACK or
+    ACK|PSH with payloads of 0..1448 B (30 % full MSS), as
+    FlushTCPSendingBuffer sends them (tcp_out.c:560-600)."""
+    rng = np.random.default_rng(seed)
+    be16 = lambda x: ((x >> 8) | (x << 8)) & 0xFFFF  # noqa: E731
+    st = dict(saddr=rng.integers(0, 2**32, ns, dtype=np.uint32),
+              sport=be16(rng.integers(1, 65536, ns)).astype(np.uint16),
+              daddr=rng.integers(0, 2**32, ns, dtype=np.uint32),
+              dport=be16(rng.integers(1, 65536, ns)).astype(np.uint16),
+              snd_nxt=rng.integers(0, 2**32, ns, dtype=np.uint32),
+              rcv_nxt=rng.integers(0, 2**32, ns, dtype=np.uint32),
+              rcv_wnd=rng.integers(0, 1 << 24, ns, dtype=np.uint32),
+              ts_recent=rng.integers(0, 2**32, ns, dtype=np.uint32))
+    plen = rng.integers(0, 1449, n).astype(np.uint16)
+    plen[rng.random(n) < 0.3] = 1448
+    plen[rng.random(n) < 0.1] = 0                                   # pure ACKs
+    flags = np.where(rng.random(n) < 0.3, 0x18, 0x10).astype(np.uint8)
+    pay = rng.integers(0, 256, int(plen.sum()) + 16, dtype=np.uint8)
+    poff = np.zeros(n, np.uint64)
+    np.cumsum(plen[:-1], out=poff[1:])
+    seg = dict(sidx=rng.integers(0, ns, n).astype(np.uint16), flags=flags, payload=pay,
+               pay_off=poff, pay_len=plen)
+    return st, seg
+
+
+def run_tx_stream(H, R, iom, ctx, st, seg, burst):
+    H.synth_reset(64)
+    n = len(seg["flags"])
+    sk = ("saddr", "sport", "daddr", "dport", "snd_nxt", "rcv_nxt", "rcv_wnd", "ts_recent")
+    gk = ("sidx", "flags", "payload", "pay_off", "pay_len")
+    assert R.refs_tx_stream(iom, ctx, len(st["saddr"]), *[st[k].ctypes.data for k in sk], n,
+                            *[seg[k].ctypes.data for k in gk], burst) == n
+    return tx_wire(H)
+
+
 # ---------------------------------------------------------------------------
 # CPU: the reference code over the software path agrees with the oracle
+
+def test_ref_stack_software_data_path_tx(H, R):  # noqa: F811
+    """SendTCPPacket -> IPOutput over the bare module (software folds): every
+    segment verifies, carries its stream's tuple, the NOP NOP TS option with
+    the stream's ts_recent, and the stream's sequence numbers in order."""
+    st, seg = stream_args(600, 31)
+    ctx = C.create_string_buffer(64)
+    wire = run_tx_stream(H, R, vtab(H, "synth_module_func"), C.addressof(ctx), st, seg, 64)
+    assert len(wire) == 600
+    lens = np.array([len(w) for w in wire], np.uint16)
+    off, total = synth.packed_offsets(lens)
+    buf = np.zeros(total + 64, np.uint8)
+    for k, w in enumerate(wire):
+        buf[int(off[k]):int(off[k]) + len(w)] = w
+    assert (Oracle().verify_batch(buf, off, lens) == 0).all()
+    nxt = st["snd_nxt"].astype(np.int64).copy()
+    for k, w in enumerate(wire):
+        j = int(seg["sidx"][k])
+        assert w[14] == 0x45 and w[46] >> 4 == 8                      # ihl 5, doff 8
+        assert int.from_bytes(w[26:30].tobytes(), "little") == int(st["saddr"][j])
+        assert int.from_bytes(w[38:42].tobytes(), "big") == nxt[j] % 2**32
+        assert bytes(w[54:56]) == b"\x01\x01" and w[56] == 8 and w[57] == 10
+        assert int.from_bytes(w[62:66].tobytes(), "big") == int(st["ts_recent"][j])
+        p0 = int(seg["pay_off"][k])
+        np.testing.assert_array_equal(w[66:], seg["payload"][p0:p0 + int(seg["pay_len"][k])])
+        nxt[j] += int(seg["pay_len"][k])
+
 
 def test_ref_stack_software_rx_matches_oracle(H, R):  # noqa: F811
     buf, off, lens = rx_set()
@@ -202,6 +266,22 @@ def test_decorator_under_reference_tx(H, P, R, D, burst):  # noqa: F811
     sw_ctx = C.create_string_buffer(64)
     sw = run_tx(H, R, vtab(H, "synth_module_func"), C.addressof(sw_ctx), a, burst)
     hw = run_tx(H, R, iom, ctx, a, burst)
+    assert len(sw) == len(hw) == 2000
+    for x, y in zip(sw, hw):
+        np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("burst", [64, 1, 1000])
+def test_decorator_under_reference_data_path(H, P, R, D, burst):  # noqa: F811
+    """mTCP's data path (SendTCPPacket -> IPOutput, tcp_out.c:223-357,
+    ip_out.c:106-175: stream state, timestamp options, payload memcpy) over
+    the decorator: wire-identical to the software folds for 2,000 segments."""
+    iom, ctx, _ = D
+    st, seg = stream_args(2000, 40 + burst)
+    sw_ctx = C.create_string_buffer(64)
+    sw = run_tx_stream(H, R, vtab(H, "synth_module_func"), C.addressof(sw_ctx), st, seg, burst)
+    hw = run_tx_stream(H, R, iom, ctx, st, seg, burst)
     assert len(sw) == len(hw) == 2000
     for x, y in zip(sw, hw):
         np.testing.assert_array_equal(x, y)
