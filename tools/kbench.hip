@@ -829,6 +829,30 @@ int imix_main(uint64_t n, int rounds)
     LANE(true, "F64 CAP32K nt", 64, 32768, true)
     LANE(true, "F32 CAP16K temporal", 32, 16384, false)
     }
+    // round 3: the list passes' loads alone (DescShape PROBE = 1): access pattern vs fold
+    MIXED(false, 6, "6 PROBE loads only", 4, 1, 16, 3, 32, 3, kWM, 256, true, 1, 1, false, true, 0, 1)
+    MIXED(false, 6, "6 PROBE loads only, temporal", 4, 1, 16, 3, 32, 3, kWM, 256, true, 1, 1, false, false, 0, 1)
+    MIXED(false, 6, "6 PROBE loads only K3/K2", 4, 1, 16, 3, 32, 3, kWM, 256, true, 3, 2, false, true, 0, 1)
+    MIXED(false, 8, "8 PROBE loads only", 4, 1, 16, 3, 32, 3, kWM, 256, true, 1, 1, false, true, 0, 1)
+    MIXED(false, 6, "6 PROBE loads only F=512", 4, 1, 16, 3, 32, 3, kWM, 512, true, 1, 1, false, true, 0, 1)
+    vs.push_back({"verify  mixed PROBE loads only, 6 blocks/CU (LDS pad)", vb, [&](hipStream_t st) {
+        using S_ = DescShape<4, 1, 16, 3, 32, 3, kWM, 256, true, 1, 1, false, true, 0, 1>;
+        hipLaunchKernelGGL((k_desc_mixed<S_, false, true, 6>), dim3((n + 255) / 256), dim3(256),
+                           22 * 1024, st, rx, total, doff, dlen, (u32)n, v1, nullptr, 0u);
+    }});
+    vs.push_back({"verify  mixed shipped, 6 blocks/CU (LDS pad)", vb, [&](hipStream_t st) {
+        using S_ = DescShip<false>;
+        hipLaunchKernelGGL((k_desc_mixed<S_, false, true, 6>), dim3((n + 255) / 256), dim3(256),
+                           22 * 1024, st, rx, total, doff, dlen, (u32)n, v1, nullptr, 0u);
+    }});
+    // round 3: shared 128 B lines read once, through LDS (DescShape EDGE)
+    MIXED(false, 6, "6 EDGE64", 4, 1, 16, 3, 32, 3, kWM, 256, true, 1, 1, false, true, 0, 0, 64)
+    MIXED(false, 6, "6 EDGE96", 4, 1, 16, 3, 32, 3, kWM, 256, true, 1, 1, false, true, 0, 0, 96)
+    MIXED(false, 6, "6 EDGE96 K3/K2", 4, 1, 16, 3, 32, 3, kWM, 256, true, 3, 2, false, true, 0, 0, 96)
+    MIXED(false, 6, "6 PROBE loads only EDGE96", 4, 1, 16, 3, 32, 3, kWM, 256, true, 1, 1, false, true, 0, 1, 96)
+    MIXED(true, 6, "6 STAGE nt, temporal loads EDGE64", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true, false, 0, 0, 64)
+    MIXED(true, 6, "6 STAGE nt, nt loads EDGE96", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true, true, 0, 0, 96)
+    MIXED(true, 5, "5 STAGE nt, temporal loads EDGE96", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true, false, 0, 0, 96)
     // round 3: class-split blocks (k_desc_part): one class of one tile per block
 #define PART(C_, OCC_, TAG, NT_, WM_, ...)                                                 \
     vs.push_back({std::string(C_ ? "compute" : "verify ") + " part " + TAG,                 \
@@ -852,18 +876,12 @@ int imix_main(uint64_t n, int rounds)
                            dim3(256), 0, st, C_ ? tx : rx, total, doff, dlen, (u32)n,       \
                            C_ ? nullptr : v1, nullptr, 0u, Ext{});                          \
     }});
+    if (getenv("KB_REGION")) {   // measured r03: 501-783 us verify, 546-742 us fill (the fold
+                                 // from LDS: 4-way bank conflicts, group-divergent loops)
     REGION(false, "F64 CAP32K G4 nt", kWM, 64, 32768, 4, true)
-    REGION(false, "F64 CAP32K G8 nt", kWM, 64, 32768, 8, true)
-    REGION(false, "F64 CAP32K G16 nt", kWM, 64, 32768, 16, true)
     REGION(false, "F48 CAP24K G4 nt", kWM, 48, 24576, 4, true)
-    REGION(false, "F96 CAP40K G4 nt", kWM, 96, 40960, 4, true)
-    REGION(false, "F128 CAP56K G4 nt", kWM, 128, 57344, 4, true)
-    REGION(false, "F64 CAP32K G4 temporal", kWM, 64, 32768, 4, false)
     REGION(true, "F64 CAP32K G4 nt, sector nt", WM_SECTOR_NT, 64, 32768, 4, true)
-    REGION(true, "F64 CAP32K G4 temporal, sector nt", WM_SECTOR_NT, 64, 32768, 4, false)
-    REGION(true, "F64 CAP32K G4 nt, sector sc1", WM_SECTOR_SC1, 64, 32768, 4, true)
-    REGION(true, "F96 CAP40K G4 nt, sector nt", WM_SECTOR_NT, 96, 40960, 4, true)
-    REGION(true, "F64 CAP32K G8 nt, sector nt", WM_SECTOR_NT, 64, 32768, 8, true)
+    }
     vs.push_back({"verify  desc (launch_verify_desc)", vb, [&](hipStream_t st) {
         CK(launch_verify_desc(rx, total, doff, dlen, (u32)n, v1, 0u, st));
     }});
