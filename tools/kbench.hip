@@ -235,6 +235,399 @@ __global__ void __launch_bounds__(256) k_fill_ceiling(uint8_t* __restrict__ p,
 }
 
 // ---------------------------------------------------------------------------
+// MEASURED, NOT SHIPPED (round 3, DESIGN.md §4 "IMIX, round 3"): the class-split
+// blocks (k_desc_part: 339-435 us verify) and the whole block region through LDS
+// (k_desc_region: 501-783 us verify) on C3, against the list kernel's 276 us.
+// ---------------------------------------------------------------------------
+// Class-split descriptor batch (C3 IMIX and other large device batches).
+// k_desc_mixed walks three size-class lists one after another inside each
+// block: ~13 dependent trips per block (its descriptors, then 3 + 6 + 3 list
+// trips for 256 IMIX frames), most of them carrying only 4-12 KiB.  Here each
+// block does ONE class of one tile: the batch is cut into super-tiles of ST
+// frames, and each super-tile into tiles of T0 / T1 / T2 frames, one block per
+// (tile, class).  A block reads its tile's descriptors (one per thread,
+// temporal loads: the tile's other classes' blocks are its neighbours in
+// dispatch order on the same XCD, so they find those lines in L2), keeps its
+// own class's frames (ballot + prefix: frame order), and runs them on that
+// class's group shape -- usually in one trip, with every group of every wave
+// doing the same kind of frame.  The tile sizes give each class about one
+// trip of work per block.  Class-0 blocks also report the tile's bad
+// descriptors.  Outputs go straight from LDS to their frames' slots, only for
+// the block's own frames (the other classes' blocks write the rest).
+template <int ST_, int T0_, int K0_, int T1_, int K1_, int T2_, bool STAGE_ = false,
+          int G0_ = 4, int U0_ = 1>
+struct PartShape {
+    static constexpr int ST = ST_, T0 = T0_, T1 = T1_, T2 = T2_, K0 = K0_, K1 = K1_;
+    static constexpr bool STAGE = STAGE_;
+    static_assert(ST % T0 == 0 && ST % T1 == 0 && ST % T2 == 0, "whole tiles per super-tile");
+    static_assert(T0 <= kBlock && T1 <= kBlock && T2 <= kBlock, "one descriptor per thread");
+    static constexpr int NB0 = ST / T0, NB1 = ST / T1, NB2 = ST / T2, NB = NB0 + NB1 + NB2;
+    // class shapes: as DescShip (class 0: G0 x U0 lanes; class 1: 16 x 3; class 2: 32 x 3, looping)
+    static constexpr int G0 = G0_, U0 = U0_, G1 = 16, U1 = 3, G2 = 32, U2 = 3;
+    static constexpr int C0 = 16 * G0 * U0, C1 = 16 * G1 * U1;   // class bounds (bytes)
+};
+
+template <class P, bool COMPUTE, bool EXT, int WM, bool NT>
+__device__ __forceinline__ void desc_part(uint8_t* __restrict__ frames, uint64_t frames_bytes,
+                                          const uint64_t* __restrict__ off,
+                                          const uint16_t* __restrict__ lens, u32 n,
+                                          uint8_t* __restrict__ out_code,
+                                          uint32_t* __restrict__ out_csum, u32 flags,
+                                          const Ext& ext)
+{
+    __shared__ uint64_t soff[kBlock];
+    __shared__ uint16_t slen[kBlock];
+    __shared__ uint16_t list[kBlock];
+    __shared__ int wcnt[kBlock / 64];
+    __shared__ uint8_t codes[kBlock];
+    __shared__ uint32_t csums[COMPUTE ? kBlock : 1];
+    __shared__ uint32_t hashes[EXT && !COMPUTE ? kBlock : 1];
+    __shared__ uint16_t queues[EXT && !COMPUTE ? kBlock : 1];
+    __shared__ uint4 stage[COMPUTE && P::STAGE ? 4 * kBlock : 1];
+    const uint32_t b = kXCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t sup = b / P::NB, k = b % P::NB;
+    // class 2 tiles first in dispatch order (the longest blocks), class 0 last
+    int my;
+    uint32_t tile, T;
+    if (k < (uint32_t)P::NB2) {
+        my = 2; tile = k; T = P::T2;
+    } else if (k < (uint32_t)(P::NB2 + P::NB1)) {
+        my = 1; tile = k - P::NB2; T = P::T1;
+    } else {
+        my = 0; tile = k - P::NB2 - P::NB1; T = P::T0;
+    }
+    const uint64_t f0 = (uint64_t)sup * P::ST + (uint64_t)tile * T;
+    if (f0 >= n)
+        return;                                        // block-uniform
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint64_t i = f0 + t;
+    bool mine = false, listed = false;
+    if (t < (int)T && i < n) {
+        const uint64_t o = off[i];
+        const u32 len = lens[i];
+        const bool ok = (o & 15) == 0 && o <= frames_bytes && len <= frames_bytes - o;
+        if (!ok) {
+            mine = my == 0;                            // class-0 blocks report bad descriptors
+            codes[t] = COMPUTE ? GCS_TX_BAD_DESC : GCS_V_BAD_DESC;
+            if (COMPUTE)
+                csums[t] = 0;
+            if (EXT && !COMPUTE) {
+                hashes[t] = 0;
+                queues[t] = 0xFFFF;
+            }
+        } else {
+            const int c = len <= (u32)P::C0 ? 0 : (len <= (u32)P::C1 ? 1 : 2);
+            listed = mine = c == my;
+            soff[t] = o;
+            slen[t] = (uint16_t)len;
+        }
+    }
+    // the block's own frames of its class, in frame order
+    const uint64_t m = __ballot(listed);
+    if (lane == 0)
+        wcnt[w] = __popcll(m);
+    __syncthreads();
+    int base = 0, count = 0;
+#pragma unroll
+    for (int q = 0; q < kBlock / 64; q++) {
+        base += q < w ? wcnt[q] : 0;
+        count += wcnt[q];
+    }
+    if (listed)
+        list[base + __popcll(m & ((1ull << lane) - 1))] = (uint16_t)t;
+    __syncthreads();
+    if (count) {
+        uint32_t* hl = EXT && !COMPUTE ? hashes : nullptr;
+        uint16_t* ql = EXT && !COMPUTE ? queues : nullptr;
+        uint4* stg = COMPUTE && P::STAGE ? stage : nullptr;
+        if (my == 0)
+            desc_class<P::G0, P::U0, COMPUTE, false, EXT, WM, P::K0, NT>(frames, frames_bytes, soff, slen, list, count, flags, codes, csums, ext, hl, ql, stg);
+        else if (my == 1)
+            desc_class<P::G1, P::U1, COMPUTE, false, EXT, WM, P::K1, NT>(frames, frames_bytes, soff, slen, list, count, flags, codes, csums, ext, hl, ql, stg);
+        else
+            desc_class<P::G2, P::U2, COMPUTE, true, EXT, WM, 1, NT>(frames, frames_bytes, soff, slen, list, count, flags, codes, csums, ext, hl, ql, stg);
+    }
+    __syncthreads();                                   // codes / stage complete
+    if (COMPUTE && P::STAGE && !(flags & GCS_CF_NO_INPLACE)) {
+        // the listed frames' staged sector-0 write-backs, in frame order, four
+        // lanes per sector (desc_tail's rule: a status that fills, inside the
+        // frame and the buffer)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int q = r * kBlock + t, j = q >> 2, c = q & 3;
+            if (j >= count)
+                continue;
+            const int ft = list[j];
+            const u32 st = codes[ft];
+            const bool wip = st == GCS_TX_OK || st == GCS_TX_IP_ONLY || st == GCS_TX_BAD_TCPLEN ||
+                             (EXT && (st == GCS_TX_ICMP_OK || st == GCS_TX_BAD_ICMPLEN));
+            if (!wip || 16 * c >= (int)slen[ft])
+                continue;
+            const uint64_t ob = soff[ft] + 16 * c;
+            if (ob + 16 <= frames_bytes)
+                stg16<WM>(frames + ob, stage[4 * ft + c]);
+        }
+    }
+    if (!mine)
+        return;
+    if (out_code)
+        out_code[i] = codes[t];
+    if (COMPUTE && out_csum)
+        out_csum[i] = csums[t];
+    if (EXT && !COMPUTE) {
+        if (ext.hash)
+            ext.hash[i] = hashes[t];
+        if (ext.queue)
+            ext.queue[i] = queues[t];
+    }
+}
+
+template <class P, bool COMPUTE, bool EXT, int WM, bool NT, int OCC = 1>
+__global__ void __launch_bounds__(kBlock, OCC)
+k_desc_part(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __restrict__ off,
+            const uint16_t* __restrict__ lens, u32 n, uint8_t* __restrict__ out_code,
+            uint32_t* __restrict__ out_csum, u32 flags, Ext ext)
+{
+    desc_part<P, COMPUTE, EXT, WM, NT>(frames, frames_bytes, off, lens, n, out_code, out_csum,
+                                       flags, ext);
+}
+
+template <class P>
+__host__ inline dim3 part_grid(u32 n)
+{
+    return dim3((unsigned)(((uint64_t)n + P::ST - 1) / P::ST * P::NB));
+}
+
+// ---------------------------------------------------------------------------
+// Descriptor batch through LDS (C3 IMIX; PSIO-packed batches, pslib.c:132-156).
+// A block takes F consecutive descriptors and moves the bytes they cover,
+// [lo, hi), into LDS with LDS-DMA: 1 KiB per wave instruction, every 16 B of
+// the region read once and coalesced, all of a block's region in flight at
+// once and no VGPRs held for it.  Groups of G lanes then fold the frames out
+// of LDS with the shared per-frame code (masks, reductions, epilogue).  The
+// list kernel's problem was its ~13 dependent HBM trips per block, most with
+// 4-12 KiB in flight; here a block makes two (its descriptors, its region)
+// with the whole region in flight.  A frame whose bytes lie past the first
+// CAP bytes of the region (a tile of large frames; descriptors that are not
+// packed) is folded from global memory by its group instead.  A TX fill
+// patches sector 0 of each LDS frame inside the region and stores the
+// sectors in frame order at the end, four lanes per sector (the staged
+// write-back of the list kernel).
+template <int F_, int CAP_, int G_, bool LNT_, int OCC_ = 1>
+struct RegionShape {
+    static constexpr int F = F_, CAP = CAP_, G = G_, OCC = OCC_;
+    static constexpr bool LNT = LNT_;
+    static_assert(CAP % 1024 == 0, "whole DMA instructions");
+    static_assert(G == 4 || G == 8 || G == 16, "group shapes with U = 8 / G chunks in v");
+    static constexpr int U = 8 / G > 0 ? 8 / G : 1;   // v: the frame's chunks 0..7 (held for the epilogue)
+};
+
+template <class R, bool COMPUTE, bool EXT, int WM>
+__device__ __forceinline__ void region_frame(const uint8_t* __restrict__ lsrc, uint8_t* __restrict__ f,
+                                             u32 len, int64_t avail, bool active, bool in_lds,
+                                             int sub, u32 flags, uint8_t* code, uint32_t* csum,
+                                             const XFrame& xf, uint8_t* stage)
+{
+    constexpr int G = R::G, U = R::U;
+    const int nch = active ? (int)((len + 15) >> 4) : 0;
+    auto rd = [&](int c) -> uint4 {
+        if (in_lds)
+            return *reinterpret_cast<const uint4*>(lsrc + 16 * c);
+        return load_chunk<true, R::LNT>(f + 16 * c, avail - 16 * c);
+    };
+    uint4 v[U];
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+        const int c = j * G + sub;
+        v[j] = c < nch ? rd(c) : make_uint4(0, 0, 0, 0);
+    }
+    Hdr h;
+    h.d3 = group_bcast<G, 0>(v[0].w);
+    h.d4 = group_bcast<G, 1>(v[0].x);
+    h.d5 = group_bcast<G, 1>(v[0].y);
+    const int ts = 14 + 4 * (int)((h.d3 >> 16) & 15u);
+    const int te = 14 + (int)bswap16(h.d4 & 0xFFFFu);
+    Acc a = {0u, 0u, 0u};
+    const bool fast = __all(ts == 34 || !active);   // wave-uniform: ihl == 5 everywhere
+    if (fast) {
+        const Mask5 m = masks5<COMPUTE>(sub);
+        accum_fast5<COMPUTE, true>(v[0], sub, te, m, a);
+#pragma unroll
+        for (int j = 1; j < U; j++)
+            accum_fast5<COMPUTE, false>(v[j], j * G + sub, te, m, a);
+    } else {
+#pragma unroll
+        for (int j = 0; j < U; j++)
+            accum_chunk<COMPUTE>(v[j], 16 * (j * G + sub), ts, te, a);
+    }
+    // chunks 8.. (ts <= 74, so no header field lies past chunk 5; the check
+    // field of a long IP header is in v): the TCP segment's interior or tail
+    for (int c0 = U * G; c0 < nch; c0 += 4 * G) {      // group-divergent trip count
+        uint4 w[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int c = c0 + u * G + sub;
+            w[u] = c < nch ? rd(c) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int c = c0 + u * G + sub;
+            if (fast) {
+                accum_fast5<COMPUTE, false>(w[u], c, te, Mask5{}, a);
+            } else {
+                accum_chunk<COMPUTE>(w[u], 16 * c, ts, te, a);
+            }
+        }
+    }
+    epilogue<G, U, COMPUTE, WM, EXT>(h, a, f, len, avail, true, sub, flags, code,
+                                     COMPUTE ? csum : nullptr, active, v, xf, stage);
+}
+
+template <class R, bool COMPUTE, bool EXT, int WM>
+__device__ __forceinline__ void desc_region(uint8_t* __restrict__ frames, uint64_t frames_bytes,
+                                            const uint64_t* __restrict__ off,
+                                            const uint16_t* __restrict__ lens, u32 n,
+                                            uint8_t* __restrict__ out_code,
+                                            uint32_t* __restrict__ out_csum, u32 flags,
+                                            const Ext& ext)
+{
+    constexpr int F = R::F, CAP = R::CAP, G = R::G, NG = kBlock / G, NW = kBlock / 64;
+    static_assert(F <= kBlock, "one descriptor per thread");
+    __shared__ __attribute__((aligned(16))) uint8_t region[CAP];
+    __shared__ uint64_t soff[F];
+    __shared__ uint16_t slen[F];
+    __shared__ uint8_t sin[F];          // 0: bad descriptor, 1: frame in LDS, 2: from global memory
+    __shared__ uint8_t codes[F];
+    __shared__ uint32_t csums[COMPUTE ? F : 1];
+    __shared__ uint32_t hashes[EXT && !COMPUTE ? F : 1];
+    __shared__ uint16_t queues[EXT && !COMPUTE ? F : 1];
+    __shared__ uint64_t red[2][NW];
+    const uint32_t blk = kXCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint64_t f0 = (uint64_t)blk * F;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    // phase 0: descriptors, and the block's region [lo, hi) over its valid frames
+    uint64_t o = 0, lo = ~0ull, hi = 0;
+    u32 len = 0;
+    bool ok = false;
+    if (t < F && f0 + t < n) {
+        o = off[f0 + t];
+        len = lens[f0 + t];
+        ok = (o & 15) == 0 && o <= frames_bytes && len <= frames_bytes - o;
+        soff[t] = ok ? o : 0;
+        slen[t] = (uint16_t)len;
+        if (ok) {
+            lo = o;
+            hi = (o + len + 15) & ~15ull;
+        } else {
+            sin[t] = 0;
+            codes[t] = COMPUTE ? GCS_TX_BAD_DESC : GCS_V_BAD_DESC;
+            if (COMPUTE)
+                csums[t] = 0;
+            if (EXT && !COMPUTE) {
+                hashes[t] = 0;
+                queues[t] = 0xFFFF;
+            }
+        }
+    }
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t l2 = __shfl_xor(lo, d, 64), h2 = __shfl_xor(hi, d, 64);
+        lo = l2 < lo ? l2 : lo;
+        hi = h2 > hi ? h2 : hi;
+    }
+    if (lane == 0) {
+        red[0][w] = lo;
+        red[1][w] = hi;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NW; q++) {
+        lo = red[0][q] < lo ? red[0][q] : lo;
+        hi = red[1][q] > hi ? red[1][q] : hi;
+    }
+    // LDS holds [lo, dend): at most CAP bytes, never past the buffer's last
+    // whole 16 B chunk (every DMA source stays inside the buffer)
+    const uint64_t bend = frames_bytes & ~15ull;
+    uint64_t dend = hi < bend ? hi : bend;
+    if (dend < lo)
+        dend = lo;                                     // no valid frame: nothing to move
+    if (dend - lo > (uint64_t)CAP)
+        dend = lo + CAP;
+    if (t < F && ok)
+        sin[t] = o + ((len + 15) & ~15u) <= dend ? 1 : 2;
+    if (dend > lo) {
+        const u32 base = (u32)(uintptr_t)region;
+        const int nins = (int)((dend - lo + 1023) >> 10);
+        for (int q = w; q < nins; q += NW) {
+            const uint64_t g = lo + 1024ull * q + 16ull * lane;
+            glds16<R::LNT>(frames + (g < dend ? g : dend - 16),
+                           __builtin_amdgcn_readfirstlane(base + 1024u * (u32)q));
+        }
+        wait_vmcnt<0>();
+    }
+    __syncthreads();
+    // phase 1: fold, one frame per group of G lanes at a time
+    const int g = t / G, sub = t & (G - 1);
+    for (int ft0 = 0; ft0 < F; ft0 += NG) {            // block-uniform
+        const int ft = ft0 + g;
+        const bool act = ft < F && f0 + ft < n && sin[ft] != 0;
+        const int fs = act ? ft : 0;
+        const uint64_t fo = act ? soff[fs] : 0;
+        const bool in_lds = act && sin[fs] == 1;
+        XFrame xf{};
+        if constexpr (EXT && !COMPUTE)
+            if (ext.hash || ext.queue)
+                xf = XFrame{{ext.key[0], ext.key[1], ext.key[2], ext.key[3]},
+                            hashes + fs, queues + fs, ext.nq, ext.nq_magic, ext.endian, nullptr};
+        region_frame<R, COMPUTE, EXT, WM>(region + (in_lds ? fo - lo : 0), frames + fo,
+                                          act ? slen[fs] : 0u, (int64_t)(frames_bytes - fo), act,
+                                          in_lds, sub, flags, codes + fs, csums + fs, xf,
+                                          COMPUTE && in_lds ? region + (fo - lo) : nullptr);
+    }
+    __syncthreads();
+    if (COMPUTE && !(flags & GCS_CF_NO_INPLACE)) {
+        // sector 0 of every LDS frame from the region, in frame order, four
+        // lanes per sector (two packed 64 B frames make one whole line)
+#pragma unroll
+        for (int r = 0; r < (4 * F + kBlock - 1) / kBlock; r++) {
+            const int q = r * kBlock + t, ft = q >> 2, c = q & 3;
+            if (ft >= F || f0 + ft >= n || sin[ft] != 1)
+                continue;
+            const u32 st = codes[ft];
+            const bool wip = st == GCS_TX_OK || st == GCS_TX_IP_ONLY || st == GCS_TX_BAD_TCPLEN ||
+                             (EXT && (st == GCS_TX_ICMP_OK || st == GCS_TX_BAD_ICMPLEN));
+            if (!wip || 16 * c >= (int)slen[ft])
+                continue;
+            const uint64_t ob = soff[ft] + 16 * c;
+            stg16<WM>(frames + ob, *reinterpret_cast<const uint4*>(region + (ob - lo)));
+        }
+    }
+    if (t < F && f0 + t < n) {
+        const uint64_t i = f0 + t;
+        if (out_code)
+            out_code[i] = codes[t];
+        if (COMPUTE && out_csum)
+            out_csum[i] = csums[t];
+        if (EXT && !COMPUTE) {
+            if (ext.hash)
+                ext.hash[i] = hashes[t];
+            if (ext.queue)
+                ext.queue[i] = queues[t];
+        }
+    }
+}
+
+template <class R, bool COMPUTE, bool EXT, int WM>
+__global__ void __launch_bounds__(kBlock, R::OCC)
+k_desc_region(uint8_t* __restrict__ frames, uint64_t frames_bytes,
+              const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens, u32 n,
+              uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags, Ext ext)
+{
+    desc_region<R, COMPUTE, EXT, WM>(frames, frames_bytes, off, lens, n, out_code, out_csum,
+                                     flags, ext);
+}
+
+// ---------------------------------------------------------------------------
 // MEASURED, NOT SHIPPED ("IMIX one frame per lane").
 // Descriptor batches, one frame per lane out of LDS (C3 IMIX).  A one-wave
 // block takes F consecutive descriptors.  When their frames lie within CAP
@@ -845,14 +1238,9 @@ int imix_main(uint64_t n, int rounds)
         hipLaunchKernelGGL((k_desc_mixed<S_, false, true, 6>), dim3((n + 255) / 256), dim3(256),
                            22 * 1024, st, rx, total, doff, dlen, (u32)n, v1, nullptr, 0u);
     }});
-    // round 3: shared 128 B lines read once, through LDS (DescShape EDGE)
-    MIXED(false, 6, "6 EDGE64", 4, 1, 16, 3, 32, 3, kWM, 256, true, 1, 1, false, true, 0, 0, 64)
-    MIXED(false, 6, "6 EDGE96", 4, 1, 16, 3, 32, 3, kWM, 256, true, 1, 1, false, true, 0, 0, 96)
-    MIXED(false, 6, "6 EDGE96 K3/K2", 4, 1, 16, 3, 32, 3, kWM, 256, true, 3, 2, false, true, 0, 0, 96)
-    MIXED(false, 6, "6 PROBE loads only EDGE96", 4, 1, 16, 3, 32, 3, kWM, 256, true, 1, 1, false, true, 0, 1, 96)
-    MIXED(true, 6, "6 STAGE nt, temporal loads EDGE64", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true, false, 0, 0, 64)
-    MIXED(true, 6, "6 STAGE nt, nt loads EDGE96", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true, true, 0, 0, 96)
-    MIXED(true, 5, "5 STAGE nt, temporal loads EDGE96", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true, false, 0, 0, 96)
+    // round 3: the shared-line (EDGE) list variant -- lines shared by neighbouring
+    // frames of different classes read once into LDS -- measured 350-356 us verify,
+    // 451-531 us fill (its loads alone 247 vs 251 us); removed from the kernels
     // round 3: class-split blocks (k_desc_part): one class of one tile per block
 #define PART(C_, OCC_, TAG, NT_, WM_, ...)                                                 \
     vs.push_back({std::string(C_ ? "compute" : "verify ") + " part " + TAG,                 \
