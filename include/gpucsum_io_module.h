@@ -165,6 +165,7 @@ struct gpucsum_stats {
 	uint64_t rx_inner;       /* RX_CHAINED: chained frames left to the inner's checks */
 	uint64_t rx_rptr_changed;/* inner get_rptr changed a frame after its verify   */
 	uint64_t tx_inner_full;  /* TX_EAGER: inner get_wptr had no buffer: frame lost  */
+	uint64_t tx_posts;       /* async TX fill posts (GPUCSUM_TX_GROUP)            */
 };
 int gpucsum_get_stats(struct mtcp_thread_context *ctx, struct gpucsum_stats *out);
 

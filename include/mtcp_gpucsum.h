@@ -288,6 +288,23 @@ int gcs_verify_ptrs(gcs_ctx *ctx, uint8_t *const *pkts, const uint16_t *len,
 int gcs_compute_ptrs(gcs_ctx *ctx, uint8_t *const *pkts, const uint16_t *len,
                      uint32_t n, uint8_t *status, uint32_t *csums);
 
+/* Asynchronous TX fill of a host burst (the plugin fills frames as mTCP
+ * completes them, tcp_out.c:239-333, instead of all at send_pkts).  With the
+ * context's burst server on, the frames are posted to the resident grid and
+ * the call returns at once with *ticket != 0; gcs_wait(ctx, *ticket) then
+ * completes it: status[] / csums[] written (either may be NULL) and every
+ * frame's check fields filled in place.  Until then the frames and the output
+ * arrays must stay valid and the frames unmodified.  Frames all in one
+ * registered region (gcs_host_register) at 16 B-aligned addresses are read
+ * and filled where they are; others are copied into the context's pinned
+ * async staging.  Without the server, or for a batch larger than one request
+ * (512 frames / 256 KiB staged), the fill runs synchronously and *ticket = 0.
+ * gcs_wait(ctx, t) completes every async fill posted on ctx up to ticket t;
+ * gcs_wait(ctx, 0) does nothing. */
+int gcs_compute_ptrs_async(gcs_ctx *ctx, uint8_t *const *pkts, const uint16_t *len,
+                           uint32_t n, uint8_t *status, uint32_t *csums, uint64_t *ticket);
+int gcs_wait(gcs_ctx *ctx, uint64_t ticket);
+
 /* Host-memory RX verify + RSS steering (see gcs_classify_dev); hash or queue
  * may be NULL, not both.  The host entry points take GCS_VF_ICMP as well. */
 int gcs_classify(gcs_ctx *ctx, uint8_t *frames, const uint64_t *off,

@@ -233,18 +233,20 @@ class GatherPool {
 namespace {
 
 // Host side of the burst server (gcs_kernels.hip k_burst_server): small host
-// batches in direct mode are posted to a resident grid through a mailbox in
-// pinned fine-grained memory, instead of one kernel launch + event wait each.
-// The grid lives at most life_us and leaves after idle_us without work; a
-// batch posted to a grid that has gone (or is going) is served by a fresh
-// launch, so every batch completes and the grid never outlives its bounds.
+// batches in direct mode are posted to a resident grid through a ring of
+// request slots in pinned fine-grained memory, instead of one kernel launch +
+// event wait each.  post() returns at once; wait(q) completes every request up
+// to q, in order.  The grid lives at most life_us and leaves after idle_us
+// without work; requests posted to a grid that has gone (or is going) are
+// served by a fresh launch, so every request completes and the grid never
+// outlives its bounds.
 class BurstServer {
   public:
     ~BurstServer()
     {
         if (prof_ && prof_n_)
             std::fprintf(stderr,
-                         "[gcs burst server] %llu requests: request writes %.2f us; post->ack "
+                         "[gcs burst server] %llu requests: request writes %.2f us; post->done "
                          "%.2f us, of which serving %.2f us and release fence %.2f us "
                          "(slowest block)\n",
                          (unsigned long long)prof_n_, prof_write_ / prof_n_, prof_total_ / prof_n_,
@@ -272,94 +274,161 @@ class BurstServer {
         // test-only (tests/test_gpu_host.py): start the request numbers near a
         // 16-bit tag or 32-bit wrap instead of after 65k real bursts
         if (const char* s = std::getenv("GCS_SERVER_SEQ_START"))
-            seq_ = (uint32_t)std::strtoul(s, nullptr, 0);
+            posted_ = done_ = (uint32_t)std::strtoul(s, nullptr, 0);
         return GCS_OK;
     }
 
-    // Serve one request (n <= gcs::kServerMaxFrames): frames at device address
+    // Post one request (n <= gcs::kSlotFrames): frames at device address
     // `frames` (bytes, a multiple of 16), frame i at off[i], len[i] bytes.
-    // Returns when every block has acknowledged it, with the verdicts /
-    // statuses in code[] and, for a fill, the checks in csum[].
-    // in_place: the kernel writes the frames themselves (host memory), so the
-    // call also waits for every block's release + ack; otherwise the tagged
-    // result records alone complete it.
-    int serve(uint8_t* frames, uint64_t bytes, const uint64_t* off, const uint16_t* len,
-              uint32_t n, bool compute, uint32_t flags, uint8_t* code, uint32_t* csum,
-              bool in_place = false)
+    // When it completes (wait), the verdicts / statuses go to code[] and, for a
+    // fill, the checks to csum[]: both must stay valid until then.
+    // in_place: the kernel writes the frames themselves (host memory), so
+    // completion also waits for the serving blocks' release + ack; otherwise
+    // the tagged result records alone complete it.
+    int post(uint8_t* frames, uint64_t bytes, const uint64_t* off, const uint16_t* len,
+             uint32_t n, bool compute, uint32_t flags, uint8_t* code, uint32_t* csum,
+             bool in_place, uint32_t* ticket)
     {
+        const uint32_t q = gcs::server_next(posted_);
+        Req& r = req_[q % gcs::kServerSlots];
+        if (r.pending) {                  // the slot's previous request must be done
+            int rc = wait(r.q);
+            if (rc) return rc;
+        }
         if (launched_ && any_exited()) {
-            int rc = wait_exit();
+            int rc = relaunch();
             if (rc) return rc;
         }
         if (!launched_) {
-            int rc = launch(seq_);
+            int rc = launch();
             if (rc) return rc;
         }
-        // The records carry q's low 16 bits, and cleared records read as tag
-        // 0: a request whose tag would be 0 could look complete before the
-        // grid has read it, so those numbers are never posted (this also
-        // skips 0 itself when seq_ wraps).
-        uint32_t q = ++seq_;
-        if ((q & 0xFFFFu) == 0)
-            q = ++seq_;
-        const uint64_t tag = (uint64_t)(q & 0xFFFFu) << 48;
+        gcs::ServerSlot& sl = mb_->slot[q % gcs::kServerSlots];
         const auto tw = std::chrono::steady_clock::now();
-        std::memset(mb_->rec, 0, n * sizeof(uint64_t));   // no record of an older request
+        std::memset(sl.rec, 0, n * sizeof(uint64_t));   // no record of an older request
         // each 16 B line: its fields, then its seq (x86 keeps the order)
         for (uint32_t i = 0; i < n; i++) {
-            gcs::ServerDesc& d = mb_->desc[i];
+            gcs::ServerDesc& d = sl.desc[i];
             d.off = off[i];
             d.len = len[i];
             __atomic_store_n(&d.seq, q, __ATOMIC_RELEASE);
         }
-        mb_->b.frames = reinterpret_cast<uint64_t>(frames);
-        mb_->b.bytes16 = (uint32_t)(bytes / 16);
-        __atomic_store_n(&mb_->b.seq, q, __ATOMIC_RELEASE);
-        mb_->a.n = n;
-        mb_->a.mode = (compute ? 1u : 0u) | (flags << 1);
+        sl.b.frames = reinterpret_cast<uint64_t>(frames);
+        sl.b.bytes16 = (uint32_t)(bytes / 16);
+        __atomic_store_n(&sl.b.seq, q, __ATOMIC_RELEASE);
+        sl.a.n = n;
+        sl.a.mode = (compute ? 1u : 0u) | (flags << 1);
+        sl.a.cmd = 0;
+        r = Req{q, n, compute, in_place, true, code, csum, 0, std::chrono::steady_clock::now()};
+        __atomic_store_n(&sl.a.seq, q, __ATOMIC_RELEASE);
+        if (prof_)
+            prof_write_ += std::chrono::duration<double, std::micro>(r.t0 - tw).count();
+        posted_ = q;
+        if (ticket) *ticket = q;
+        return GCS_OK;
+    }
+
+    // Complete every posted request up to and including q, in order.
+    int wait(uint32_t q)
+    {
+        while ((int32_t)(q - done_) > 0 && done_ != posted_) {
+            const uint32_t r = gcs::server_next(done_);
+            int rc = complete(req_[r % gcs::kServerSlots]);
+            if (rc) return rc;
+            done_ = r;
+        }
+        return GCS_OK;
+    }
+
+    uint32_t posted() const { return posted_; }
+
+    // Serve one batch (n <= gcs::kServerMaxFrames) and return when it is done.
+    int serve(uint8_t* frames, uint64_t bytes, const uint64_t* off, const uint16_t* len,
+              uint32_t n, bool compute, uint32_t flags, uint8_t* code, uint32_t* csum,
+              bool in_place = false)
+    {
+        uint32_t q = done_;
+        for (uint32_t k = 0; k < n; k += gcs::kSlotFrames) {
+            const uint32_t m = std::min<uint32_t>(gcs::kSlotFrames, n - k);
+            int rc = post(frames, bytes, off + k, len + k, m, compute, flags,
+                          code ? code + k : nullptr, csum ? csum + k : nullptr, in_place, &q);
+            if (rc) return rc;
+        }
+        return wait(q);
+    }
+
+    // Complete what is posted, ask the grid to leave and wait until it has.
+    int stop()
+    {
+        if (!launched_) return GCS_OK;
+        int rc = wait(posted_);
+        for (auto& sl : mb_->slot)
+            __atomic_store_n(&sl.a.cmd, 1u, __ATOMIC_RELEASE);
+        int rc2 = wait_exit();
+        return rc ? rc : rc2;
+    }
+
+  private:
+    struct Req {
+        uint32_t q, n;
+        bool compute, in_place, pending;
+        uint8_t* code;
+        uint32_t* csum;
+        uint32_t have;                               // records [0, have) carry q
+        std::chrono::steady_clock::time_point t0;    // posted
+    };
+
+    // Wait until request r is done (its records, and for an in-place request
+    // the serving blocks' acks), relaunching the grid when it left before.
+    int complete(Req& r)
+    {
+        const uint64_t tag = (uint64_t)(r.q & 0xFFFFu) << 48;
+        gcs::ServerSlot& sl = mb_->slot[r.q % gcs::kServerSlots];
+        const int nb = (int)std::min<uint32_t>(gcs::kServerBlocks,
+                                               (r.n + gcs::kServerFPB - 1) / gcs::kServerFPB);
         const auto t0 = std::chrono::steady_clock::now();
-        __atomic_store_n(&mb_->a.seq, q, __ATOMIC_RELEASE);
-        uint32_t have = 0;                   // records [0, have) carry q
         for (;;) {
-            while (have < n &&
-                   (__atomic_load_n(&mb_->rec[have], __ATOMIC_ACQUIRE) >> 48) == (tag >> 48))
-                have++;
-            bool all = have == n, gone = false;
-            for (int b = 0; b < gcs::kServerBlocks; b++) {
-                if (__atomic_load_n(&mb_->ack[b].v, __ATOMIC_ACQUIRE) == q)
-                    continue;
-                if (in_place)
-                    all = false;
-                if (__atomic_load_n(&mb_->state[b].v, __ATOMIC_ACQUIRE) == 2)
-                    gone = true;
-            }
+            while (r.have < r.n &&
+                   (__atomic_load_n(&sl.rec[r.have], __ATOMIC_ACQUIRE) >> 48) == (tag >> 48))
+                r.have++;
+            bool all = r.have == r.n;
+            if (all && r.in_place)
+                for (int k = 0; k < nb; k++) {
+                    const int b = gcs::server_block(r.q, (uint32_t)k * gcs::kServerFPB);
+                    if ((int32_t)(__atomic_load_n(&mb_->ack[b].v, __ATOMIC_ACQUIRE) - r.q) < 0)
+                        all = false;
+                }
             if (all)
                 break;
-            if (gone) {
-                // the grid left before serving q: a fresh grid serves it again
-                // (blocks that had served it redo their share: same results)
-                int rc = wait_exit();
-                if (!rc) rc = launch(q - 1);
+            if (!launched_ || any_exited()) {
+                // the grid left (or is leaving) before serving r: a fresh grid
+                // serves every request after done_ again (blocks that had
+                // served one redo their share: the same results)
+                int rc = relaunch();
                 if (rc) return rc;
                 continue;
             }
             if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
-                (void)stop();
+                for (auto& s2 : mb_->slot)
+                    __atomic_store_n(&s2.a.cmd, 1u, __ATOMIC_RELEASE);
+                (void)wait_exit();
                 std::snprintf(g_hip_err, sizeof g_hip_err, "burst server: no answer in 2 s");
                 return GCS_EHIP;
             }
             __builtin_ia32_pause();
         }
-        for (uint32_t i = 0; i < n; i++) {
-            const uint64_t r = mb_->rec[i];
-            if (code) code[i] = (uint8_t)(r >> 32);
-            if (compute && csum) csum[i] = (uint32_t)r;
+        for (uint32_t i = 0; i < r.n; i++) {
+            const uint64_t v = sl.rec[i];
+            if (r.code) r.code[i] = (uint8_t)(v >> 32);
+            if (r.compute && r.csum) r.csum[i] = (uint32_t)v;
         }
+        r.pending = false;
         if (prof_) {
-            // GCS_SERVER_PROF: per request, the slowest block's serve and
-            // release times (wall clock), averaged and printed at exit
+            // GCS_SERVER_PROF: per request, the slowest serving block's serve
+            // and release times (wall clock), averaged and printed at exit
             double sv = 0, rl = 0;
-            for (int b = 0; b < gcs::kServerBlocks; b++) {
+            for (int k = 0; k < nb; k++) {
+                const int b = gcs::server_block(r.q, (uint32_t)k * gcs::kServerFPB);
                 sv = std::max(sv, (double)(mb_->prof[b][1] - mb_->prof[b][0]));
                 rl = std::max(rl, (double)(mb_->prof[b][2] - mb_->prof[b][1]));
             }
@@ -367,21 +436,11 @@ class BurstServer {
             prof_serve_ += sv / ticks_per_us_;
             prof_release_ += rl / ticks_per_us_;
             prof_total_ += std::chrono::duration<double, std::micro>(
-                               std::chrono::steady_clock::now() - t0).count();
-            prof_write_ += std::chrono::duration<double, std::micro>(t0 - tw).count();
+                               std::chrono::steady_clock::now() - r.t0).count();
         }
         return GCS_OK;
     }
 
-    // Ask the grid to leave and wait until it has.
-    int stop()
-    {
-        if (!launched_) return GCS_OK;
-        __atomic_store_n(&mb_->a.cmd, 1u, __ATOMIC_RELEASE);
-        return wait_exit();
-    }
-
-  private:
     bool any_exited() const
     {
         for (int b = 0; b < gcs::kServerBlocks; b++)
@@ -399,12 +458,26 @@ class BurstServer {
         return GCS_OK;
     }
 
-    int launch(uint32_t done)
+    // The grid (or part of it) left: make the rest leave, then start a fresh
+    // grid that serves every request after done_.
+    int relaunch()
+    {
+        if (launched_) {
+            for (auto& sl : mb_->slot)
+                __atomic_store_n(&sl.a.cmd, 1u, __ATOMIC_RELEASE);
+            int rc = wait_exit();
+            if (rc) return rc;
+        }
+        return launch();
+    }
+
+    int launch()
     {
         for (int b = 0; b < gcs::kServerBlocks; b++)
             __atomic_store_n(&mb_->state[b].v, 0u, __ATOMIC_RELAXED);
-        __atomic_store_n(&mb_->a.cmd, 0u, __ATOMIC_RELEASE);
-        HIP_TRY(gcs::launch_burst_server(dmb_, done, idle_ticks_, life_ticks_, kMaxPolls,
+        for (auto& sl : mb_->slot)
+            __atomic_store_n(&sl.a.cmd, 0u, __ATOMIC_RELEASE);
+        HIP_TRY(gcs::launch_burst_server(dmb_, done_, idle_ticks_, life_ticks_, kMaxPolls,
                                          prof_, stream_));
         launched_ = true;
         return GCS_OK;
@@ -415,7 +488,9 @@ class BurstServer {
     gcs::ServerMailbox* dmb_ = nullptr;   // device view
     hipStream_t stream_ = nullptr;
     uint64_t idle_ticks_ = 0, life_ticks_ = 0;
-    uint32_t seq_ = 0;
+    uint32_t posted_ = 0;                 // last request posted
+    uint32_t done_ = 0;                   // last request completed (all before it too)
+    Req req_[gcs::kServerSlots] = {};
     bool launched_ = false;
     bool prof_ = false;
     double ticks_per_us_ = 100.0;
@@ -438,6 +513,25 @@ struct gcs_ctx {
     Slot slot[kSlots];
     std::unique_ptr<GatherPool> pool;
     std::unique_ptr<BurstServer> server;   // gcs_ctx_set_burst_server / GCS_BURST_SERVER
+
+    // gcs_compute_ptrs_async: one record per server slot (request q lives in
+    // slot q % kServerSlots), with its own pinned staging for pageable frames
+    struct AsyncReq {
+        bool pending = false;
+        bool staged = false;
+        uint32_t q = 0, n = 0;
+        uint8_t* status = nullptr;          // the caller's outputs (nullable)
+        uint32_t* csums = nullptr;
+        std::vector<uint8_t*> ptrs;         // the caller's frames (staged: scatter target)
+        std::vector<uint16_t> lens;
+        std::vector<uint64_t> off;          // descriptors as posted
+        std::vector<uint16_t> dlen;
+        std::vector<uint8_t> st;            // results, written by the server
+        std::vector<uint32_t> cs;
+        uint8_t* h_stage = nullptr;         // pinned staging (kAsyncStageBytes)
+        uint8_t* d_stage = nullptr;         // its device view
+    };
+    AsyncReq areq[gcs::kServerSlots];
 
     // Copy work for `count` frames / `bytes` bytes: inline when small, else
     // spread over the gather pool.
@@ -1005,6 +1099,8 @@ try {
     {
         DeviceGuard g(ctx->device);
         ctx->server.reset();   // exit command, wait for the grid to drain
+        for (auto& a : ctx->areq)
+            if (a.h_stage) (void)hipHostFree(a.h_stage);
         for (auto& s : ctx->slot) {
             if (s.stream)
                 (void)hipStreamSynchronize(s.stream);
@@ -1353,6 +1449,130 @@ int gcs_compute(gcs_ctx* ctx, uint8_t* frames, const uint64_t* off, const uint16
                 uint32_t n, uint8_t* status, uint32_t* csums)
 try {
     return run_host_batch(ctx, frames, off, nullptr, len, n, status, csums, 0u, true);
+} GCS_CATCH
+
+namespace {
+
+constexpr uint64_t kAsyncStageBytes = 256u << 10;   // per server slot
+
+// Finish async request a: its server request is done (results in a.st /
+// a.cs); write the caller's outputs and, for staged frames, the checks.
+void async_finish(gcs_ctx::AsyncReq& a)
+{
+    for (uint32_t i = 0; i < a.n; i++) {
+        if (a.status) a.status[i] = a.st[i];
+        if (a.csums) a.csums[i] = a.cs[i];
+        if (a.staged && a.ptrs[i])
+            scatter_tx(a.ptrs[i], a.lens[i], a.st[i], a.cs[i]);
+    }
+    a.pending = false;
+}
+
+int async_wait(gcs_ctx* ctx, uint32_t q)
+{
+    DeviceGuard g(ctx->device);
+    if (ctx->server) {
+        int rc = ctx->server->wait(q);
+        if (rc) return rc;
+    }
+    for (auto& a : ctx->areq)
+        if (a.pending && (int32_t)(q - a.q) >= 0)
+            async_finish(a);
+    return GCS_OK;
+}
+
+}  // namespace
+
+int gcs_compute_ptrs_async(gcs_ctx* ctx, uint8_t* const* pkts, const uint16_t* len, uint32_t n,
+                           uint8_t* status, uint32_t* csums, uint64_t* ticket)
+try {
+    if (!ctx || !ticket || (n && (!pkts || !len)))
+        return GCS_EINVAL;
+    *ticket = 0;
+    if (n == 0)
+        return GCS_OK;
+    if (!ctx->server || n > (uint32_t)gcs::kSlotFrames)
+        return run_host_batch(ctx, nullptr, nullptr, pkts, len, n, status, csums, 0u, true);
+    DeviceGuard g(ctx->device);
+    // in place: every frame inside one registered region, 16 B-aligned
+    RegRegion reg{};
+    uint32_t first = 0;
+    while (first < n && !pkts[first])
+        first++;
+    bool inplace = first < n && find_region(pkts[first], &reg);
+    uint64_t staged = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        staged += (len[i] + kSlotAlign - 1) / kSlotAlign * kSlotAlign;
+        const uint8_t* p = pkts[i];
+        if (inplace && p)
+            inplace = p >= reg.host && (uint64_t)(p - reg.host) + len[i] <= (reg.bytes & ~15ull) &&
+                      ((uintptr_t)p & 15) == 0;
+    }
+    if (!inplace && staged > kAsyncStageBytes)
+        return run_host_batch(ctx, nullptr, nullptr, pkts, len, n, status, csums, 0u, true);
+    const uint32_t q = gcs::server_next(ctx->server->posted());
+    gcs_ctx::AsyncReq& a = ctx->areq[q % gcs::kServerSlots];
+    if (a.pending) {                     // the slot's previous async fill: finish it first
+        int rc = async_wait(ctx, a.q);
+        if (rc) return rc;
+    }
+    if (a.st.size() < (size_t)gcs::kSlotFrames) {
+        a.ptrs.resize(gcs::kSlotFrames);
+        a.lens.resize(gcs::kSlotFrames);
+        a.off.resize(gcs::kSlotFrames);
+        a.dlen.resize(gcs::kSlotFrames);
+        a.st.resize(gcs::kSlotFrames);
+        a.cs.resize(gcs::kSlotFrames);
+    }
+    a.staged = !inplace;
+    uint8_t* frames_d = reg.dev;
+    uint64_t bytes = reg.bytes & ~15ull;
+    if (a.staged) {
+        if (!a.h_stage) {
+            HIP_TRY(hipHostMalloc((void**)&a.h_stage, kAsyncStageBytes, hipHostMallocDefault));
+            HIP_TRY(hipHostGetDevicePointer((void**)&a.d_stage, a.h_stage, 0));
+        }
+        uint64_t used = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            a.off[i] = used;
+            a.dlen[i] = pkts[i] ? len[i] : 0;
+            if (pkts[i])
+                std::memcpy(a.h_stage + used, pkts[i], len[i]);
+            used += (len[i] + kSlotAlign - 1) / kSlotAlign * kSlotAlign;
+        }
+        frames_d = a.d_stage;
+        bytes = (used + 15) / 16 * 16;
+    } else {
+        for (uint32_t i = 0; i < n; i++) {
+            a.off[i] = pkts[i] ? (uint64_t)(pkts[i] - reg.host) : 0;
+            a.dlen[i] = pkts[i] ? len[i] : 0;
+        }
+    }
+    for (uint32_t i = 0; i < n; i++) {
+        a.ptrs[i] = pkts[i];
+        a.lens[i] = len[i];
+    }
+    a.n = n;
+    a.status = status;
+    a.csums = csums;
+    uint32_t got = 0;
+    int rc = ctx->server->post(frames_d, bytes, a.off.data(), a.dlen.data(), n, true,
+                               a.staged ? GCS_CF_NO_INPLACE : 0u, a.st.data(), a.cs.data(),
+                               /*in_place=*/!a.staged, &got);
+    if (rc) return rc;
+    a.q = got;
+    a.pending = true;
+    *ticket = got;
+    return GCS_OK;
+} GCS_CATCH
+
+int gcs_wait(gcs_ctx* ctx, uint64_t ticket)
+try {
+    if (!ctx)
+        return GCS_EINVAL;
+    if (ticket == 0)
+        return GCS_OK;
+    return async_wait(ctx, (uint32_t)ticket);
 } GCS_CATCH
 
 int gcs_verify_ptrs(gcs_ctx* ctx, uint8_t* const* pkts, const uint16_t* len, uint32_t n,

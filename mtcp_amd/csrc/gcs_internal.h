@@ -21,16 +21,29 @@ struct Ext {
 // short-lived resident grid that takes host batches from a mailbox in pinned
 // fine-grained memory instead of one kernel launch per batch.
 //
-// One poll is ONE load instruction of wave 0 of each block: lane 0 reads
-// request line A, lane 1 line B, lanes 2.. the descriptors of the block's
-// first frames.  Each 16 B line is read in one piece, and every line carries
-// the request number, so a poll that sees seq q in all the lines it needs
-// has a consistent request (the host writes each line's fields before its
-// seq, and the lines before line A's seq).  Results go to tagged per-frame
-// records in the mailbox; each block then releases and writes ack[b] = q
-// (what the host waits for when the frames themselves were written in place).
+// The mailbox is a ring of kServerSlots request slots.  Request q (a 32-bit
+// sequence number; numbers whose low 16 bits are 0 are never used, see
+// server_next) lives in slot q % kServerSlots, so the host can post
+// requests while earlier ones are still being served (the plugin's TX fill
+// posts frames as mTCP completes them).  Every block serves the requests in
+// order.  Request q's frames go to the blocks in turn starting at block
+// q % kServerBlocks (kServerFPB frames per block and pass), so a run of small
+// requests is served by different blocks at once.
+//
+// One poll is ONE load instruction of wave 0 of a block: lane 0 reads the
+// slot's line A, lane 1 its line B, lanes 2.. the descriptors of the block's
+// first frames of that request.  Each 16 B line is read in one piece and
+// carries the request number, so a poll that sees seq q in all the lines it
+// needs has a consistent request (the host writes each line's fields before
+// its seq, and the lines before line A's seq).  Results go to tagged
+// per-frame records in the slot; a block that served frames of q then
+// releases and writes ack[b] = q (what the host waits for when the frames
+// themselves were written in place).
 constexpr int kServerBlocks = 8;
-constexpr int kServerMaxFrames = 4096;
+constexpr int kServerFPB = 8;            // frames per block and pass (32 lanes x 3 chunks each)
+constexpr int kServerSlots = 8;
+constexpr int kSlotFrames = 512;         // frames per request
+constexpr int kServerMaxFrames = 4096;   // a larger synchronous batch: several requests
 struct alignas(16) ServerReqA {
     uint32_t seq;                       // request number (written last)
     uint32_t cmd;                       // 0 = serve, 1 = exit now
@@ -52,21 +65,39 @@ struct alignas(64) ServerLine {
     uint32_t v;
     uint32_t pad[15];
 };
-struct ServerMailbox {
+struct alignas(64) ServerSlot {
     ServerReqA a;                        // host
     ServerReqB b;                        // host
     uint8_t pad0[32];
-    ServerLine ack[kServerBlocks];       // device
-    ServerLine state[kServerBlocks];     // device: 1 serving, 2 exited
-    uint64_t prof[kServerBlocks][8];     // device, GCS_SERVER_PROF: wall-clock marks of
-                                         // the last request (seen, served, released)
-    ServerDesc desc[kServerMaxFrames];   // host
+    ServerDesc desc[kSlotFrames];        // host
     // device: one record per frame, written in ONE 8 B store once the frame
     // is done: csum (ip | tcp << 16) | code << 32 | (seq & 0xFFFF) << 48.  The
     // host sees a request's results complete when every record carries its
     // seq -- without waiting for the blocks' release fence and ack.
-    uint64_t rec[kServerMaxFrames];
+    uint64_t rec[kSlotFrames];
 };
+struct ServerMailbox {
+    ServerLine ack[kServerBlocks];       // device: the last request each block served frames of
+    ServerLine state[kServerBlocks];     // device: 1 serving, 2 exited
+    uint64_t prof[kServerBlocks][8];     // device, GCS_SERVER_PROF: wall-clock marks of
+                                         // the block's last request (seen, served, released)
+    ServerSlot slot[kServerSlots];
+};
+
+// The request number after q: q + 1, skipping numbers whose 16-bit record tag
+// would be 0 (a cleared record reads as tag 0).  Host and kernel both use it.
+__host__ __device__ inline uint32_t server_next(uint32_t q)
+{
+    q += 1;
+    return (q & 0xFFFFu) == 0 ? q + 1 : q;
+}
+
+// Block holding frame i of request q: frames go out kServerFPB per block,
+// starting at block q % kServerBlocks.
+__host__ __device__ inline int server_block(uint32_t q, uint32_t i)
+{
+    return (int)((q + i / kServerFPB) % kServerBlocks);
+}
 
 hipError_t launch_burst_server(ServerMailbox* mb, uint32_t done_seq, uint64_t idle_ticks,
                                uint64_t life_ticks, uint32_t max_polls, bool prof,

@@ -214,24 +214,29 @@ k_desc(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __re
 }
 
 // Burst server: a grid of kServerBlocks blocks that stays resident for at most
-// life_ticks (wall clock) and serves host batches posted in a mailbox
-// (gcs_internal.h ServerMailbox) -- each batch with the per-frame work of
-// k_desc<G,U> (frames in pinned host memory, read and written over PCIe),
-// without a kernel launch and event wait per batch.
+// life_ticks (wall clock) and serves host batches posted in the mailbox's
+// request ring (gcs_internal.h ServerMailbox) -- each batch with the per-frame
+// work of k_desc<G,U> (frames in pinned host memory, read and written over
+// PCIe), without a kernel launch and event wait per batch.  Each block serves
+// every request in order (q = server_next(last)); its frames of request q are
+// i = kServerFPB * ((b - q) mod kServerBlocks) + grp, then + 64 per pass.
 //
-// Every block ends: on the host's exit command, after idle_ticks without a
-// request, after life_ticks in total, or after max_polls polls -- whichever
-// comes first, so the grid always drains and work queued behind it on the
-// same hardware queue waits at most life_ticks.  All decisions are taken by
-// thread 0 from the poll's lines in LDS and broadcast (block-uniform control
-// flow: no wave leaves the loop while another waits at a barrier).
+// Every block ends: on the host's exit command (cmd in the slot it polls),
+// after idle_ticks without a request, after life_ticks in total, or after
+// max_polls polls -- whichever comes first, so the grid always drains and work
+// queued behind it on the same hardware queue waits at most life_ticks.  All
+// decisions are taken by thread 0 from the poll's lines in LDS and broadcast
+// (block-uniform control flow: no wave leaves the loop while another waits at
+// a barrier).
 template <int G, int U, bool PROF, int kPollWaves>
 __global__ void __launch_bounds__(kBlock)
 k_burst_server(ServerMailbox* mb, uint32_t done_seq, uint64_t idle_ticks, uint64_t life_ticks,
                uint32_t max_polls)
 {
-    enum { IDLE = 0, WORK = 1, EXIT = 2 };
+    enum { IDLE = 0, WORK = 1, EXIT = 2, SKIP = 3 };
     constexpr int FPB = kBlock / G;
+    static_assert(FPB == kServerFPB, "the mailbox's frames per block and pass");
+    constexpr int kPass = kServerBlocks * FPB;          // frames of one request per pass
     // kPollWaves = 2: a second wave polls half a round trip behind the first
     __shared__ uint4 s_line[2 + FPB];
     __shared__ uint32_t s_claim;             // IDLE until a polling wave claims WORK / EXIT
@@ -248,16 +253,20 @@ k_burst_server(ServerMailbox* mb, uint32_t done_seq, uint64_t idle_ticks, uint64
                            __HIP_MEMORY_SCOPE_SYSTEM);
     }
     __syncthreads();
-    // what lane < 2 + FPB of a polling wave reads each poll
-    const volatile u32x4* src = nullptr;
-    if (lane == 0)
-        src = reinterpret_cast<const volatile u32x4*>(&mb->a);
-    else if (lane == 1)
-        src = reinterpret_cast<const volatile u32x4*>(&mb->b);
-    else if (lane < 2 + FPB)
-        src = reinterpret_cast<const volatile u32x4*>(&mb->desc[blockIdx.x * FPB + lane - 2]);
     for (;;) {
+        const uint32_t q = server_next(last);            // the request this block serves next
+        ServerSlot* sl = &mb->slot[q % kServerSlots];
+        const uint32_t first = (uint32_t)FPB * ((blockIdx.x + kServerBlocks - q % kServerBlocks) %
+                                                kServerBlocks);   // this block's first frame of q
         if (wave < kPollWaves) {
+            // what lane < 2 + FPB of a polling wave reads each poll
+            const volatile u32x4* src = nullptr;
+            if (lane == 0)
+                src = reinterpret_cast<const volatile u32x4*>(&sl->a);
+            else if (lane == 1)
+                src = reinterpret_cast<const volatile u32x4*>(&sl->b);
+            else if (lane < 2 + FPB)
+                src = reinterpret_cast<const volatile u32x4*>(&sl->desc[first + lane - 2]);
             if (wave == 1)
                 __builtin_amdgcn_s_sleep(32);   // stagger: ~2k cycles behind wave 0
             for (;;) {
@@ -267,20 +276,24 @@ k_burst_server(ServerMailbox* mb, uint32_t done_seq, uint64_t idle_ticks, uint64
                 if (src)
                     v = *src;                   // one 16 B read per lane, one round trip
                 // lane 0 judges the poll from the lanes' lines (wave-wide shuffles)
-                const uint32_t q = __shfl(v.x, 0), cmd = __shfl(v.y, 0), n = __shfl(v.z, 0);
+                const uint32_t aq = __shfl(v.x, 0), cmd = __shfl(v.y, 0), n = __shfl(v.z, 0);
                 const uint32_t bseq = __shfl(v.w, 1);
                 bool ok = bseq == q;
                 for (int j = 0; j < FPB; j++) {
                     const uint32_t dseq = __shfl(v.w, 2 + j);
-                    if (blockIdx.x * FPB + j < n && dseq != q)
+                    if (first + j < n && dseq != q)
                         ok = false;
                 }
                 const uint64_t now = __builtin_amdgcn_s_memrealtime();
                 uint32_t act = IDLE;
                 if (cmd != 0 || now - t_start > life_ticks || ++polls >= max_polls)
                     act = EXIT;
-                else if (q != last)
+                else if (aq == q)
                     act = ok ? WORK : IDLE;     // torn poll: look again
+                else if ((int32_t)(aq - q) > 0)
+                    act = SKIP;                 // q is done and its slot reused: this block
+                                                // had no frames in it (the host reuses a slot
+                                                // only after its request completed)
                 else if (now - t_last > idle_ticks)
                     act = EXIT;
                 if (act == IDLE) {
@@ -300,18 +313,27 @@ k_burst_server(ServerMailbox* mb, uint32_t done_seq, uint64_t idle_ticks, uint64
         const uint32_t act = s_claim;
         if (act == EXIT)
             break;
+        if (act == SKIP) {
+            __syncthreads();                 // every thread has read s_claim
+            if (t == 0)
+                s_claim = IDLE;
+            last = q;
+            t_last = __builtin_amdgcn_s_memrealtime();
+            __syncthreads();
+            continue;
+        }
         // a request: its lines were written before its seq (fence-acquire
         // after observing it: later loads see everything the host wrote)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         const uint64_t t_seen = __builtin_amdgcn_s_memrealtime();
         const uint4 a = s_line[0], b = s_line[1];
-        const uint32_t q = a.x, n = a.z, compute = a.w & 1u, flags = a.w >> 1;
+        const uint32_t n = a.z, compute = a.w & 1u, flags = a.w >> 1;
         uint8_t* frames = reinterpret_cast<uint8_t*>((uint64_t)b.x | ((uint64_t)b.y << 32));
         const uint64_t bytes = (uint64_t)b.z * 16;
         const uint4 d0 = s_line[2 + grp];
-        for (uint32_t i = blockIdx.x * FPB + grp, pass = 0; i < n;
-             i += gridDim.x * FPB, pass++) {
-            const uint4 d = pass == 0 ? d0 : *reinterpret_cast<const uint4*>(&mb->desc[i]);
+        const bool mine = first < n;                     // block-uniform: frames of q here
+        for (uint32_t i = first + grp, pass = 0; i < n; i += kPass, pass++) {
+            const uint4 d = pass == 0 ? d0 : *reinterpret_cast<const uint4*>(&sl->desc[i]);
             const uint64_t o = (uint64_t)d.x | ((uint64_t)d.y << 32);
             const u32 len = d.z & 0xFFFFu;
             const bool ok = (o & 15) == 0 && o <= bytes && len <= bytes - o;
@@ -327,26 +349,28 @@ k_burst_server(ServerMailbox* mb, uint32_t done_seq, uint64_t idle_ticks, uint64
             if (sub == 0) {                  // the group's results, in one 8 B store
                 const uint64_t r = (uint64_t)s_csum[grp] | ((uint64_t)s_code[grp] << 32) |
                                    ((uint64_t)(q & 0xFFFFu) << 48);
-                __hip_atomic_store(&mb->rec[i], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&sl->rec[i], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
         uint64_t t_served = 0;
-        if (PROF) {
+        if (PROF && mine) {
             __syncthreads();
             t_served = __builtin_amdgcn_s_memrealtime();
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // this wave's results reach host memory
+        if (mine)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // this wave's results reach host memory
         __syncthreads();                     // every wave done with s_line / s_claim
         if (t == 0) {
-            if (PROF) {
+            if (PROF && mine) {
                 mb->prof[blockIdx.x][0] = t_seen;
                 mb->prof[blockIdx.x][1] = t_served;
                 mb->prof[blockIdx.x][2] = __builtin_amdgcn_s_memrealtime();
                 mb->prof[blockIdx.x][3] = polls;
             }
             s_claim = IDLE;
-            __hip_atomic_store(&mb->ack[blockIdx.x].v, q, __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
+            if (mine)
+                __hip_atomic_store(&mb->ack[blockIdx.x].v, q, __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
         }
         last = q;
         t_last = __builtin_amdgcn_s_memrealtime();

@@ -33,6 +33,7 @@
 #define GPUCSUM_SHADOW_ROOM 2048             /* MAX_PKT_SIZE: mTCP never asks for more */
 #define GPUCSUM_DEFAULT_SEG_MAX 1514         /* ETHERNET_HEADER_LEN + 1500 B MTU */
 #define V_INNER 0xFE                         /* RX_CHAINED frame: inner's own checks */
+#define GPUCSUM_ASYNC_MAX 512                /* frames per async post (gcs_compute_ptrs_async) */
 
 struct rx_if {
 	int32_t n;
@@ -46,6 +47,9 @@ struct rx_if {
 
 struct tx_if {
 	uint32_t n;
+	uint32_t done;      /* frames [0, done) are complete (mTCP moved on from them) */
+	uint32_t posted;    /* frames [0, posted) are posted to the GPU (async fill)  */
+	uint64_t ticket;    /* the last async post's ticket (0: none)                */
 	uint8_t *ptr[GPUCSUM_MAX_BURST];
 	uint16_t len[GPUCSUM_MAX_BURST];
 	uint8_t status[GPUCSUM_MAX_BURST];
@@ -55,6 +59,7 @@ struct tx_if {
 struct gthr {
 	struct mtcp_thread_context *ctx;
 	gcs_ctx *gcs;
+	uint32_t tx_group;      /* async TX fill: post every tx_group completed frames (0: off) */
 	struct rx_if *rx[GPUCSUM_MAX_IFS];
 	struct tx_if *tx[GPUCSUM_MAX_IFS];
 	struct gpucsum_stats st;
@@ -206,6 +211,13 @@ static void gpucsum_init_handle(struct mtcp_thread_context *ctx)
 		rc = gcs_ctx_set_burst_server(g->gcs, 1);
 		if (rc)
 			die("gcs_ctx_set_burst_server", rc);
+		/* fill as you go: a TX frame is complete once mTCP asks for the next
+		 * one or for its checksum (tcp_out.c:239-333); every
+		 * GPUCSUM_TX_GROUP (default 8, 0 = off) completed frames go to the
+		 * server while mTCP builds the rest, so send_pkts waits only for
+		 * the last group */
+		env = getenv("GPUCSUM_TX_GROUP");
+		g->tx_group = env ? (uint32_t)atoi(env) : 8;
 	}
 	env = getenv("GPUCSUM_RSS_QUEUES");
 	if (env && atoi(env) > 0) {
@@ -249,18 +261,68 @@ static struct tx_if *txq(struct gthr *g, int ifidx)
 	return q;
 }
 
+/* Async fill of the completed frames not yet posted: [posted, done). */
+static void post_tx(struct gthr *g, struct tx_if *q)
+{
+	uint64_t t = 0;
+	int rc;
+
+	if (q->done <= q->posted)
+		return;
+	rc = gcs_compute_ptrs_async(g->gcs, q->ptr + q->posted, q->len + q->posted,
+	                            q->done - q->posted, q->status + q->posted, NULL, &t);
+	if (rc) {
+		/* leave them to flush_tx's synchronous fill */
+		g->st.gpu_failures++;
+		fprintf(stderr, "[gpucsum] async TX fill of %u frames failed: %s %s\n",
+		        q->done - q->posted, gcs_strerror(rc), gcs_last_hip_error());
+		g->tx_group = 0;
+		return;
+	}
+	if (t)
+		q->ticket = t;
+	g->st.tx_posts++;
+	q->posted = q->done;
+}
+
+/* Frames [0, upto) of queue q are complete: post them once a group is ready. */
+static void tx_complete(struct gthr *g, struct tx_if *q, uint32_t upto)
+{
+	if (upto > q->done)
+		q->done = upto;
+	if (g->tx_group && q->done - q->posted >= g->tx_group)
+		post_tx(g, q);
+}
+
 /* TX fill of every queued frame of one interface (ip_out.c:155-173 and
  * tcp_out.c:323-333, batched).  TX_EAGER: the queued frames are shadow slots;
  * once filled they go, in order, into inner get_wptr buffers (the inner may
- * transmit the previous one on each call, netmap_module.c:155-156). */
+ * transmit the previous one on each call, netmap_module.c:155-156).  With the
+ * async fill, earlier groups are in flight already: post the tail, wait. */
 static void flush_tx(struct gthr *g, int ifidx, struct tx_if *q)
 {
 	uint32_t k;
-	int rc;
+	int rc = 0;
 
 	if (!q || q->n == 0)
 		return;
-	rc = gcs_compute_ptrs(g->gcs, q->ptr, q->len, q->n, q->status, NULL);
+	if (q->posted > 0 || (g->tx_group && q->n <= GPUCSUM_ASYNC_MAX)) {
+		q->done = q->n;
+		post_tx(g, q);
+		if (q->posted == q->n) {
+			rc = gcs_wait(g->gcs, q->ticket);
+		} else {
+			/* the tail could not be posted: wait for what was, fill the rest */
+			rc = gcs_wait(g->gcs, q->ticket);
+			if (!rc)
+				rc = gcs_compute_ptrs(g->gcs, q->ptr + q->posted, q->len + q->posted,
+				                      q->n - q->posted, q->status + q->posted, NULL);
+		}
+	} else {
+		rc = gcs_compute_ptrs(g->gcs, q->ptr, q->len, q->n, q->status, NULL);
+	}
+	q->done = q->posted = 0;
+	q->ticket = 0;
 	if (rc) {
 		g->st.gpu_failures++;
 		fprintf(stderr, "[gpucsum] TX fill of %u frames failed: %s %s\n", q->n,
@@ -298,6 +360,8 @@ static uint8_t *gpucsum_get_wptr(struct mtcp_thread_context *ctx, int ifidx, uin
 		return NULL;
 	if (q->n == GPUCSUM_MAX_BURST)
 		flush_tx(g, ifidx, q);  /* all queued frames are complete by now */
+	else
+		tx_complete(g, q, q->n);   /* the frames handed out so far are complete */
 	if (q->shadow) {
 		if (len > GPUCSUM_SHADOW_ROOM)
 			return NULL;
@@ -494,8 +558,18 @@ static void gpucsum_destroy_handle(struct mtcp_thread_context *ctx)
 static int32_t gpucsum_dev_ioctl(struct mtcp_thread_context *ctx, int nif, int cmd, void *argp)
 {
 	switch (cmd) {
-	case PKT_TX_IP_CSUM:          /* ip_out.c:91, :163 (ICMP)          */
 	case PKT_TX_TCPIP_CSUM:       /* tcp_out.c:206, :326               */
+		/* asked after the segment's headers and payload are written: the
+		 * port's most recent get_wptr frame is complete (an ICMP frame's
+		 * PKT_TX_IP_CSUM comes before its ICMP part: not a signal) */
+		{
+			struct gthr *g = ctx ? lookup(ctx) : NULL;
+			struct tx_if *q = (g && nif >= 0 && nif < GPUCSUM_MAX_IFS) ? g->tx[nif] : NULL;
+			if (q && q->n)
+				tx_complete(g, q, q->n);
+		}
+		return 0;
+	case PKT_TX_IP_CSUM:          /* ip_out.c:91, :163 (ICMP)          */
 	case PKT_RX_IP_CSUM:          /* ip_in.c:30                        */
 	case PKT_RX_TCP_CSUM:         /* tcp_in.c:1227                     */
 	case PKT_TX_TCPIP_CSUM_PEEK:  /* ip_out.c:88, :160                 */

@@ -34,6 +34,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "mtcp.h"
 #include "eth_in.h"
@@ -188,6 +189,23 @@ int refs_tx_tcp(struct io_module_func *iom, struct mtcp_thread_context *ctx, uin
  * out on stream sidx[k] with flags[k] and payload bytes pay_off/pay_len;
  * cur_ts advances by one per send round.  Returns segments written, or -1 on a
  * NULL get_wptr that a send round does not cure (tcp_out.c:799-802 retries). */
+static double refs_now_us(void)
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
+}
+
+/* refs_tx_stream, with send_us[k] = the time the k-th every-`burst` send_pkts
+ * call blocked the mTCP thread (core.c:846-848), when send_us is not NULL. */
+int refs_tx_stream_timed(struct io_module_func *iom, struct mtcp_thread_context *ctx,
+                         uint32_t ns, const uint32_t *saddr, const uint16_t *sport,
+                         const uint32_t *daddr, const uint16_t *dport, const uint32_t *snd_nxt,
+                         const uint32_t *rcv_nxt, const uint32_t *rcv_wnd,
+                         const uint32_t *ts_recent, uint32_t n, const uint16_t *sidx,
+                         const uint8_t *flags, const uint8_t *payload, const uint64_t *pay_off,
+                         const uint16_t *pay_len, uint32_t burst, double *send_us);
+
 int refs_tx_stream(struct io_module_func *iom, struct mtcp_thread_context *ctx, uint32_t ns,
                    const uint32_t *saddr, const uint16_t *sport, const uint32_t *daddr,
                    const uint16_t *dport, const uint32_t *snd_nxt, const uint32_t *rcv_nxt,
@@ -195,6 +213,20 @@ int refs_tx_stream(struct io_module_func *iom, struct mtcp_thread_context *ctx, 
                    const uint16_t *sidx, const uint8_t *flags, const uint8_t *payload,
                    const uint64_t *pay_off, const uint16_t *pay_len, uint32_t burst)
 {
+	return refs_tx_stream_timed(iom, ctx, ns, saddr, sport, daddr, dport, snd_nxt, rcv_nxt,
+	                            rcv_wnd, ts_recent, n, sidx, flags, payload, pay_off, pay_len,
+	                            burst, NULL);
+}
+
+int refs_tx_stream_timed(struct io_module_func *iom, struct mtcp_thread_context *ctx,
+                         uint32_t ns, const uint32_t *saddr, const uint16_t *sport,
+                         const uint32_t *daddr, const uint16_t *dport, const uint32_t *snd_nxt,
+                         const uint32_t *rcv_nxt, const uint32_t *rcv_wnd,
+                         const uint32_t *ts_recent, uint32_t n, const uint16_t *sidx,
+                         const uint8_t *flags, const uint8_t *payload, const uint64_t *pay_off,
+                         const uint16_t *pay_len, uint32_t burst, double *send_us)
+{
+	uint32_t kb = 0;
 	tcp_stream *st;
 	struct tcp_send_vars *sv;
 	struct tcp_recv_vars *rv;
@@ -247,7 +279,11 @@ int refs_tx_stream(struct io_module_func *iom, struct mtcp_thread_context *ctx, 
 			goto out;
 		}
 		if (burst && (k + 1) % burst == 0) {
+			double t0 = refs_now_us();
 			iom->send_pkts(ctx, 0);
+			if (send_us)
+				send_us[kb] = refs_now_us() - t0;
+			kb++;
 			refs_mgr.cur_ts++;
 		}
 	}

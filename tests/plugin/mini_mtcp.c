@@ -20,6 +20,7 @@
  */
 #include <stdint.h>
 #include <string.h>
+#include <time.h>
 
 #include "../../include/gpucsum_io_module.h"
 #include "../../oracle/csum_ref.h"
@@ -243,11 +244,40 @@ int32_t mini_send(io_module_func *iom, struct mtcp_thread_context *ctx, int ifid
 
 /* TX: write n prepared frames (check fields as mTCP leaves them: 0) through
  * the module in mTCP's order, flushing with send_pkts every `burst` frames. */
+static double now_us(void)
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
+}
+
+static int mini_tx_impl(io_module_func *iom, struct mtcp_thread_context *ctx, int ifidx,
+                        const uint8_t *buf, const uint64_t *off, const uint16_t *len,
+                        uint32_t n, uint32_t burst, double *send_us, double *burst_us);
+
 int mini_tx(io_module_func *iom, struct mtcp_thread_context *ctx, int ifidx,
             const uint8_t *buf, const uint64_t *off, const uint16_t *len, uint32_t n,
             uint32_t burst)
 {
-	uint32_t i, sent = 0;
+	return mini_tx_impl(iom, ctx, ifidx, buf, off, len, n, burst, NULL, NULL);
+}
+
+/* mini_tx, timed: send_us[k] = the k-th send_pkts call (what blocks the mTCP
+ * thread after its burst, core.c:846-848), burst_us[k] = its whole burst from
+ * the first get_wptr to send_pkts' return (clock_gettime, microseconds). */
+int mini_tx_timed(io_module_func *iom, struct mtcp_thread_context *ctx, int ifidx,
+                  const uint8_t *buf, const uint64_t *off, const uint16_t *len, uint32_t n,
+                  uint32_t burst, double *send_us, double *burst_us)
+{
+	return mini_tx_impl(iom, ctx, ifidx, buf, off, len, n, burst, send_us, burst_us);
+}
+
+static int mini_tx_impl(io_module_func *iom, struct mtcp_thread_context *ctx, int ifidx,
+                        const uint8_t *buf, const uint64_t *off, const uint16_t *len,
+                        uint32_t n, uint32_t burst, double *send_us, double *burst_us)
+{
+	uint32_t i, sent = 0, k = 0;
+	double t_burst = now_us();
 
 	for (i = 0; i < n; i++) {
 		const uint8_t *src = buf + off[i];
@@ -289,7 +319,15 @@ int mini_tx(io_module_func *iom, struct mtcp_thread_context *ctx, int ifidx,
 			}
 		}
 		if (burst && (i + 1) % burst == 0) {
+			double t0 = now_us();
 			iom->send_pkts(ctx, ifidx);                /* core.c:846-848 */
+			double t1 = now_us();
+			if (send_us)
+				send_us[k] = t1 - t0;
+			if (burst_us)
+				burst_us[k] = t1 - t_burst;
+			k++;
+			t_burst = now_us();
 			sent = i + 1;
 		}
 	}

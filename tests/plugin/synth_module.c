@@ -65,6 +65,14 @@ int synth_set_rx(const uint8_t *buf, const uint64_t *off, const uint16_t *len, u
 }
 
 uint32_t synth_tx_sent(void) { return S.tx_sent; }
+
+/* The TX rooms (SYN_MAX_TX x SYN_BUF bytes): for registering them as an mbuf
+ * pool would be registered (gcs_host_register). */
+uint8_t *synth_tx_base(uint64_t *bytes)
+{
+	*bytes = (uint64_t)SYN_MAX_TX * SYN_BUF;
+	return S.tx_bufs;
+}
 uint32_t synth_released(void) { return S.released; }
 uint32_t synth_sends(void) { return S.sends; }
 

@@ -35,7 +35,7 @@ class GStats(C.Structure):
     _fields_ = [(k, C.c_uint64) for k in
                 ("rx_frames", "rx_errors", "rx_batches", "tx_frames", "tx_batches",
                  "gpu_failures", "rx_foreign")] + [("device", C.c_int)] + \
-                [(k, C.c_uint64) for k in ("rx_inner", "rx_rptr_changed", "tx_inner_full")]
+                [(k, C.c_uint64) for k in ("rx_inner", "rx_rptr_changed", "tx_inner_full", "tx_posts")]
 
 
 @pytest.fixture(scope="module")
@@ -54,6 +54,9 @@ def H():
     L.mini_vtable_size.restype = C.c_size_t
     L.mini_rx_loop.argtypes = [vp, vp, C.c_int, C.POINTER(Stats), vp, C.c_uint32]
     L.mini_tx.argtypes = [vp, vp, C.c_int, vp, vp, vp, C.c_uint32, C.c_uint32]
+    L.mini_tx_timed.argtypes = [vp, vp, C.c_int, vp, vp, vp, C.c_uint32, C.c_uint32, vp, vp]
+    L.synth_tx_base.argtypes = [C.POINTER(C.c_uint64)]
+    L.synth_tx_base.restype = vp
     return L
 
 
@@ -223,6 +226,58 @@ def test_decorator_tx_wire_identical(H, P, gpu_plugin, burst):
     P.gpucsum_get_stats(ctx, C.byref(after))
     assert after.tx_frames - before.tx_frames == len(off)
     assert after.gpu_failures == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("group,registered", [("0", False), ("1", False), ("8", False),
+                                              ("64", False), ("8", True), ("1", True)])
+def test_async_tx_fill_wire_identical(H, P, monkeypatch, group, registered):
+    """Fill as you go (GPUCSUM_TX_GROUP): completed frames go to the burst
+    server in groups while the mTCP-shaped loop builds the rest; send_pkts
+    posts the tail and waits.  The wire equals the software folds' for every
+    group size, with the synthetic NIC's TX rooms pageable (staged) or
+    registered (filled in place over PCIe)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("plugin GPU tests need a GPU (no CPU fallback exists)")
+    monkeypatch.setenv("GPUCSUM_TX_GROUP", group)
+    buf, off, lens = tx_frames(3000, 12)
+    ctx = C.create_string_buffer(64)
+    sw = tx_run(H, vtab(H, "synth_module_func"), C.addressof(ctx), buf, off, lens, 64)
+    assert P.gpucsum_set_inner(vtab(H, "synth_module_func")) == 0
+    iom = vtab(P, "gpucsum_module_func")
+    dctx = C.create_string_buffer(64)
+    assert H.mini_start(iom, C.addressof(dctx)) == 0
+    base = None
+    try:
+        H.synth_reset(64)
+        if registered:
+            nb = C.c_uint64()
+            base = H.synth_tx_base(C.byref(nb))
+            gpucsum.check(P.gcs_host_register(C.c_void_p(base), nb.value))
+        n = len(off)
+        assert H.mini_tx(iom, C.addressof(dctx), 0, buf.ctypes.data,
+                         np.ascontiguousarray(off, np.uint64).ctypes.data,
+                         np.ascontiguousarray(lens, np.uint16).ctypes.data, n, 64) == n
+        hw = []
+        tmp = np.zeros(2048, dtype=np.uint8)
+        for k in range(n):
+            L = H.synth_tx_frame(k, tmp.ctypes.data)
+            hw.append(tmp[:L].copy())
+        st = GStats()
+        assert P.gpucsum_get_stats(C.addressof(dctx), C.byref(st)) == 0
+    finally:
+        if base:
+            gpucsum.check(P.gcs_host_unregister(C.c_void_p(base)))
+        H.mini_stop(iom, C.addressof(dctx))
+    assert len(sw) == len(hw) == 3000
+    for a, b in zip(sw, hw):
+        np.testing.assert_array_equal(a, b)
+    assert st.tx_frames == 3000 and st.gpu_failures == 0
+    if group == "0":
+        assert st.tx_posts == 0
+    else:
+        assert st.tx_posts >= 3000 // max(int(group), 64)
 
 
 @pytest.mark.gpu
