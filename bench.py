@@ -652,6 +652,20 @@ def plugin_threads():
         return {"error": repr(e)[:200]}
 
 
+def plugin_tx_async():
+    """How long send_pkts blocks an mTCP-shaped TX loop per 64 x 1500 B burst,
+    with the plugin filling frames as mTCP completes them (GPUCSUM_TX_GROUP)
+    and without; the software path alongside (tools/tx_async_probe.py, child
+    process)."""
+    import subprocess
+    try:
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "tx_async_probe.py")],
+                           capture_output=True, text=True, timeout=240)
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    except Exception as e:   # a side measurement: report, never fail the bench line
+        return {"error": repr(e)[:200]}
+
+
 def main():
     args = parse()
     import torch
@@ -764,6 +778,7 @@ def main():
             line["pcie_inclusive"] = pcie_inclusive(gpucsum, torch)
             line["plugin_bursts"] = plugin_bursts(gpucsum)
             line["plugin_threads"] = plugin_threads()
+            line["plugin_tx_async"] = plugin_tx_async()
     ctx.close()
     if rank == 0:
         print(json.dumps(line), flush=True)

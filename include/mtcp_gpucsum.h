@@ -296,8 +296,9 @@ int gcs_compute_ptrs(gcs_ctx *ctx, uint8_t *const *pkts, const uint16_t *len,
  * frame's check fields filled in place.  Until then the frames and the output
  * arrays must stay valid and the frames unmodified.  Frames all in one
  * registered region (gcs_host_register) at 16 B-aligned addresses are read
- * and filled where they are; others are copied into the context's pinned
- * async staging.  Without the server, or for a batch larger than one request
+ * where they are; others are copied into the context's pinned async staging
+ * (GCS_ASYNC_STAGE=device: into device memory over the BAR).  The checks come
+ * back with the results; gcs_wait writes them into the frames.  Without the server, or for a batch larger than one request
  * (512 frames / 256 KiB staged), the fill runs synchronously and *ticket = 0.
  * gcs_wait(ctx, t) completes every async fill posted on ctx up to ticket t;
  * gcs_wait(ctx, 0) does nothing. */

@@ -530,7 +530,9 @@ struct gcs_ctx {
         std::vector<uint32_t> cs;
         uint8_t* h_stage = nullptr;         // pinned staging (kAsyncStageBytes)
         uint8_t* d_stage = nullptr;         // its device view
+        bool stage_dev = false;             // staging is device memory (hipFree)
     };
+    bool async_stage_dev = false;           // GCS_ASYNC_STAGE=device
     AsyncReq areq[gcs::kServerSlots];
 
     // Copy work for `count` frames / `bytes` bytes: inline when small, else
@@ -1070,6 +1072,8 @@ try {
         ctx->direct_max = std::strtoull(e, nullptr, 10);
     if (const char* e = std::getenv("GCS_DIRECT_SPREAD"))
         ctx->direct_spread = std::atoi(e) != 0;
+    if (const char* e = std::getenv("GCS_ASYNC_STAGE"))
+        ctx->async_stage_dev = std::strcmp(e, "device") == 0;
     if (const char* e = std::getenv("GCS_BURST_SERVER")) {
         if (std::atoi(e) != 0 && (rc = gcs_ctx_set_burst_server(ctx, 1)) != GCS_OK) {
             gcs_ctx_destroy(ctx);
@@ -1100,7 +1104,7 @@ try {
         DeviceGuard g(ctx->device);
         ctx->server.reset();   // exit command, wait for the grid to drain
         for (auto& a : ctx->areq)
-            if (a.h_stage) (void)hipHostFree(a.h_stage);
+            if (a.h_stage) (void)(a.stage_dev ? hipFree(a.h_stage) : hipHostFree(a.h_stage));
         for (auto& s : ctx->slot) {
             if (s.stream)
                 (void)hipStreamSynchronize(s.stream);
@@ -1456,13 +1460,13 @@ namespace {
 constexpr uint64_t kAsyncStageBytes = 256u << 10;   // per server slot
 
 // Finish async request a: its server request is done (results in a.st /
-// a.cs); write the caller's outputs and, for staged frames, the checks.
+// a.cs); write the caller's outputs and the frames' check fields.
 void async_finish(gcs_ctx::AsyncReq& a)
 {
     for (uint32_t i = 0; i < a.n; i++) {
         if (a.status) a.status[i] = a.st[i];
         if (a.csums) a.csums[i] = a.cs[i];
-        if (a.staged && a.ptrs[i])
+        if (a.ptrs[i])
             scatter_tx(a.ptrs[i], a.lens[i], a.st[i], a.cs[i]);
     }
     a.pending = false;
@@ -1529,8 +1533,18 @@ try {
     uint64_t bytes = reg.bytes & ~15ull;
     if (a.staged) {
         if (!a.h_stage) {
-            HIP_TRY(hipHostMalloc((void**)&a.h_stage, kAsyncStageBytes, hipHostMallocDefault));
-            HIP_TRY(hipHostGetDevicePointer((void**)&a.d_stage, a.h_stage, 0));
+            if (ctx->async_stage_dev) {
+                // staging in fine-grained device memory, written by the host
+                // over the BAR: the GPU then reads the frames from HBM
+                HIP_TRY(hipExtMallocWithFlags((void**)&a.h_stage, kAsyncStageBytes,
+                                              hipDeviceMallocFinegrained));
+                a.d_stage = a.h_stage;
+                a.stage_dev = true;
+            } else {
+                HIP_TRY(hipHostMalloc((void**)&a.h_stage, kAsyncStageBytes,
+                                      hipHostMallocDefault));
+                HIP_TRY(hipHostGetDevicePointer((void**)&a.d_stage, a.h_stage, 0));
+            }
         }
         uint64_t used = 0;
         for (uint32_t i = 0; i < n; i++) {
@@ -1555,10 +1569,16 @@ try {
     a.n = n;
     a.status = status;
     a.csums = csums;
+    // The kernel never writes the frames: it returns the checks in the
+    // records and gcs_wait writes them into the frames from the host.  For
+    // frames in a registered region that saves the kernel's 64 B sector
+    // writes over PCIe and the release + ack round trip an in-place
+    // completion waits for (64 x 1500 B, tools/tx_async_probe.py: send_pkts
+    // blocked 9.2 us in place vs ~6 us with host-side checks).
     uint32_t got = 0;
     int rc = ctx->server->post(frames_d, bytes, a.off.data(), a.dlen.data(), n, true,
-                               a.staged ? GCS_CF_NO_INPLACE : 0u, a.st.data(), a.cs.data(),
-                               /*in_place=*/!a.staged, &got);
+                               GCS_CF_NO_INPLACE, a.st.data(), a.cs.data(),
+                               /*in_place=*/false, &got);
     if (rc) return rc;
     a.q = got;
     a.pending = true;

@@ -69,9 +69,11 @@ out = {"workload": f"{BURSTS} bursts of {BURST} x {L}B TCP frames through mini_t
        "timer": "C clock_gettime around each send_pkts and each burst"}
 ctx = C.create_string_buffer(64)
 out["software_path"] = run(vtab(H, "synth_module_func"), C.addressof(ctx), False)
-for registered in (False, True):
-    for group in ("0", "4", "8", "16"):
+MODES = [(False, g, "host") for g in ("0", "8", "16")] + [(False, "8", "device")] + \
+        [(True, g, "host") for g in ("0", "8", "16")]
+for registered, group, stage in MODES:
         os.environ["GPUCSUM_TX_GROUP"] = group
+        os.environ["GCS_ASYNC_STAGE"] = stage
         assert P.gpucsum_set_inner(vtab(H, "synth_module_func")) == 0
         iom = vtab(P, "gpucsum_module_func")
         dctx = C.create_string_buffer(64)
@@ -80,5 +82,6 @@ for registered in (False, True):
             r = run(iom, C.addressof(dctx), registered)
         finally:
             H.mini_stop(iom, C.addressof(dctx))
-        out[f"{'registered' if registered else 'pageable'}_group{group}"] = r
+        out[f"{'registered' if registered else 'pageable'}_group{group}"
+            + ("_devstage" if stage == "device" else "")] = r
 print(json.dumps(out))
