@@ -12,6 +12,8 @@ Inputs (under the source directory, one rocprofv3 run each):
 
 Writes:
   profiles/<round>/kernel_stats.csv    the bench run's --stats summary
+  profiles/<round>/kernel_stats_extras.csv  the same for bench.py with its side
+                                       measurements (their kernels' averages)
   profiles/<round>/pmc_configs.csv     per configuration: kernel, launches,
                                        FETCH/WRITE KB, HBM bytes, duration
   profiles/pmc_summary.json            read by bench.py (roofline.traffic)
@@ -77,6 +79,9 @@ def main():
     stats = one(os.path.join(src, "bench", "**", "*kernel_stats.csv"))
     if stats:
         shutil.copy(stats, os.path.join(dst, "kernel_stats.csv"))
+    stats = one(os.path.join(src, "bench_extras", "**", "*kernel_stats.csv"))
+    if stats:
+        shutil.copy(stats, os.path.join(dst, "kernel_stats_extras.csv"))
     labels = json.load(open(os.path.join(src, "manifest.json")))["labels"]
     series = {"FETCH_SIZE": per_dispatch_counter(os.path.join(src, "fetch"), "FETCH_SIZE"),
               "WRITE_SIZE": per_dispatch_counter(os.path.join(src, "write"), "WRITE_SIZE"),

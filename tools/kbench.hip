@@ -1886,7 +1886,7 @@ int lro_main(uint64_t n, int rounds)
         hipLaunchKernelGGL((k_gro<U_>), dim3((n + 63) / 64), dim3(256), 0, st, in, n * stride,   \
                            off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd);    \
     }});
-    GROU(2) GROU(4)
+    if (getenv("KB_GRO_W256")) { GROU(2) GROU(4) }
 #define GROW(U_, W_)                                                                         \
     vs.push_back({"k_gro<" #U_ "," #W_ "> (window 64, max 16384)", bytes, [&](hipStream_t st) {  \
         hipLaunchKernelGGL((k_gro<U_, W_>), dim3((n + 63) / 64), dim3(256), 0, st, in, n * stride, \
@@ -1899,6 +1899,8 @@ int lro_main(uint64_t n, int rounds)
                            off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd);  \
     }});
     GROO(2, 64, 6)
+    // round 3: more bytes in flight per wave (U) against waves per SIMD (OCC)
+    GROO(3, 64, 5) GROO(3, 64, 6) GROO(4, 64, 4) GROO(4, 64, 5) GROO(2, 64, 8) GROO(4, 64, 6)
     vs.push_back({"verify (launch_verify_desc) for scale", (double)n * (L + 1), [&](hipStream_t st) {
         CK(launch_verify_desc(in, n * stride, off, lens, (u32)n, vd, 0u, st));
     }});
