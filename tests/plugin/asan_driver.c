@@ -302,6 +302,81 @@ static void part_errors(void)
 	printf("part 5 argument errors: ok\n");
 }
 
+/* Part 6: async TX fills (gcs_compute_ptrs_async / gcs_wait): groups of 1..100
+ * frames, up to 20 outstanding (past the 8 request slots: slot reuse), waits
+ * on older and newer tickets, a synchronous verify on the same context in
+ * between; pageable frames (staged) and frames in a registered region. */
+static void part_async(int registered)
+{
+	const uint32_t n = 3000;
+	uint64_t *off, bytes, rng = 0xC0FFEE + registered;
+	uint16_t *len;
+	uint8_t *src = imix(n, 0x6A6A + registered, &off, &len, &bytes), *ref = malloc(bytes + 64);
+	uint8_t *buf, *mem = NULL, *st = malloc(n), *vd = malloc(n), **ptrs = malloc(n * sizeof(*ptrs));
+	uint32_t *cs = malloc(n * sizeof(*cs)), i, bad = 0, posts = 0;
+	uint64_t tk[32] = {0};
+	gcs_ctx *ctx = NULL;
+	int rc = gcs_ctx_create(&ctx, 0, 4096, 8u << 20), nt = 0;
+
+	CHECK(rc == 0, "gcs_ctx_create %d", rc);
+	CHECK(gcs_ctx_set_burst_server(ctx, 1) == 0, "server on");
+	if (registered) {
+		mem = aligned_alloc(4096, (bytes + 64 + 4095) / 4096 * 4096);
+		memcpy(mem, src, bytes + 64);
+		rc = gcs_host_register(mem, (bytes + 64 + 4095) / 4096 * 4096);
+		CHECK(rc == 0, "gcs_host_register %d", rc);
+		buf = mem;
+	} else {
+		buf = src;
+	}
+	memcpy(ref, buf, bytes + 64);
+	for (i = 0; i < n; i++) {
+		ptrs[i] = buf + off[i];
+		st[i] = 0xEE;
+		cs[i] = 0xEEEEEEEEu;
+	}
+	for (i = 0; i < n;) {
+		uint32_t m = 1 + xs(&rng) % 100;
+		uint64_t t = 0;
+		if (m > n - i)
+			m = n - i;
+		rc = gcs_compute_ptrs_async(ctx, ptrs + i, len + i, m, st + i, cs + i, &t);
+		CHECK(rc == 0, "async post %d %s", rc, gcs_last_hip_error());
+		tk[nt++ % 32] = t;
+		posts++;
+		i += m;
+		if (posts % 7 == 0) {                        /* an older ticket */
+			rc = gcs_wait(ctx, tk[(nt + 28) % 32]);
+			CHECK(rc == 0, "gcs_wait (older) %d", rc);
+		}
+		if (posts % 11 == 0) {                       /* synchronous work in between */
+			uint16_t l1 = len[0];
+			uint8_t *p1 = ref;
+			rc = gcs_verify_ptrs(ctx, &p1, &l1, 1, vd, 0);
+			CHECK(rc == 0, "sync verify between async posts %d", rc);
+		}
+	}
+	rc = gcs_wait(ctx, tk[(nt - 1) % 32]);
+	CHECK(rc == 0, "gcs_wait (last) %d", rc);
+	for (i = 0; i < n; i++) {
+		uint32_t c2 = 0;
+		int s2 = ref_tx_fill(ref + off[i], len[i], &c2);
+		if (s2 != st[i] || (s2 == 0 && c2 != cs[i]))
+			bad++;
+	}
+	CHECK(memcmp(ref, buf, bytes) == 0, "async filled bytes differ from the oracle");
+	CHECK(bad == 0, "%u async statuses differ from the oracle", bad);
+	CHECK(gcs_wait(ctx, 0) == 0, "gcs_wait(0)");
+	printf("part 6 async fills (%s): %u frames in %u posts, mismatches %u\n",
+	       registered ? "registered" : "pageable", n, posts, bad);
+	gcs_ctx_destroy(ctx);
+	if (registered) {
+		CHECK(gcs_host_unregister(mem) == 0, "unregister");
+		free(mem);
+	}
+	free(src); free(ref); free(st); free(vd); free(ptrs); free(cs); free(off); free(len);
+}
+
 int main(void)
 {
 	uint64_t mism = 0, frames = 0;
@@ -322,6 +397,8 @@ int main(void)
 	part_registered();
 	part_plugin();
 	part_errors();
+	part_async(0);
+	part_async(1);
 	if (g_fail) {
 		printf("HOST DRIVER FAILED\n");
 		return 1;

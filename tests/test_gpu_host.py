@@ -272,3 +272,63 @@ def test_host_register_refuses_overlap(torch_dev):
         assert L.gcs_host_register(a + 2048, 4096) == gpucsum.K["GCS_EINVAL"]
     finally:
         gpucsum.check(L.gcs_host_unregister(a))
+
+
+@pytest.mark.parametrize("stage", ["host", "device"])
+def test_async_fill_many_outstanding(torch_dev, monkeypatch, stage):
+    """gcs_compute_ptrs_async: 40 posts of 1..120 frames without waiting (past
+    the 8 request slots, so posts finish older fills to reuse a slot), one
+    wait on an older ticket, then the last: every status, check and filled
+    frame equals the oracle.  GCS_ASYNC_STAGE=device stages in device memory."""
+    import ctypes as C
+    monkeypatch.setenv("GCS_ASYNC_STAGE", stage)
+    L = gpucsum.lib()
+    L.gcs_compute_ptrs_async.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                         C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64)]
+    L.gcs_wait.argtypes = [C.c_void_p, C.c_uint64]
+    buf, off, lens = synth.packed_frames(synth.imix_lengths(2400, seed=61), seed=62)
+    ref = buf.copy()
+    rst, rcs = Oracle().compute_batch(ref, off, lens)
+    ptrs = (C.c_void_p * len(off))(*[buf.ctypes.data + int(o) for o in off])
+    st = np.full(len(off), 0xEE, np.uint8)
+    cs = np.zeros(len(off), np.uint32)
+    rng = np.random.default_rng(63)
+    tickets = []
+    with gpucsum.Context(0, max_frames=4096, max_bytes=8 << 20) as c:
+        c.set_burst_server(True)
+        i = 0
+        while i < len(off):
+            m = min(int(rng.integers(1, 121)), len(off) - i)
+            t = C.c_uint64()
+            gpucsum.check(L.gcs_compute_ptrs_async(
+                c.h, C.cast(C.byref(ptrs, 8 * i), C.c_void_p), lens.ctypes.data + 2 * i, m,
+                st.ctypes.data + i, cs.ctypes.data + 4 * i, C.byref(t)))
+            assert t.value != 0
+            tickets.append(t.value)
+            i += m
+            if len(tickets) == 20:
+                gpucsum.check(L.gcs_wait(c.h, tickets[5]))
+        assert len(tickets) >= 25
+        gpucsum.check(L.gcs_wait(c.h, tickets[-1]))
+    np.testing.assert_array_equal(st, rst)
+    np.testing.assert_array_equal(cs, rcs)
+    np.testing.assert_array_equal(buf, ref)
+
+
+def test_async_fill_without_server_is_synchronous(torch_dev):
+    import ctypes as C
+    L = gpucsum.lib()
+    L.gcs_compute_ptrs_async.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                         C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64)]
+    buf, off, lens = synth.packed_frames(synth.imix_lengths(64, seed=71), seed=72)
+    ref = buf.copy()
+    rst, _ = Oracle().compute_batch(ref, off, lens)
+    ptrs = (C.c_void_p * len(off))(*[buf.ctypes.data + int(o) for o in off])
+    st = np.zeros(len(off), np.uint8)
+    t = C.c_uint64(123)
+    with gpucsum.Context(0, max_frames=1024, max_bytes=4 << 20) as c:
+        gpucsum.check(L.gcs_compute_ptrs_async(c.h, ptrs, lens.ctypes.data, len(off),
+                                               st.ctypes.data, None, C.byref(t)))
+    assert t.value == 0                     # done on return
+    np.testing.assert_array_equal(st, rst)
+    np.testing.assert_array_equal(buf, ref)

@@ -27,7 +27,7 @@ def run_driver(name, env_extra):
     p = subprocess.run([path], cwd=PLUGIN, env=env, capture_output=True, text=True, timeout=240)
     out = p.stdout + p.stderr
     assert p.returncode == 0 and "HOST DRIVER OK" in p.stdout, out[-4000:]
-    for part in ("part 1", "part 2", "part 3", "part 4", "part 5"):
+    for part in ("part 1", "part 2", "part 3", "part 4", "part 5", "part 6"):
         assert part in p.stdout
     return out
 
