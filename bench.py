@@ -640,14 +640,31 @@ def plugin_bursts(gcs, reps=300):
 
 def plugin_threads():
     """Bursts from several mTCP-like threads per GPU (tools/mt_probe.py), in a
-    child process with GPU_MAX_HW_QUEUES=16 as the plugin's load_module sets
-    it (this process's HIP runtime already runs with the default 4)."""
+    child process with HIP's default hardware queues, as the plugin runs."""
     import subprocess
-    env = dict(os.environ, GPU_MAX_HW_QUEUES="16")
     try:
-        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "mt_probe.py")], env=env,
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "mt_probe.py")],
                            capture_output=True, text=True, timeout=180)
         return json.loads(r.stdout.strip().splitlines()[-1])
+    except Exception as e:   # a side measurement: report, never fail the bench line
+        return {"error": repr(e)[:200]}
+
+
+def server_poll_cost():
+    """What idle burst-server rings cost the PCIe link (tools/poll_cost.py,
+    child process): the pinned verify's rate while 0, 8 and 12 other
+    contexts keep their rings of the process's grid alive with one 1-frame
+    burst every ~200 us."""
+    import subprocess
+    env = dict(os.environ, PC_KS="0,8,12,0")
+    try:
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "poll_cost.py")], env=env,
+                           capture_output=True, text=True, timeout=180)
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        quiet = d["K0"]["gib_per_s"]
+        for k in ("K8", "K12"):
+            d[k]["loss_vs_quiet"] = round(1 - d[k]["gib_per_s"] / quiet, 4)
+        return d
     except Exception as e:   # a side measurement: report, never fail the bench line
         return {"error": repr(e)[:200]}
 
@@ -779,6 +796,7 @@ def main():
             line["plugin_bursts"] = plugin_bursts(gpucsum)
             line["plugin_threads"] = plugin_threads()
             line["plugin_tx_async"] = plugin_tx_async()
+            line["server_poll_cost"] = server_poll_cost()
     ctx.close()
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -74,12 +74,11 @@
  * Frames whose queue is not this thread's own are counted in rx_foreign --
  * flows that mTCP's RSS-aware address pool (addr_pool.c:168,251) would have
  * placed on another core.
- * Burst server: each thread's context serves its bursts through a resident
- * grid polling a pinned mailbox (gcs_ctx_set_burst_server) unless the
- * environment sets GPUCSUM_BURST_SERVER=0 (then: one kernel launch per burst).
- * load_module sets GPU_MAX_HW_QUEUES=16 unless the environment already sets
- * it, before the process's first HIP call, so that every thread's grid has a
- * hardware queue of its own (mTCP runs cores / n_gpus threads per GPU).
+ * Burst server: each thread's context serves its bursts through the
+ * process's resident grid for its GPU, polling the context's request ring in
+ * pinned memory (gcs_ctx_set_burst_server), unless the environment sets
+ * GPUCSUM_BURST_SERVER=0 (then: one kernel launch per burst).  Up to 16
+ * threads per GPU share the grid; a 17th launches per burst.
  * Threading (core.c:1153-1245): load_module once on the main thread; every
  * other call from the owning mTCP thread.  Per-thread state is keyed by the
  * mtcp_thread_context pointer; mTCP thread k uses GPU k mod n_gpus (override:

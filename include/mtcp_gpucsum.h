@@ -140,12 +140,16 @@ int gcs_sync(gcs_ctx *ctx);                               /* wait for ctx stream
 
 /* Burst server (on = 1): host batches small enough for direct mode (the
  * kernel reads pinned staging over PCIe: an mTCP burst) are served by a
- * resident grid that polls a mailbox in pinned memory, instead of one kernel
- * launch and one event wait per batch.  The grid leaves after
- * GCS_SERVER_IDLE_US (default 200) without work and after GCS_SERVER_LIFE_US
- * (default 2000) in total; a later batch starts it again.  Other work on the
- * context makes it leave first.  Default: off, or the environment variable
- * GCS_BURST_SERVER=1 at gcs_ctx_create. */
+ * resident grid that polls a request ring in pinned memory, instead of one
+ * kernel launch and one event wait per batch.  ONE grid per process and
+ * device serves the rings of up to 16 contexts (one per mTCP thread; 8
+ * blocks each), on a highest-priority stream of its own; a 17th context gets
+ * GCS_ERANGE and runs without it.  The grid leaves after GCS_SERVER_LIFE_US
+ * (default 2000) in total, or when a ring's blocks have had no work for
+ * GCS_SERVER_IDLE_US (default 2000); a later batch starts it again.  A ring
+ * goes cold after GCS_SERVER_HOT_US (default 20; 0 = never) without a
+ * request: then one block, not eight, polls it over PCIe.  Default: off, or
+ * the environment variable GCS_BURST_SERVER=1 at gcs_ctx_create. */
 int gcs_ctx_set_burst_server(gcs_ctx *ctx, int on);
 
 /* Pinned host memory for zero-copy host batches: when every frame of a

@@ -232,49 +232,243 @@ class GatherPool {
 
 namespace {
 
-// Host side of the burst server (gcs_kernels.hip k_burst_server): small host
-// batches in direct mode are posted to a resident grid through a ring of
-// request slots in pinned fine-grained memory, instead of one kernel launch +
-// event wait each.  post() returns at once; wait(q) completes every request up
-// to q, in order.  The grid lives at most life_us and leaves after idle_us
-// without work; requests posted to a grid that has gone (or is going) are
-// served by a fresh launch, so every request completes and the grid never
-// outlives its bounds.
+// Host side of the burst server (gcs_kernels.hip k_burst_server).  One
+// ServerHub per device and process owns the resident grid, its stream and the
+// mailbox; each context with the server on owns one of its request rings
+// (BurstServer).  Small host batches in direct mode are posted to the ring
+// instead of one kernel launch + event wait each.  The grid lives at most
+// life_us and leaves after idle_us without work; a ring whose request finds
+// the grid gone (or going) starts a fresh one, which resumes every ring where
+// each block left it (HubPub::prog), so every request completes, none is
+// served twice, and the grid never outlives its bounds.  Callers hold the
+// device current (DeviceGuard).
+class ServerHub {
+  public:
+    static ServerHub* get(int device)
+    {
+        static std::mutex mu;
+        static ServerHub* hubs[64] = {};
+        if (device < 0 || device >= 64)
+            return nullptr;
+        std::lock_guard<std::mutex> lk(mu);
+        if (!hubs[device]) {
+            // process lifetime: never freed (a static destructor would run
+            // after the HIP runtime may have gone)
+            std::unique_ptr<ServerHub> h(new ServerHub());
+            if (h->init(device) != GCS_OK)
+                return nullptr;
+            hubs[device] = h.release();
+        }
+        return hubs[device];
+    }
+
+    // A context joins: ring index in *r, or GCS_ERANGE when kHubRings
+    // contexts of this process already use the device's grid.  The grid
+    // leaves first (it serves the rings of its launch only).
+    int join(uint32_t start, int* r)
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        int k = 0;
+        while (k < gcs::kHubRings && ((mask_ >> k) & 1u))
+            k++;
+        if (k == gcs::kHubRings)
+            return GCS_ERANGE;
+        int rc = stop_locked();
+        if (rc) return rc;
+        read_knobs();
+        std::memset(&mb_->ring[k], 0, sizeof(gcs::ServerMailbox));
+        // every slot reads as holding `start` (done): a slot left at 0 would
+        // read as NEWER than the next request near the 32-bit wrap, and be
+        // skipped as done
+        for (auto& sl : mb_->ring[k].slot)
+            sl.a.seq = start;
+        // the ring starts at `start` on the device too: nothing claimed yet
+        uint32_t prog[gcs::kServerBlocks];
+        for (auto& p : prog)
+            p = start;
+        uint64_t ent[gcs::kServerSlots];
+        for (auto& e : ent)
+            e = (uint64_t)start << 32;   // as for the slots: never newer than a request
+        HIP_TRY(hipMemcpyAsync(dpub_->prog[k], prog, sizeof prog, hipMemcpyHostToDevice, stream_));
+        HIP_TRY(hipMemcpyAsync(dpub_->ent[k], ent, sizeof ent, hipMemcpyHostToDevice, stream_));
+        HIP_TRY(hipStreamSynchronize(stream_));
+        mask_ |= 1u << k;
+        *r = k;
+        return GCS_OK;
+    }
+
+    // A context leaves (its requests all complete): the grid leaves too, and
+    // the next request of another ring starts one without this ring.
+    int leave(int r)
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        int rc = stop_locked();
+        mask_ &= ~(1u << r);
+        return rc;
+    }
+
+    // Make sure a grid whose group for ring r has not begun to leave serves
+    // it: start one if none runs or (a block of) r's group left.
+    int ensure(int r)
+    {
+        if (running(r))
+            return GCS_OK;
+        std::lock_guard<std::mutex> lk(mu_);
+        if (running(r))
+            return GCS_OK;
+        int rc = stop_locked();
+        if (rc) return rc;
+        return launch_locked();
+    }
+
+    bool running(int r) const
+    {
+        if (!launched_.load(std::memory_order_acquire))
+            return false;
+        const gcs::ServerMailbox& m = mb_->ring[r];
+        for (int b = 0; b < gcs::kServerBlocks; b++)
+            if (__atomic_load_n(&m.state[b].v, __ATOMIC_ACQUIRE) == 2)
+                return false;
+        return true;
+    }
+
+    // Ask the grid to leave and wait until it has (the exit path of a
+    // request that got no answer).
+    int stop()
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        return stop_locked();
+    }
+
+    gcs::ServerMailbox* ring(int r) { return &mb_->ring[r]; }
+    bool prof() const { return prof_; }
+    double ticks_per_us() const { return ticks_per_us_; }
+
+  private:
+    int init(int device)
+    {
+        HIP_TRY(hipHostMalloc((void**)&mb_, sizeof(gcs::HubMailbox),
+                              hipHostMallocCoherent | hipHostMallocMapped));
+        std::memset(mb_, 0, sizeof(gcs::HubMailbox));
+        HIP_TRY(hipHostGetDevicePointer((void**)&dmb_, mb_, 0));
+        HIP_TRY(hipMalloc((void**)&dpub_, sizeof(gcs::HubPub)));
+        HIP_TRY(hipMemset(dpub_, 0, sizeof(gcs::HubPub)));
+        // the highest priority: a queue pool of its own, so the resident grid
+        // holds back no context's launches behind it on a shared hardware queue
+        int least = 0, greatest = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIP_TRY(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, greatest));
+        int khz = 0;
+        HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
+        ticks_per_us_ = khz > 0 ? khz / 1000.0 : 100.0;
+        prof_ = std::getenv("GCS_SERVER_PROF") != nullptr;   // process-wide
+        read_knobs();
+        return GCS_OK;
+    }
+
+    // Read at each join (under mu_), so a process (a test) may change them
+    // between contexts.
+    void read_knobs()
+    {
+        // a group that leaves alone makes the next request of its ring restart
+        // the whole grid: idle rings go cold instead (hot_ticks), and by
+        // default only the lifetime ends the grid
+        const char* e = std::getenv("GCS_SERVER_IDLE_US");
+        idle_ticks_ = (uint64_t)((e ? std::atof(e) : 2000.0) * ticks_per_us_);
+        e = std::getenv("GCS_SERVER_LIFE_US");
+        life_ticks_ = (uint64_t)((e ? std::atof(e) : 2000.0) * ticks_per_us_);
+        // a ring without a request for this long goes cold: only the leader
+        // block polls its host lines (0: never cold)
+        e = std::getenv("GCS_SERVER_HOT_US");
+        const double hot_us = e ? std::atof(e) : 20.0;
+        hot_ticks_ = hot_us > 0 ? (uint64_t)(hot_us * ticks_per_us_) : ~0ull;
+        // extra ~2 us naps between the polls of a block with no hot ring
+        e = std::getenv("GCS_SERVER_COLD_NAPS");
+        cold_naps_ = e ? (uint32_t)std::atoi(e) : 0;
+    }
+
+    // Every block ends within life_ticks of its start (or at the exit
+    // command); the stream sync then confirms the grid has drained.
+    int stop_locked()
+    {
+        if (!launched_.load(std::memory_order_relaxed))
+            return GCS_OK;
+        __atomic_store_n(&mb_->cmd.v, 1u, __ATOMIC_RELEASE);
+        HIP_TRY(hipStreamSynchronize(stream_));
+        launched_.store(false, std::memory_order_release);
+        return GCS_OK;
+    }
+
+    // One group of kServerBlocks blocks per ring in use.
+    int launch_locked()
+    {
+        if (mask_ == 0)
+            return GCS_OK;
+        int groups = 0;
+        uint64_t ids = 0;
+        for (int k = 0; k < gcs::kHubRings; k++) {
+            if (!((mask_ >> k) & 1u))
+                continue;
+            for (auto& st : mb_->ring[k].state)
+                __atomic_store_n(&st.v, 0u, __ATOMIC_RELAXED);
+            ids |= (uint64_t)k << (4 * groups++);
+        }
+        __atomic_store_n(&mb_->cmd.v, 0u, __ATOMIC_RELEASE);
+        HIP_TRY(hipMemsetAsync(dpub_->exit, 0, sizeof dpub_->exit, stream_));
+        HIP_TRY(gcs::launch_burst_server(dmb_, dpub_, groups, ids, idle_ticks_, life_ticks_,
+                                         hot_ticks_, kMaxPolls, cold_naps_, prof_, stream_));
+        launched_.store(true, std::memory_order_release);
+        return GCS_OK;
+    }
+
+    static constexpr uint32_t kMaxPolls = 1u << 22;   // hard bound beside the clock
+    std::mutex mu_;
+    gcs::HubMailbox* mb_ = nullptr;       // host view
+    gcs::HubMailbox* dmb_ = nullptr;      // device view
+    gcs::HubPub* dpub_ = nullptr;         // device memory
+    hipStream_t stream_ = nullptr;
+    uint32_t mask_ = 0;                   // rings in use
+    std::atomic<bool> launched_{false};
+    uint64_t idle_ticks_ = 0, life_ticks_ = 0, hot_ticks_ = 0;
+    uint32_t cold_naps_ = 0;
+    bool prof_ = false;
+    double ticks_per_us_ = 100.0;
+};
+
+// One context's request ring.  post() returns at once; wait(q) completes
+// every request up to q, in order.  Used by one thread at a time (the
+// context's).
 class BurstServer {
   public:
     ~BurstServer()
     {
-        if (prof_ && prof_n_)
+        if (prof_n_)
             std::fprintf(stderr,
                          "[gcs burst server] %llu requests: request writes %.2f us; post->done "
                          "%.2f us, of which serving %.2f us and release fence %.2f us "
                          "(slowest block)\n",
                          (unsigned long long)prof_n_, prof_write_ / prof_n_, prof_total_ / prof_n_,
                          prof_serve_ / prof_n_, prof_release_ / prof_n_);
-        (void)stop();
-        if (stream_) (void)hipStreamDestroy(stream_);
-        if (mb_) (void)hipHostFree(mb_);
+        if (hub_ && r_ >= 0) {
+            (void)wait(posted_);
+            (void)hub_->leave(r_);
+        }
     }
 
     int init(int device)
     {
-        HIP_TRY(hipHostMalloc((void**)&mb_, sizeof(gcs::ServerMailbox),
-                              hipHostMallocCoherent | hipHostMallocMapped));
-        std::memset(mb_, 0, sizeof(gcs::ServerMailbox));
-        HIP_TRY(hipHostGetDevicePointer((void**)&dmb_, mb_, 0));
-        HIP_TRY(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-        int khz = 0;
-        HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
-        const double ticks_per_us = ticks_per_us_ = khz > 0 ? khz / 1000.0 : 100.0;
-        const char* e = std::getenv("GCS_SERVER_IDLE_US");
-        idle_ticks_ = (uint64_t)((e ? std::atof(e) : 200.0) * ticks_per_us);
-        e = std::getenv("GCS_SERVER_LIFE_US");
-        life_ticks_ = (uint64_t)((e ? std::atof(e) : 2000.0) * ticks_per_us);
-        prof_ = std::getenv("GCS_SERVER_PROF") != nullptr;
+        hub_ = ServerHub::get(device);
+        if (!hub_) {
+            std::snprintf(g_hip_err, sizeof g_hip_err, "burst server: hub setup failed");
+            return GCS_EHIP;
+        }
         // test-only (tests/test_gpu_host.py): start the request numbers near a
         // 16-bit tag or 32-bit wrap instead of after 65k real bursts
         if (const char* s = std::getenv("GCS_SERVER_SEQ_START"))
             posted_ = done_ = (uint32_t)std::strtoul(s, nullptr, 0);
+        int rc = hub_->join(done_, &r_);
+        if (rc) return rc;
+        mb_ = hub_->ring(r_);
         return GCS_OK;
     }
 
@@ -295,14 +489,8 @@ class BurstServer {
             int rc = wait(r.q);
             if (rc) return rc;
         }
-        if (launched_ && any_exited()) {
-            int rc = relaunch();
-            if (rc) return rc;
-        }
-        if (!launched_) {
-            int rc = launch();
-            if (rc) return rc;
-        }
+        int rc = hub_->ensure(r_);
+        if (rc) return rc;
         gcs::ServerSlot& sl = mb_->slot[q % gcs::kServerSlots];
         const auto tw = std::chrono::steady_clock::now();
         std::memset(sl.rec, 0, n * sizeof(uint64_t));   // no record of an older request
@@ -321,7 +509,7 @@ class BurstServer {
         sl.a.cmd = 0;
         r = Req{q, n, compute, in_place, true, code, csum, 0, std::chrono::steady_clock::now()};
         __atomic_store_n(&sl.a.seq, q, __ATOMIC_RELEASE);
-        if (prof_)
+        if (hub_->prof())
             prof_write_ += std::chrono::duration<double, std::micro>(r.t0 - tw).count();
         posted_ = q;
         if (ticket) *ticket = q;
@@ -357,16 +545,8 @@ class BurstServer {
         return wait(q);
     }
 
-    // Complete what is posted, ask the grid to leave and wait until it has.
-    int stop()
-    {
-        if (!launched_) return GCS_OK;
-        int rc = wait(posted_);
-        for (auto& sl : mb_->slot)
-            __atomic_store_n(&sl.a.cmd, 1u, __ATOMIC_RELEASE);
-        int rc2 = wait_exit();
-        return rc ? rc : rc2;
-    }
+    // Complete what is posted (the grid stays for the other rings).
+    int stop() { return wait(posted_); }
 
   private:
     struct Req {
@@ -379,7 +559,7 @@ class BurstServer {
     };
 
     // Wait until request r is done (its records, and for an in-place request
-    // the serving blocks' acks), relaunching the grid when it left before.
+    // the serving blocks' acks), starting a grid when the last one left first.
     int complete(Req& r)
     {
         const uint64_t tag = (uint64_t)(r.q & 0xFFFFu) << 48;
@@ -400,18 +580,15 @@ class BurstServer {
                 }
             if (all)
                 break;
-            if (!launched_ || any_exited()) {
+            if (!hub_->running(r_)) {
                 // the grid left (or is leaving) before serving r: a fresh grid
-                // serves every request after done_ again (blocks that had
-                // served one redo their share: the same results)
-                int rc = relaunch();
+                // resumes each block where it stopped
+                int rc = hub_->ensure(r_);
                 if (rc) return rc;
                 continue;
             }
             if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
-                for (auto& s2 : mb_->slot)
-                    __atomic_store_n(&s2.a.cmd, 1u, __ATOMIC_RELEASE);
-                (void)wait_exit();
+                (void)hub_->stop();
                 std::snprintf(g_hip_err, sizeof g_hip_err, "burst server: no answer in 2 s");
                 return GCS_EHIP;
             }
@@ -423,7 +600,7 @@ class BurstServer {
             if (r.compute && r.csum) r.csum[i] = (uint32_t)v;
         }
         r.pending = false;
-        if (prof_) {
+        if (hub_->prof()) {
             // GCS_SERVER_PROF: per request, the slowest serving block's serve
             // and release times (wall clock), averaged and printed at exit
             double sv = 0, rl = 0;
@@ -433,67 +610,20 @@ class BurstServer {
                 rl = std::max(rl, (double)(mb_->prof[b][2] - mb_->prof[b][1]));
             }
             prof_n_++;
-            prof_serve_ += sv / ticks_per_us_;
-            prof_release_ += rl / ticks_per_us_;
+            prof_serve_ += sv / hub_->ticks_per_us();
+            prof_release_ += rl / hub_->ticks_per_us();
             prof_total_ += std::chrono::duration<double, std::micro>(
                                std::chrono::steady_clock::now() - r.t0).count();
         }
         return GCS_OK;
     }
 
-    bool any_exited() const
-    {
-        for (int b = 0; b < gcs::kServerBlocks; b++)
-            if (__atomic_load_n(&mb_->state[b].v, __ATOMIC_ACQUIRE) == 2)
-                return true;
-        return false;
-    }
-
-    // Every block ends within life_ticks of its start (or at the exit
-    // command); the stream sync then confirms the grid has drained.
-    int wait_exit()
-    {
-        HIP_TRY(hipStreamSynchronize(stream_));
-        launched_ = false;
-        return GCS_OK;
-    }
-
-    // The grid (or part of it) left: make the rest leave, then start a fresh
-    // grid that serves every request after done_.
-    int relaunch()
-    {
-        if (launched_) {
-            for (auto& sl : mb_->slot)
-                __atomic_store_n(&sl.a.cmd, 1u, __ATOMIC_RELEASE);
-            int rc = wait_exit();
-            if (rc) return rc;
-        }
-        return launch();
-    }
-
-    int launch()
-    {
-        for (int b = 0; b < gcs::kServerBlocks; b++)
-            __atomic_store_n(&mb_->state[b].v, 0u, __ATOMIC_RELAXED);
-        for (auto& sl : mb_->slot)
-            __atomic_store_n(&sl.a.cmd, 0u, __ATOMIC_RELEASE);
-        HIP_TRY(gcs::launch_burst_server(dmb_, done_, idle_ticks_, life_ticks_, kMaxPolls,
-                                         prof_, stream_));
-        launched_ = true;
-        return GCS_OK;
-    }
-
-    static constexpr uint32_t kMaxPolls = 1u << 22;   // hard bound beside the clock
-    gcs::ServerMailbox* mb_ = nullptr;    // host view
-    gcs::ServerMailbox* dmb_ = nullptr;   // device view
-    hipStream_t stream_ = nullptr;
-    uint64_t idle_ticks_ = 0, life_ticks_ = 0;
+    ServerHub* hub_ = nullptr;
+    int r_ = -1;                          // ring index in the hub
+    gcs::ServerMailbox* mb_ = nullptr;    // this ring (host view)
     uint32_t posted_ = 0;                 // last request posted
     uint32_t done_ = 0;                   // last request completed (all before it too)
     Req req_[gcs::kServerSlots] = {};
-    bool launched_ = false;
-    bool prof_ = false;
-    double ticks_per_us_ = 100.0;
     uint64_t prof_n_ = 0;
     double prof_total_ = 0, prof_serve_ = 0, prof_release_ = 0, prof_write_ = 0;
 };
@@ -850,8 +980,8 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
                 if (rc) return rc;
             } else {
                 if (ctx->server) {
-                    // a resident grid on a shared hardware queue would hold this
-                    // launch back until its idle or lifetime exit
+                    // this context's posted requests complete first (the grid
+                    // runs on a queue of its own: it holds no launch back)
                     int rc = ctx->server->stop();
                     if (rc) return rc;
                 }
@@ -960,8 +1090,8 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
             continue;
         }
         if (ctx->server) {
-            // other work on this context's streams: the grid leaves first, so
-            // nothing queues behind it on a shared hardware queue
+            // other work on this context's streams: its posted requests
+            // complete first, in order
             int rc = ctx->server->stop();
             if (rc) return rc;
         }
@@ -1075,7 +1205,9 @@ try {
     if (const char* e = std::getenv("GCS_ASYNC_STAGE"))
         ctx->async_stage_dev = std::strcmp(e, "device") == 0;
     if (const char* e = std::getenv("GCS_BURST_SERVER")) {
-        if (std::atoi(e) != 0 && (rc = gcs_ctx_set_burst_server(ctx, 1)) != GCS_OK) {
+        // a context beyond the grid's kHubRings runs without it (GCS_ERANGE)
+        if (std::atoi(e) != 0 && (rc = gcs_ctx_set_burst_server(ctx, 1)) != GCS_OK &&
+            rc != GCS_ERANGE) {
             gcs_ctx_destroy(ctx);
             return rc;
         }
@@ -1102,7 +1234,7 @@ try {
         return GCS_EINVAL;
     {
         DeviceGuard g(ctx->device);
-        ctx->server.reset();   // exit command, wait for the grid to drain
+        ctx->server.reset();   // its requests complete; the ring leaves the grid
         for (auto& a : ctx->areq)
             if (a.h_stage) (void)(a.stage_dev ? hipFree(a.h_stage) : hipHostFree(a.h_stage));
         for (auto& s : ctx->slot) {

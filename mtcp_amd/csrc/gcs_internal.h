@@ -17,18 +17,23 @@ struct Ext {
     uint32_t nq, nq_magic, endian;   // nq_magic = ceil(2^32 / nq) (0 for nq == 1)
 };
 
-// Burst server (gcs_api.cpp BurstServer, gcs_kernels.hip k_burst_server): a
-// short-lived resident grid that takes host batches from a mailbox in pinned
-// fine-grained memory instead of one kernel launch per batch.
+// Burst server (gcs_api.cpp ServerHub / BurstServer, gcs_kernels.hip
+// k_burst_server): ONE short-lived resident grid per process and device that
+// takes host batches from the request rings of up to kHubRings contexts (one
+// per mTCP thread) in pinned fine-grained memory, instead of one kernel
+// launch per batch -- and instead of one resident grid per context, each
+// holding a hardware queue of its own (12 per-context grids
+// cost the pinned verify 6-15%).  The grid has kServerBlocks blocks per ring
+// in use (a ring's group); ring ids of the groups travel in the launch.
 //
-// The mailbox is a ring of kServerSlots request slots.  Request q (a 32-bit
+// A context's ring is kServerSlots request slots.  Request q (a 32-bit
 // sequence number; numbers whose low 16 bits are 0 are never used, see
 // server_next) lives in slot q % kServerSlots, so the host can post
 // requests while earlier ones are still being served (the plugin's TX fill
-// posts frames as mTCP completes them).  Every block serves the requests in
-// order.  Request q's frames go to the blocks in turn starting at block
-// q % kServerBlocks (kServerFPB frames per block and pass), so a run of small
-// requests is served by different blocks at once.
+// posts frames as mTCP completes them).  Every block of the ring's group
+// serves its requests in order.  Request q's frames go to the blocks in turn
+// starting at block q % kServerBlocks (kServerFPB frames per block and pass),
+// so a run of small requests is served by different blocks at once.
 //
 // One poll is ONE load instruction of wave 0 of a block: lane 0 reads the
 // slot's line A, lane 1 its line B, lanes 2.. the descriptors of the block's
@@ -37,16 +42,23 @@ struct Ext {
 // needs has a consistent request (the host writes each line's fields before
 // its seq, and the lines before line A's seq).  Results go to tagged
 // per-frame records in the slot; a block that served frames of q then
-// releases and writes ack[b] = q (what the host waits for when the frames
-// themselves were written in place).
+// releases and writes the ring's ack[b] = q (what the host waits for when the
+// frames themselves were written in place).
+//
+// A block that has seen no request for hot_ticks goes cold: the group's
+// block 0 (its leader) then reads only line A per poll and publishes each
+// request it claims in HubPub (device memory); the other blocks follow that
+// copy instead of polling host memory, and go hot again when a request has
+// frames for them.
 constexpr int kServerBlocks = 8;
 constexpr int kServerFPB = 8;            // frames per block and pass (32 lanes x 3 chunks each)
 constexpr int kServerSlots = 8;
 constexpr int kSlotFrames = 512;         // frames per request
 constexpr int kServerMaxFrames = 4096;   // a larger synchronous batch: several requests
+constexpr int kHubRings = 16;            // contexts one grid serves (4-bit ring ids)
 struct alignas(16) ServerReqA {
     uint32_t seq;                       // request number (written last)
-    uint32_t cmd;                       // 0 = serve, 1 = exit now
+    uint32_t cmd;                       // unused (0)
     uint32_t n;                         // frames
     uint32_t mode;                      // bit 0: compute (TX fill); bits 1..: flags
 };
@@ -76,12 +88,33 @@ struct alignas(64) ServerSlot {
     // seq -- without waiting for the blocks' release fence and ack.
     uint64_t rec[kSlotFrames];
 };
+// One context's request ring.
 struct ServerMailbox {
     ServerLine ack[kServerBlocks];       // device: the last request each block served frames of
-    ServerLine state[kServerBlocks];     // device: 1 serving, 2 exited
+    ServerLine state[kServerBlocks];     // device: 1 serving, 2 exited (this launch's group)
     uint64_t prof[kServerBlocks][8];     // device, GCS_SERVER_PROF: wall-clock marks of
                                          // the block's last request (seen, served, released)
     ServerSlot slot[kServerSlots];
+};
+struct HubMailbox {
+    ServerLine cmd;                      // host: 1 = leave now (the group leaders poll it)
+    ServerMailbox ring[kHubRings];
+};
+
+// Device memory.  ent[r][q % kServerSlots] = q << 32 | n for each request q
+// of ring r its group's leader claimed (n = 0 for one it skipped); exit[r] =
+// that leader left.  prog[r][b] = the last request of ring r that block b
+// finished: a fresh grid resumes there, so no block serves a request twice.
+// The host sets a ring's entries (to the ring's start: "done") when a context
+// joins, and clears exit[] before each launch.
+struct alignas(16) PubFlag {
+    uint32_t v;
+    uint32_t pad[3];
+};
+struct HubPub {
+    uint64_t ent[kHubRings][kServerSlots];
+    PubFlag exit[kHubRings];
+    uint32_t prog[kHubRings][kServerBlocks];
 };
 
 // The request number after q: q + 1, skipping numbers whose 16-bit record tag
@@ -99,9 +132,11 @@ __host__ __device__ inline int server_block(uint32_t q, uint32_t i)
     return (int)((q + i / kServerFPB) % kServerBlocks);
 }
 
-hipError_t launch_burst_server(ServerMailbox* mb, uint32_t done_seq, uint64_t idle_ticks,
-                               uint64_t life_ticks, uint32_t max_polls, bool prof,
-                               hipStream_t s);
+// groups rings, ring_ids: 4 bits per group (group g serves ring
+// (ring_ids >> 4g) & 15); the grid is groups * kServerBlocks blocks.
+hipError_t launch_burst_server(HubMailbox* mb, HubPub* pub, int groups, uint64_t ring_ids,
+                               uint64_t idle_ticks, uint64_t life_ticks, uint64_t hot_ticks,
+                               uint32_t max_polls, uint32_t cold_naps, bool prof, hipStream_t s);
 
 hipError_t launch_verify_fixed(uint8_t* frames, uint64_t stride, uint32_t frame_len, uint32_t n,
                                uint8_t* verdict, uint32_t flags, hipStream_t s);

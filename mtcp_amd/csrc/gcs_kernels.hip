@@ -213,164 +213,207 @@ k_desc(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __re
                                                 out_csum ? out_csum + i : nullptr);
 }
 
-// Burst server: a grid of kServerBlocks blocks that stays resident for at most
-// life_ticks (wall clock) and serves host batches posted in the mailbox's
-// request ring (gcs_internal.h ServerMailbox) -- each batch with the per-frame
-// work of k_desc<G,U> (frames in pinned host memory, read and written over
-// PCIe), without a kernel launch and event wait per batch.  Each block serves
-// every request in order (q = server_next(last)); its frames of request q are
-// i = kServerFPB * ((b - q) mod kServerBlocks) + grp, then + 64 per pass.
+// Burst server: a grid of kServerBlocks blocks per ring in use that stays
+// resident for at most life_ticks (wall clock) and serves the host batches
+// posted in the contexts' request rings (gcs_internal.h HubMailbox) -- each
+// batch with the per-frame work of k_desc<G,U> (frames in pinned host memory,
+// read and written over PCIe), without a kernel launch and event wait per
+// batch.  Group g (blocks 8g..8g+7) serves ring (ring_ids >> 4g) & 15: each of
+// its blocks serves every request in order (q = server_next(last)); its
+// frames of request q are i = kServerFPB * ((b - q) mod kServerBlocks) + grp,
+// then + 64 per pass.
 //
-// Every block ends: on the host's exit command (cmd in the slot it polls),
-// after idle_ticks without a request, after life_ticks in total, or after
-// max_polls polls -- whichever comes first, so the grid always drains and work
-// queued behind it on the same hardware queue waits at most life_ticks.  All
-// decisions are taken by thread 0 from the poll's lines in LDS and broadcast
-// (block-uniform control flow: no wave leaves the loop while another waits at
-// a barrier).
-template <int G, int U, bool PROF, int kPollWaves>
+// Every block ends: on the host's exit command (which each group's leader
+// polls and publishes), after idle_ticks without a request, after life_ticks
+// in total, or after max_polls polls -- whichever comes first, so the grid
+// always drains.  All decisions are taken by wave 0 from the poll's lines
+// and broadcast through LDS (block-uniform control flow: no wave leaves the
+// loop while another waits at a barrier).
+template <int G, int U, bool PROF>
 __global__ void __launch_bounds__(kBlock)
-k_burst_server(ServerMailbox* mb, uint32_t done_seq, uint64_t idle_ticks, uint64_t life_ticks,
-               uint32_t max_polls)
+k_burst_server(HubMailbox* mb, HubPub* pub, uint64_t ring_ids, uint64_t idle_ticks,
+               uint64_t life_ticks, uint64_t hot_ticks, uint32_t max_polls, uint32_t cold_naps)
 {
     enum { IDLE = 0, WORK = 1, EXIT = 2, SKIP = 3 };
     constexpr int FPB = kBlock / G;
     static_assert(FPB == kServerFPB, "the mailbox's frames per block and pass");
     constexpr int kPass = kServerBlocks * FPB;          // frames of one request per pass
-    // kPollWaves = 2: a second wave polls half a round trip behind the first
-    __shared__ uint4 s_line[2 + FPB];
-    __shared__ uint32_t s_claim;             // IDLE until a polling wave claims WORK / EXIT
+    constexpr int kLanes = 2 + FPB;                     // lines of a poll
+    __shared__ uint4 s_line[kLanes];
+    __shared__ uint32_t s_claim;
     __shared__ uint8_t s_code[FPB];          // a frame's results, packed into its record
     __shared__ uint32_t s_csum[FPB];
     const int t = threadIdx.x, sub = t & (G - 1), grp = t / G;
     const int wave = t >> 6, lane = t & 63;
-    uint32_t last = done_seq, polls = 0;
+    const int blk = blockIdx.x % kServerBlocks;
+    const int r = (int)((ring_ids >> (4 * (blockIdx.x / kServerBlocks))) & 15u);
+    const bool leader = blk == 0;
+    ServerMailbox* rm = &mb->ring[r];
+    uint32_t last = pub->prog[r][blk], polls = 0;
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-    uint64_t t_last = t_start;
+    uint64_t t_last = t_start;               // this block's last request (hot window, idle exit)
     if (t == 0) {
         s_claim = IDLE;
-        __hip_atomic_store(&mb->state[blockIdx.x].v, 1u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&rm->state[blk].v, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     __syncthreads();
     for (;;) {
         const uint32_t q = server_next(last);            // the request this block serves next
-        ServerSlot* sl = &mb->slot[q % kServerSlots];
-        const uint32_t first = (uint32_t)FPB * ((blockIdx.x + kServerBlocks - q % kServerBlocks) %
+        ServerSlot* sl = &rm->slot[q % kServerSlots];
+        const uint32_t first = (uint32_t)FPB * ((blk + kServerBlocks - q % kServerBlocks) %
                                                 kServerBlocks);   // this block's first frame of q
-        if (wave < kPollWaves) {
-            // what lane < 2 + FPB of a polling wave reads each poll
-            const volatile u32x4* src = nullptr;
-            if (lane == 0)
-                src = reinterpret_cast<const volatile u32x4*>(&sl->a);
-            else if (lane == 1)
-                src = reinterpret_cast<const volatile u32x4*>(&sl->b);
-            else if (lane < 2 + FPB)
-                src = reinterpret_cast<const volatile u32x4*>(&sl->desc[first + lane - 2]);
-            if (wave == 1)
-                __builtin_amdgcn_s_sleep(32);   // stagger: ~2k cycles behind wave 0
+        if (wave == 0) {
             for (;;) {
-                if (__hip_atomic_load(&s_claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
-                    break;                      // the other polling wave has claimed
+                const uint64_t now = __builtin_amdgcn_s_memrealtime();
+                const bool hot = now - t_last <= hot_ticks;
+                // ONE load per lane, all in flight together: the lines of q
+                // when hot (the leader reads line A when cold too), the
+                // leader's entry for q's slot for a cold follower (the 16 B
+                // pair holding it), and in lane 63 the exit flag (the host's
+                // command for the leader; the leader's exit, every 8th poll,
+                // for the others)
+                const bool follow = !hot && !leader && lane == 0;
+                const volatile u32x4* src = nullptr;
+                if ((hot && lane < kLanes) || (leader && lane == 0))
+                    src = lane == 0   ? reinterpret_cast<const volatile u32x4*>(&sl->a)
+                          : lane == 1 ? reinterpret_cast<const volatile u32x4*>(&sl->b)
+                                      : reinterpret_cast<const volatile u32x4*>(&sl->desc[first + lane - 2]);
+                else if (follow)
+                    src = reinterpret_cast<const volatile u32x4*>(
+                        &pub->ent[r][(q % kServerSlots) & ~1u]);
+                else if (lane == 63 && (leader || (polls & 7) == 0))
+                    src = leader ? reinterpret_cast<const volatile u32x4*>(&mb->cmd.v)
+                                 : reinterpret_cast<const volatile u32x4*>(&pub->exit[r].v);
                 u32x4 v = {0, 0, 0, 0};
                 if (src)
-                    v = *src;                   // one 16 B read per lane, one round trip
-                // lane 0 judges the poll from the lanes' lines (wave-wide shuffles)
-                const uint32_t aq = __shfl(v.x, 0), cmd = __shfl(v.y, 0), n = __shfl(v.z, 0);
-                const uint32_t bseq = __shfl(v.w, 1);
-                bool ok = bseq == q;
-                for (int j = 0; j < FPB; j++) {
-                    const uint32_t dseq = __shfl(v.w, 2 + j);
-                    if (first + j < n && dseq != q)
-                        ok = false;
+                    v = *src;
+                // line A's (seq, n), or the leader's entry's (q, n)
+                uint32_t dq = v.x, dn = v.z;
+                if (follow) {
+                    dq = (q & 1u) ? v.w : v.y;
+                    dn = (q & 1u) ? v.z : v.x;
                 }
-                const uint64_t now = __builtin_amdgcn_s_memrealtime();
+                const uint32_t x0 = __shfl(dq, 0), z0 = __shfl(dn, 0);
+                // a consistent poll has seq q in line B and in the descriptor
+                // lines of the block's frames: each lane checks its own line
+                const bool torn = hot && lane >= 1 && lane < kLanes &&
+                                  first + (lane >= 2 ? lane - 2 : 0) < z0 && v.w != q;
+                const bool ok = __ballot(torn) == 0;
                 uint32_t act = IDLE;
-                if (cmd != 0 || now - t_start > life_ticks || ++polls >= max_polls)
-                    act = EXIT;
-                else if (aq == q)
-                    act = ok ? WORK : IDLE;     // torn poll: look again
-                else if ((int32_t)(aq - q) > 0)
-                    act = SKIP;                 // q is done and its slot reused: this block
+                if (hot) {
+                    if (x0 == q)
+                        act = ok ? WORK : IDLE;  // torn poll: look again
+                    else if ((int32_t)(x0 - q) > 0)
+                        act = SKIP;             // q is done and its slot reused: this block
                                                 // had no frames in it (the host reuses a slot
                                                 // only after its request completed)
-                else if (now - t_last > idle_ticks)
+                } else if (leader) {
+                    if (x0 == q && first >= z0) {
+                        act = WORK;             // out, none of its frames here: publish n
+                    } else if (x0 == q) {
+                        // out: publish it now, so the other blocks start their
+                        // polls of it while this one reads its lines
+                        if (lane == 0)
+                            __hip_atomic_store(&pub->ent[r][q % kServerSlots],
+                                               ((uint64_t)q << 32) | z0, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                        t_last = now;
+                    } else if ((int32_t)(x0 - q) > 0) {
+                        act = SKIP;
+                    }
+                } else {
+                    // the leader's entry for q's slot: q itself (skip it unless
+                    // it has frames here), a newer request (q is done), or older
+                    if (x0 == q && first < z0)
+                        t_last = now;
+                    else if ((int32_t)(x0 - q) >= 0)
+                        act = SKIP;
+                }
+                if (__shfl(v.x, 63) != 0 || now - t_start > life_ticks || ++polls >= max_polls ||
+                    (act == IDLE && now - t_last > idle_ticks))
                     act = EXIT;
                 if (act == IDLE) {
                     __builtin_amdgcn_s_sleep(2);
+                    if (!hot)
+                        for (uint32_t k = 0; k < cold_naps; k++)
+                            __builtin_amdgcn_s_sleep(63);   // ~4k cycles a nap
                     continue;
                 }
-                uint32_t won = 0;
                 if (lane == 0)
-                    won = atomicCAS(&s_claim, (uint32_t)IDLE, act) == IDLE;
-                won = __shfl(won, 0);
-                if (won && lane < 2 + FPB)
+                    s_claim = act;
+                if (act == WORK && lane < kLanes)
                     s_line[lane] = make_uint4(v.x, v.y, v.z, v.w);
                 break;
             }
         }
         __syncthreads();
         const uint32_t act = s_claim;
-        if (act == EXIT)
+        if (act == EXIT) {
+            if (leader && t == 0)
+                __hip_atomic_store(&pub->exit[r].v, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
-        if (act == SKIP) {
-            __syncthreads();                 // every thread has read s_claim
-            if (t == 0)
-                s_claim = IDLE;
-            last = q;
-            t_last = __builtin_amdgcn_s_memrealtime();
-            __syncthreads();
-            continue;
         }
-        // a request: its lines were written before its seq (fence-acquire
-        // after observing it: later loads see everything the host wrote)
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        const uint64_t t_seen = __builtin_amdgcn_s_memrealtime();
-        const uint4 a = s_line[0], b = s_line[1];
-        const uint32_t n = a.z, compute = a.w & 1u, flags = a.w >> 1;
-        uint8_t* frames = reinterpret_cast<uint8_t*>((uint64_t)b.x | ((uint64_t)b.y << 32));
-        const uint64_t bytes = (uint64_t)b.z * 16;
-        const uint4 d0 = s_line[2 + grp];
-        const bool mine = first < n;                     // block-uniform: frames of q here
-        for (uint32_t i = first + grp, pass = 0; i < n; i += kPass, pass++) {
-            const uint4 d = pass == 0 ? d0 : *reinterpret_cast<const uint4*>(&sl->desc[i]);
-            const uint64_t o = (uint64_t)d.x | ((uint64_t)d.y << 32);
-            const u32 len = d.z & 0xFFFFu;
-            const bool ok = (o & 15) == 0 && o <= bytes && len <= bytes - o;
-            uint8_t* f = frames + (ok ? o : 0);
-            const int64_t avail = ok ? (int64_t)(bytes - o) : 0;
-            s_csum[grp] = 0;
-            if (compute)
-                do_frame<G, U, true, true, true, kNT, kWM>(f, len, avail, ok, sub, flags,
-                                                           s_code + grp, s_csum + grp);
-            else
-                do_frame<G, U, false, true, true, kNT, kWM>(f, len, avail, ok, sub, flags,
-                                                            s_code + grp, nullptr);
-            if (sub == 0) {                  // the group's results, in one 8 B store
-                const uint64_t r = (uint64_t)s_csum[grp] | ((uint64_t)s_code[grp] << 32) |
-                                   ((uint64_t)(q & 0xFFFFu) << 48);
-                __hip_atomic_store(&sl->rec[i], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (leader && t == 0) {
+            // the leader publishes what it claimed before serving it: one
+            // self-describing 8 B entry (no ordering against other stores)
+            const uint64_t e = ((uint64_t)q << 32) | (act == WORK ? s_line[0].z : 0u);
+            __hip_atomic_store(&pub->ent[r][q % kServerSlots], e, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        bool mine = false;
+        uint64_t t_seen = 0, t_served = 0;
+        if (act == WORK) {
+            // a request: its lines were written before its seq (fence-acquire
+            // after observing it: later loads see everything the host wrote)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            t_seen = __builtin_amdgcn_s_memrealtime();
+            const uint4 a = s_line[0], b = s_line[1];
+            const uint32_t n = a.z, compute = a.w & 1u, flags = a.w >> 1;
+            uint8_t* frames = reinterpret_cast<uint8_t*>((uint64_t)b.x | ((uint64_t)b.y << 32));
+            const uint64_t bytes = (uint64_t)b.z * 16;
+            const uint4 d0 = s_line[2 + grp];
+            mine = first < n;                            // block-uniform: frames of q here
+            for (uint32_t i = first + grp, pass = 0; i < n; i += kPass, pass++) {
+                const uint4 d = pass == 0 ? d0 : *reinterpret_cast<const uint4*>(&sl->desc[i]);
+                const uint64_t o = (uint64_t)d.x | ((uint64_t)d.y << 32);
+                const u32 len = d.z & 0xFFFFu;
+                const bool ok = (o & 15) == 0 && o <= bytes && len <= bytes - o;
+                uint8_t* f = frames + (ok ? o : 0);
+                const int64_t avail = ok ? (int64_t)(bytes - o) : 0;
+                s_csum[grp] = 0;
+                if (compute)
+                    do_frame<G, U, true, true, true, kNT, kWM>(f, len, avail, ok, sub, flags,
+                                                               s_code + grp, s_csum + grp);
+                else
+                    do_frame<G, U, false, true, true, kNT, kWM>(f, len, avail, ok, sub, flags,
+                                                                s_code + grp, nullptr);
+                if (sub == 0) {                  // the group's results, in one 8 B store
+                    const uint64_t rv = (uint64_t)s_csum[grp] | ((uint64_t)s_code[grp] << 32) |
+                                        ((uint64_t)(q & 0xFFFFu) << 48);
+                    __hip_atomic_store(&sl->rec[i], rv, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+                }
             }
+            if (PROF && mine) {
+                __syncthreads();
+                t_served = __builtin_amdgcn_s_memrealtime();
+            }
+            if (mine)
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // this wave's results reach host memory
         }
-        uint64_t t_served = 0;
-        if (PROF && mine) {
-            __syncthreads();
-            t_served = __builtin_amdgcn_s_memrealtime();
-        }
-        if (mine)
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // this wave's results reach host memory
         __syncthreads();                     // every wave done with s_line / s_claim
         if (t == 0) {
             if (PROF && mine) {
-                mb->prof[blockIdx.x][0] = t_seen;
-                mb->prof[blockIdx.x][1] = t_served;
-                mb->prof[blockIdx.x][2] = __builtin_amdgcn_s_memrealtime();
-                mb->prof[blockIdx.x][3] = polls;
+                rm->prof[blk][0] = t_seen;
+                rm->prof[blk][1] = t_served;
+                rm->prof[blk][2] = __builtin_amdgcn_s_memrealtime();
+                rm->prof[blk][3] = polls;
             }
-            s_claim = IDLE;
             if (mine)
-                __hip_atomic_store(&mb->ack[blockIdx.x].v, q, __ATOMIC_RELEASE,
+                __hip_atomic_store(&rm->ack[blk].v, q, __ATOMIC_RELEASE,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&pub->prog[r][blk], q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_claim = IDLE;
         }
         last = q;
         t_last = __builtin_amdgcn_s_memrealtime();
@@ -379,22 +422,22 @@ k_burst_server(ServerMailbox* mb, uint32_t done_seq, uint64_t idle_ticks, uint64
     __threadfence_system();
     __syncthreads();
     if (t == 0)
-        __hip_atomic_store(&mb->state[blockIdx.x].v, 2u, __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&rm->state[blk].v, 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-hipError_t launch_burst_server(ServerMailbox* mb, uint32_t done_seq, uint64_t idle_ticks,
-                               uint64_t life_ticks, uint32_t max_polls, bool prof,
-                               hipStream_t s)
+hipError_t launch_burst_server(HubMailbox* mb, HubPub* pub, int groups, uint64_t ring_ids,
+                               uint64_t idle_ticks, uint64_t life_ticks, uint64_t hot_ticks,
+                               uint32_t max_polls, uint32_t cold_naps, bool prof, hipStream_t s)
 {
-    // One polling wave: a second one, half a round trip behind, measured no
-    // faster (64 x 1500 B: 8.5-9.2 vs 8.5-8.7 us, profiles/r02/burst_latency.md).
+    if (groups < 1 || groups > kHubRings)
+        return hipErrorInvalidValue;
+    const dim3 grid(kServerBlocks * groups);
     if (prof)
-        hipLaunchKernelGGL((k_burst_server<32, 3, true, 1>), dim3(kServerBlocks), dim3(kBlock),
-                           0, s, mb, done_seq, idle_ticks, life_ticks, max_polls);
+        hipLaunchKernelGGL((k_burst_server<32, 3, true>), grid, dim3(kBlock), 0, s, mb, pub,
+                           ring_ids, idle_ticks, life_ticks, hot_ticks, max_polls, cold_naps);
     else
-        hipLaunchKernelGGL((k_burst_server<32, 3, false, 1>), dim3(kServerBlocks), dim3(kBlock),
-                           0, s, mb, done_seq, idle_ticks, life_ticks, max_polls);
+        hipLaunchKernelGGL((k_burst_server<32, 3, false>), grid, dim3(kBlock), 0, s, mb, pub,
+                           ring_ids, idle_ticks, life_ticks, hot_ticks, max_polls, cold_naps);
     return hipGetLastError();
 }
 

@@ -158,12 +158,10 @@ static void gpucsum_load_module(void)
 		fprintf(stderr, "[gpucsum] no inner I/O module: call gpucsum_set_inner() first\n");
 		exit(EXIT_FAILURE);
 	}
-	/* Before the process's first HIP call: one hardware queue per burst grid.
-	 * mTCP puts cores / n_gpus threads on each GPU, each context with its own
-	 * resident grid; with HIP's default 4 queues, grids beyond the fourth wait
-	 * behind others (8 threads per GPU: 32.7 us per burst with 4 queues,
-	 * 11.6 us with 16; tests/test_gpu_mt.py).  An explicit setting wins. */
-	setenv("GPU_MAX_HW_QUEUES", "16", 0);
+	/* HIP's default hardware queues suffice: the threads of one GPU share
+	 * one resident burst grid, on a stream of its own (gcs_api.cpp
+	 * ServerHub; 12 threads per GPU: 23 us per burst with 4 queues, 22 us
+	 * with 16, tools/mt_probe.py) */
 	rc = gcs_device_count(&n);
 	if (rc || n <= 0)
 		die("gcs_device_count (no MI355X visible)", rc ? rc : GCS_ENODEV);
@@ -209,15 +207,17 @@ static void gpucsum_init_handle(struct mtcp_thread_context *ctx)
 	env = getenv("GPUCSUM_BURST_SERVER");
 	if (!env || atoi(env) != 0) {
 		rc = gcs_ctx_set_burst_server(g->gcs, 1);
-		if (rc)
+		if (rc && rc != GCS_ERANGE)
 			die("gcs_ctx_set_burst_server", rc);
+		/* GCS_ERANGE: 16 threads of this process already share the
+		 * device's grid; this one launches per burst */
 		/* fill as you go: a TX frame is complete once mTCP asks for the next
 		 * one or for its checksum (tcp_out.c:239-333); every
 		 * GPUCSUM_TX_GROUP (default 8, 0 = off) completed frames go to the
 		 * server while mTCP builds the rest, so send_pkts waits only for
 		 * the last group */
 		env = getenv("GPUCSUM_TX_GROUP");
-		g->tx_group = env ? (uint32_t)atoi(env) : 8;
+		g->tx_group = rc ? 0 : env ? (uint32_t)atoi(env) : 8;
 	}
 	env = getenv("GPUCSUM_RSS_QUEUES");
 	if (env && atoi(env) > 0) {

@@ -332,3 +332,97 @@ def test_async_fill_without_server_is_synchronous(torch_dev):
     assert t.value == 0                     # done on return
     np.testing.assert_array_equal(st, rst)
     np.testing.assert_array_equal(buf, ref)
+
+
+@pytest.mark.parametrize("life_us", [2000, 150])
+def test_hub_serves_many_contexts_at_once(torch_dev, monkeypatch, life_us):
+    """One grid per process serves the rings of 12 contexts, one per thread,
+    posting at once (mTCP threads on one GPU); contexts join while the grid
+    serves the others (each join makes it leave and restart), and with a
+    150 us lifetime the grid also leaves mid-traffic and a fresh one resumes
+    every ring where each block stopped.  Every burst equals the oracle."""
+    import threading
+    monkeypatch.setenv("GCS_SERVER_LIFE_US", str(life_us))
+    O = Oracle()
+    errors = []
+
+    def worker(w):
+        try:
+            with gpucsum.Context(0, max_frames=1024, max_bytes=4 << 20) as c:
+                c.set_burst_server(True)
+                for k, (buf, off, lens) in enumerate(bursts(12, 64, 1000 + 37 * w)):
+                    b1 = buf.copy()
+                    st, cs = c.compute_host(b1, off, lens)
+                    ref = buf.copy()
+                    rst, rcs = O.compute_batch(ref, off, lens)
+                    np.testing.assert_array_equal(st, rst)
+                    np.testing.assert_array_equal(cs, rcs)
+                    np.testing.assert_array_equal(b1, ref)
+                    bad = synth.corrupt(ref, off, lens, frac_log2=2, seed=k + w)
+                    v = c.verify_host(ref.copy(), off, lens)
+                    np.testing.assert_array_equal(v, O.verify_batch(ref.copy(), off, lens))
+                    assert (v[bad] != 0).all()
+        except Exception as e:                 # noqa: BLE001 (re-raised below)
+            errors.append((w, e))
+
+    th = [threading.Thread(target=worker, args=(w,)) for w in range(12)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not any(t.is_alive() for t in th)
+    assert not errors, errors[:2]
+
+
+def test_hub_ring_limit(torch_dev):
+    """A 17th context of the process gets GCS_ERANGE from
+    gcs_ctx_set_burst_server and still serves its bursts (launch per batch);
+    a ring freed by a leaving context is taken again."""
+    L = gpucsum.lib()
+    O = Oracle()
+    ctxs = [gpucsum.Context(0, max_frames=256, max_bytes=1 << 20) for _ in range(17)]
+    try:
+        for c in ctxs[:16]:
+            c.set_burst_server(True)
+        assert L.gcs_ctx_set_burst_server(ctxs[16].h, 1) == gpucsum.K["GCS_ERANGE"]
+        for j, c in enumerate(ctxs):
+            buf, off, lens = bursts(1, 64, 1300 + j)[0]
+            v = c.verify_host(buf.copy(), off, lens)
+            np.testing.assert_array_equal(v, O.verify_batch(buf.copy(), off, lens))
+        ctxs[3].set_burst_server(False)
+        gpucsum.check(L.gcs_ctx_set_burst_server(ctxs[16].h, 1))
+        buf, off, lens = bursts(1, 64, 1400)[0]
+        v = ctxs[16].verify_host(buf.copy(), off, lens)
+        np.testing.assert_array_equal(v, O.verify_batch(buf.copy(), off, lens))
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+def test_hub_grid_holds_no_launch_back(torch_dev, monkeypatch):
+    """The resident grid runs on a highest-priority stream of its own: while
+    it stays resident (idle and lifetime exits set to 5 s), another context's
+    launches -- a DMA batch too large for the server -- finish in well under
+    the grid's lifetime instead of queueing behind it."""
+    import time
+    monkeypatch.setenv("GCS_SERVER_IDLE_US", "5000000")
+    monkeypatch.setenv("GCS_SERVER_LIFE_US", "5000000")
+    O = Oracle()
+    big = bursts(1, 20000, 1500)[0]
+    with gpucsum.Context(0, max_frames=1024, max_bytes=4 << 20) as cs, \
+            gpucsum.Context(0, max_frames=1 << 15, max_bytes=32 << 20) as cb:
+        cs.set_burst_server(True)
+        buf, off, lens = bursts(1, 64, 1501)[0]
+        np.testing.assert_array_equal(cs.verify_host(buf.copy(), off, lens),
+                                      O.verify_batch(buf.copy(), off, lens))
+        buf, off, lens = big
+        cb.verify_host(buf.copy(), off, lens)          # warm-up (first launches)
+        t0 = time.perf_counter()
+        v = cb.verify_host(buf.copy(), off, lens)
+        dt = time.perf_counter() - t0
+        np.testing.assert_array_equal(v, O.verify_batch(buf.copy(), off, lens))
+        assert dt < 0.5, dt
+        # and the grid still serves
+        buf, off, lens = bursts(1, 64, 1502)[0]
+        np.testing.assert_array_equal(cs.verify_host(buf.copy(), off, lens),
+                                      O.verify_batch(buf.copy(), off, lens))

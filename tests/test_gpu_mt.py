@@ -1,12 +1,11 @@
 """Several mTCP-like threads on ONE GPU at once (tests/plugin/mt_bursts.c).
 
 mTCP maps thread k to GPU k mod n_gpus (gpucsum_module.c), so a 64-core host
-with 8 GPUs puts 8 threads -- 8 contexts, and with the burst server 8
-resident grids -- on each device, sharing its GPU_MAX_HW_QUEUES (4) hardware
-queues.  Each thread fills and verifies its own 64-frame bursts and checks
-every frame against the oracle; all must be exact, and no thread may stall
-(each grid leaves within its 2 ms lifetime, so a grid queued behind another
-on the same hardware queue still runs).
+with 8 GPUs puts 8 threads -- 8 contexts, with the burst server 8 rings of
+the process's one resident grid -- on each device, with HIP's default 4
+hardware queues.  Each thread fills and verifies its own 64-frame bursts and
+checks every frame against the oracle; all must be exact, and no thread may
+stall.
 """
 import ctypes as C
 import os

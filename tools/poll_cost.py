@@ -5,7 +5,10 @@ one-frame burst every ~200 us, so their grids stay resident and poll their
 mailboxes in host memory between bursts (as the grids of K mTCP threads per
 GPU do).  Meanwhile the main thread runs the PCIe-inclusive verify of
 bench.py (1M x 1500 B pinned host frames: H2D copies, kernel, D2H verdicts)
-and reports its rate for K = 0, 8, 12.  Prints one JSON object."""
+and reports its rate for K = 0, 8, 12 (PC_KS).  PC_HELPER_SERVER=0 runs the
+helpers without the burst server (a launch per burst): the control that
+separates what idle grids cost from what the helpers' bursts cost.  Prints
+one JSON object."""
 import ctypes as C
 import json
 import os
@@ -27,12 +30,14 @@ off = np.arange(N, dtype=np.uint64) * stride
 lens = np.full(N, FL, dtype=np.uint16)
 pinned = gpucsum.PinnedBuffer(src.nbytes)
 pinned.array[:] = src
+HELPER_SERVER = os.environ.get("PC_HELPER_SERVER", "1") != "0"
+KS = [int(k) for k in os.environ.get("PC_KS", "0,8,12,0").split(",")]
 
 
 def helper(stop, stats):
     one, ostride = synth.fixed_frames(1, 1500, seed=5)
     with gpucsum.Context(0, max_frames=64, max_bytes=1 << 20) as c:
-        c.set_burst_server(True)
+        c.set_burst_server(HELPER_SERVER)
         v = np.zeros(1, np.uint8)
         ptrs = (C.c_void_p * 1)(one.ctypes.data)
         ln = np.full(1, 1500, np.uint16)
@@ -47,10 +52,12 @@ def helper(stop, stats):
 out = {"workload": f"verify of {N} x {FL} B pinned host frames (gcs_verify: H2D, kernel, D2H) "
                    "while K other contexts' burst-server grids poll between 1-frame bursts "
                    "every ~200 us",
-       "GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES", "default (4)")}
+       "GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES", "default (4)"),
+       "helper_server": HELPER_SERVER,
+       "GCS_SERVER_HOT_US": os.environ.get("GCS_SERVER_HOT_US", "default (20)")}
 with gpucsum.Context(0, max_frames=1 << 16, max_bytes=96 << 20) as c:
     c.compute_host(pinned.array, off, lens)            # valid checks: every frame accepted
-    for K in (0, 8, 12, 0):
+    for K in KS:
         stop, stats = threading.Event(), []
         th = [threading.Thread(target=helper, args=(stop, stats)) for _ in range(K)]
         for t in th:
@@ -65,7 +72,9 @@ with gpucsum.Context(0, max_frames=1 << 16, max_bytes=96 << 20) as c:
         for t in th:
             t.join()
         assert int((codes != 0).sum()) == 0
-        key = f"K{K}" if f"K{K}" not in out else f"K{K}_again"
+        key = f"K{K}"
+        while key in out:
+            key += "_again"
         out[key] = {"gib_per_s": N * FL / dt / 2**30, "gb_per_s_h2d": N * stride / dt / 1e9,
                     "helper_bursts": int(sum(stats))}
 pinned.free()
