@@ -145,8 +145,8 @@ int gcs_sync(gcs_ctx *ctx);                               /* wait for ctx stream
  * device serves the rings of up to 16 contexts (one per mTCP thread; 8
  * blocks each), on a highest-priority stream of its own; a 17th context gets
  * GCS_ERANGE and runs without it.  The grid leaves after GCS_SERVER_LIFE_US
- * (default 2000) in total, or when a ring's blocks have had no work for
- * GCS_SERVER_IDLE_US (default 2000); a later batch starts it again.  A ring
+ * (default 10000) in total, or when a ring's blocks have had no work for
+ * GCS_SERVER_IDLE_US (default 10000); a later batch starts it again.  A ring
  * goes cold after GCS_SERVER_HOT_US (default 20; 0 = never) without a
  * request: then one block, not eight, polls it over PCIe.  Default: off, or
  * the environment variable GCS_BURST_SERVER=1 at gcs_ctx_create. */

@@ -374,9 +374,11 @@ class ServerHub {
         // the whole grid: idle rings go cold instead (hot_ticks), and by
         // default only the lifetime ends the grid
         const char* e = std::getenv("GCS_SERVER_IDLE_US");
-        idle_ticks_ = (uint64_t)((e ? std::atof(e) : 2000.0) * ticks_per_us_);
+        idle_ticks_ = (uint64_t)((e ? std::atof(e) : 10000.0) * ticks_per_us_);
         e = std::getenv("GCS_SERVER_LIFE_US");
-        life_ticks_ = (uint64_t)((e ? std::atof(e) : 2000.0) * ticks_per_us_);
+        // every ring waits for a relaunch: 10 ms (12 threads per GPU: 18 us
+        // per burst, 23 us with 2 ms; the grid holds no other launch back)
+        life_ticks_ = (uint64_t)((e ? std::atof(e) : 10000.0) * ticks_per_us_);
         // a ring without a request for this long goes cold: only the leader
         // block polls its host lines (0: never cold)
         e = std::getenv("GCS_SERVER_HOT_US");

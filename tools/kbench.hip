@@ -235,6 +235,109 @@ __global__ void __launch_bounds__(256) k_fill_ceiling(uint8_t* __restrict__ p,
 }
 
 // ---------------------------------------------------------------------------
+// Round 3b: a GLOBAL size-class partition, then one
+// homogeneous pass per class.  k_class_part writes, per class, entries
+// (off | len << 48) and the frame's index, wave by wave (a wave's frames keep
+// their order; waves are appended as they finish).  k_list_small serves the
+// <= 64 B class one lane per frame (as k_small does for fixed stride);
+// k_list<G,U> the others, G lanes per frame.  Outputs go to the frame's index.
+__device__ __forceinline__ int frame_class(u32 len, u32 c1max, u32 c2max)
+{
+    return len <= 64 ? 0 : (len <= c1max ? 1 : (len <= c2max ? 2 : 3));
+}
+
+__global__ void __launch_bounds__(256)
+k_class_part(const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens, u32 n,
+             u32 c1max, u32 c2max, uint64_t* __restrict__ ent, uint32_t* __restrict__ idx,
+             uint32_t* __restrict__ cnt, u32 cap)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const bool on = i < n;
+    const u32 L = on ? lens[i] : 0u;
+    const uint64_t o = on ? off[i] : 0;
+    const int c = on ? frame_class(L, c1max, c2max) : -1;
+    const uint64_t below = (1ull << lane) - 1;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint64_t m = __ballot(c == k);
+        if (!m)
+            continue;
+        uint32_t base = 0;
+        if (lane == __builtin_ctzll(m))
+            base = atomicAdd(&cnt[k], (uint32_t)__popcll(m));
+        base = __shfl(base, __builtin_ctzll(m));
+        if (c == k) {
+            const uint32_t pos = base + (uint32_t)__popcll(m & below);
+            ent[(uint64_t)k * cap + pos] = o | ((uint64_t)L << 48);
+            idx[(uint64_t)k * cap + pos] = (uint32_t)i;
+        }
+    }
+}
+
+template <bool COMPUTE>
+__global__ void __launch_bounds__(256)
+k_list_small(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __restrict__ ent,
+             const uint32_t* __restrict__ idx, u32 n, uint8_t* __restrict__ out_code,
+             uint32_t* __restrict__ out_csum, u32 flags)
+{
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);
+    const uint64_t i = (uint64_t)blk * 256 + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint64_t e = ent[i];
+    const uint64_t o = e & ((1ull << 48) - 1);
+    const u32 L = (u32)(e >> 48);
+    const uint32_t oi = idx[i];
+    const bool ok = (o & 15) == 0 && o <= frames_bytes && L <= frames_bytes - o;
+    uint8_t* f = frames + (ok ? o : 0);
+    const int nch = ok ? (int)((L + 15) >> 4) : 0;
+    uint4 v[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+        v[c] = c < nch ? ldg16<kNT>(f + 16 * c) : make_uint4(0, 0, 0, 0);
+    Hdr h = {v[0].w, v[1].x, v[1].y};
+    const int ts = 14 + 4 * (int)((h.d3 >> 16) & 15u);
+    const int te = 14 + (int)bswap16(h.d4 & 0xFFFFu);
+    Acc a = {0u, 0u, 0u};
+    if (ts == 34) {
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+            accum_fast5<COMPUTE, true>(v[c], c, te, masks5<COMPUTE>(c), a);
+    } else {
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+            accum_chunk<COMPUTE>(v[c], 16 * c, ts, te, a);
+    }
+    epilogue<1, 4, COMPUTE, WM_SECTOR_SC1, false>(h, a, f, L, ok ? (int64_t)(frames_bytes - o) : 0,
+                                                ok, 0, flags, out_code ? out_code + oi : nullptr,
+                                                out_csum ? out_csum + oi : nullptr, true, v,
+                                                XFrame{});
+}
+
+template <int G, int U, bool COMPUTE, int WM>
+__global__ void __launch_bounds__(256)
+k_list(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __restrict__ ent,
+       const uint32_t* __restrict__ idx, u32 n, uint8_t* __restrict__ out_code,
+       uint32_t* __restrict__ out_csum, u32 flags)
+{
+    constexpr int FPB = 256 / G;
+    const int sub = threadIdx.x & (G - 1);
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);
+    const uint64_t i = (uint64_t)blk * FPB + threadIdx.x / G;
+    if (i >= n)
+        return;
+    const uint64_t e = ent[i];
+    const uint64_t o = e & ((1ull << 48) - 1);
+    const u32 L = (u32)(e >> 48);
+    const uint32_t oi = idx[i];
+    const bool ok = (o & 15) == 0 && o <= frames_bytes && L <= frames_bytes - o;
+    do_frame<G, U, COMPUTE, true, true, kNT, WM>(frames + (ok ? o : 0), L,
+                                                 ok ? (int64_t)(frames_bytes - o) : 0, ok, sub,
+                                                 flags, out_code ? out_code + oi : nullptr,
+                                                 out_csum ? out_csum + oi : nullptr);
+}
+
 // MEASURED, NOT SHIPPED (round 3, DESIGN.md §4 "IMIX, round 3"): the class-split
 // blocks (k_desc_part: 339-435 us verify) and the whole block region through LDS
 // (k_desc_region: 501-783 us verify) on C3, against the list kernel's 276 us.
@@ -1269,6 +1372,57 @@ int imix_main(uint64_t n, int rounds)
     REGION(false, "F64 CAP32K G4 nt", kWM, 64, 32768, 4, true)
     REGION(false, "F48 CAP24K G4 nt", kWM, 48, 24576, 4, true)
     REGION(true, "F64 CAP32K G4 nt, sector nt", WM_SECTOR_NT, 64, 32768, 4, true)
+    }
+    // round 3b: global class partition + homogeneous passes (KB_GPART)
+    uint64_t* gent = nullptr;
+    uint32_t *gidx = nullptr, *gcnt = nullptr;
+    uint32_t hcnt[4] = {0, 0, 0, 0};
+    if (getenv("KB_GPART")) {
+        CK(hipMalloc(&gent, 8 * 4 * n));
+        CK(hipMalloc(&gidx, 4 * 4 * n));
+        CK(hipMalloc(&gcnt, 16));
+        CK(hipMemsetAsync(gcnt, 0, 16, s));
+        hipLaunchKernelGGL(k_class_part, dim3((n + 255) / 256), dim3(256), 0, s, doff, dlen, (u32)n,
+                           576u, 1536u, gent, gidx, gcnt, (u32)n);
+        CK(hipMemcpyAsync(hcnt, gcnt, 16, hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+        std::printf("classes: %u %u %u %u\n", hcnt[0], hcnt[1], hcnt[2], hcnt[3]);
+        auto passes = [&, n](hipStream_t st, bool C, int v2) {
+            uint8_t* fr = C ? tx : rx;
+            uint8_t* oc = C ? nullptr : v1;
+            const u32 n0 = hcnt[0], n1 = hcnt[1], n2 = hcnt[2];
+            if (n0)
+                hipLaunchKernelGGL((C ? k_list_small<true> : k_list_small<false>), dim3((n0 + 255) / 256),
+                                   dim3(256), 0, st, fr, total, gent, gidx, n0, oc, nullptr, 0u);
+            if (n1) {
+                if (v2 == 0)
+                    hipLaunchKernelGGL((C ? k_list<16, 3, true, WM_SECTOR_SC1> : k_list<16, 3, false, WM_SECTOR_SC1>),
+                                       dim3((n1 + 15) / 16), dim3(256), 0, st, fr, total, gent + n,
+                                       gidx + n, n1, oc, nullptr, 0u);
+                else
+                    hipLaunchKernelGGL((C ? k_list<8, 5, true, WM_SECTOR_SC1> : k_list<8, 5, false, WM_SECTOR_SC1>),
+                                       dim3((n1 + 31) / 32), dim3(256), 0, st, fr, total, gent + n,
+                                       gidx + n, n1, oc, nullptr, 0u);
+            }
+            if (n2)
+                hipLaunchKernelGGL((C ? k_list<32, 3, true, WM_SECTOR_SC1> : k_list<32, 3, false, WM_SECTOR_SC1>),
+                                   dim3((n2 + 7) / 8), dim3(256), 0, st, fr, total, gent + 2 * n,
+                                   gidx + 2 * n, n2, oc, nullptr, 0u);
+        };
+        auto part = [&, n](hipStream_t st) {
+            CK(hipMemsetAsync(gcnt, 0, 16, st));
+            hipLaunchKernelGGL(k_class_part, dim3((n + 255) / 256), dim3(256), 0, st, doff, dlen,
+                               (u32)n, 576u, 1536u, gent, gidx, gcnt, (u32)n);
+        };
+        vs.push_back({"verify  gpart passes only 64|16x3|32x3", vb, [=](hipStream_t st) { passes(st, false, 0); }});
+        vs.push_back({"verify  gpart passes only 64|8x5|32x3", vb, [=](hipStream_t st) { passes(st, false, 1); }});
+        vs.push_back({"verify  gpart partition + passes 64|16x3|32x3", vb, [=](hipStream_t st) { part(st); passes(st, false, 0); }});
+        vs.push_back({"verify  gpart partition alone", vb, [=](hipStream_t st) { part(st); }});
+        vs.push_back({"compute gpart passes only 64|16x3|32x3", cb, [=](hipStream_t st) { passes(st, true, 0); }});
+        vs.push_back({"compute gpart partition + passes FRESH", cb, [=](hipStream_t st) { part(st); passes(st, true, 0); }});
+        vs.back().prep = [&](hipStream_t st) {
+            hipLaunchKernelGGL(k_zero_checks_desc, dim3((n + 255) / 256), dim3(256), 0, st, tx, doff, dlen, n);
+        };
     }
     vs.push_back({"verify  desc (launch_verify_desc)", vb, [&](hipStream_t st) {
         CK(launch_verify_desc(rx, total, doff, dlen, (u32)n, v1, 0u, st));

@@ -71,6 +71,8 @@ ctx = C.create_string_buffer(64)
 out["software_path"] = run(vtab(H, "synth_module_func"), C.addressof(ctx), False)
 MODES = [(False, g, "host") for g in ("0", "8", "16")] + [(False, "8", "device")] + \
         [(True, g, "host") for g in ("0", "8", "16")]
+if os.environ.get("TXP_SMALL_GROUPS"):
+    MODES += [(False, g, st) for g in ("2", "4") for st in ("host", "device")]
 for registered, group, stage in MODES:
         os.environ["GPUCSUM_TX_GROUP"] = group
         os.environ["GCS_ASYNC_STAGE"] = stage
