@@ -2054,7 +2054,13 @@ int lro_main(uint64_t n, int rounds)
     }});
     GROO(2, 64, 6)
     // round 3: more bytes in flight per wave (U) against waves per SIMD (OCC)
+    if (getenv("KB_GRO_SHAPES")) {   // measured r03: none faster (kbench_lro_shapes.log)
     GROO(3, 64, 5) GROO(3, 64, 6) GROO(4, 64, 4) GROO(4, 64, 5) GROO(2, 64, 8) GROO(4, 64, 6)
+    }
+    // round 3b: two batches in flight per wave (k_gro PIPE: batch b + 1's loads
+    // issued before batch b is assembled, folded and stored) measured 929-1766 us
+    // against 766 us (spills: 32-176 B per lane; profiles/r03/kbench_lro_pipe.log);
+    // removed from the kernel
     vs.push_back({"verify (launch_verify_desc) for scale", (double)n * (L + 1), [&](hipStream_t st) {
         CK(launch_verify_desc(in, n * stride, off, lens, (u32)n, vd, 0u, st));
     }});
