@@ -146,6 +146,32 @@ __device__ __forceinline__ u32 group_sum(u32 x)
     return x;
 }
 
+// Inclusive prefix sum (u32, wrapping) over the 64 lanes of a wave, on DPP:
+// row_shr 1/2/4/8 inside each 16-lane row, then row_bcast:15 (rows 1, 3) and
+// row_bcast:31 (rows 2, 3).  A lane whose source lies outside its row, or a
+// row the mask leaves out, adds `old` = 0.  Every lane must be active.
+__device__ __forceinline__ u32 wave_incl_scan(u32 x)
+{
+    x += (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);
+    x += (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);
+    x += (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);
+    x += (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);
+    x += (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+    x += (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
+    return x;
+}
+
+// Sum of the LE 16-bit words of chunk v inside its first r bytes (r in
+// [0, 16]); a word straddling r (r odd) keeps its low byte, the reference's
+// odd-tail rule (tcp_util.c:262-263).
+__device__ __forceinline__ u32 chunk_prefix_sum(uint4 v, int r)
+{
+    u32 s = hsum(v.x & low_mask(r));
+    s = sad(v.y & low_mask(r - 4), s);
+    s = sad(v.z & low_mask(r - 8), s);
+    return sad(v.w & low_mask(r - 12), s);
+}
+
 // Value of lane SRC (< G) of this lane's G-group.
 template <int G, int SRC>
 __device__ __forceinline__ u32 group_bcast(u32 x)

@@ -747,6 +747,339 @@ k_desc_mixed_x(uint8_t* __restrict__ frames, uint64_t frames_bytes,
 }
 
 // ---------------------------------------------------------------------------
+// Packed descriptor batches as a prefix-sum stream (IMIX, C3).
+//
+// A frame's TCP fold over [ts, te) is a difference of two prefix sums of the
+// block region's 16-bit words: sum[a, b) = Q(b) - Q(a), exact in u32 because
+// one frame's words sum to < 2^32 (len < 64 KiB) and wrap-around cancels in
+// the difference.  So the block's packed region is read ONCE, as four plain
+// streams (one per wave, 1 KiB per load instruction, no per-frame group
+// shapes, no class passes): each lane folds its chunk to one word sum, a DPP
+// wave scan turns the sums into chunk prefixes, and the lanes holding a
+// frame's first chunks or last chunk park what the per-frame step needs in
+// LDS -- chunks 0..3 (the headers, and for TX the sector that is written
+// back), the prefix at the frame's first chunk, and Q at the frame's end.
+// Then one lane per frame parses its headers from LDS, folds chunks 0..3 with
+// the list kernels' exact masks (accum_chunk) and adds the words [64, te) as
+// Q(te) - Q(64), then runs the shared epilogue (verdict, or fill into the
+// staged sector).  Per-frame results are identical as integers to the group
+// kernels' (the same words, the same u32 sums).
+//
+// Fast frames: ihl <= 8 (IP header, doff byte and tcph->check inside chunks
+// 0..3) and te <= 64 or te == len (the segment ends at the frame's end, as
+// every frame mTCP builds).  Other frames of the block go to one list pass on
+// 32 x 3 lanes (desc_class, as desc_mixed's class 2).  A block streams only
+// when its frames are valid, non-empty, in offset order, chunk-disjoint with
+// gaps <= 64 B, and the region (<= RMAX chunks) ends inside the buffer;
+// otherwise it runs desc_mixed's three class passes.  Reference layout:
+// PSIO's packed chunk (pslib.c:132-156, ps.h:181-213).
+template <int U_, int RMAX_, int OCC_, bool PIPE_ = false, int PROBE_ = 0>
+struct StreamShape {
+    static constexpr int U = U_;          // chunks per lane per trip (64 * U per wave)
+    static constexpr int RMAX = RMAX_;    // region chunks a streaming block may span
+    static constexpr int OCC = OCC_;
+    static constexpr bool PIPE = PIPE_;   // issue trip k+1's loads before folding trip k
+    static constexpr int PROBE = PROBE_;  // A/B (kbench): 1 = phase 2 loads only, 2 = no phase 3
+    static_assert(RMAX % 64 == 0 && RMAX <= 65536, "start chunks fit 16 bits");
+};
+
+template <class S, class T, bool COMPUTE, bool XCD>
+__device__ __forceinline__ void desc_stream(uint8_t* __restrict__ frames, uint64_t frames_bytes,
+                                            const uint64_t* __restrict__ off,
+                                            const uint16_t* __restrict__ lens, u32 n,
+                                            uint8_t* __restrict__ out_code,
+                                            uint32_t* __restrict__ out_csum, u32 flags)
+{
+    static_assert(S::F == kBlock && S::R == 1, "one descriptor per thread");
+    static_assert(!COMPUTE || S::STAGE, "TX stages sector 0 in hdr");
+    constexpr int F = kBlock, NW = kBlock / 64, RW = T::RMAX / 64, U = T::U;
+    __shared__ uint64_t soff[F];
+    __shared__ uint16_t slen[F];
+    __shared__ uint16_t list[3][F];
+    __shared__ int cnt[3];
+    __shared__ int wcnt[3][NW];
+    __shared__ uint8_t codes[F];
+    __shared__ uint32_t csums[COMPUTE ? F : 1];
+    __shared__ uint4 hdr[4 * F];       // chunks 0..3 per frame; TX: the staged sector 0
+    __shared__ uint64_t bm[RW];        // bit c: a frame starts at region chunk c
+    __shared__ uint16_t rbase[RW];     // frames starting before chunk 64 * w
+    __shared__ u32 meta[F];            // start chunk << 16 | len
+    __shared__ u32 pfirst[F];          // wave-local prefix at the first chunk
+    __shared__ u32 qend[F];            // wave-local Q(len)
+    __shared__ u32 wtot[NW];
+    __shared__ u32 nchunks_s;
+
+    const uint32_t blk = XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint64_t f0 = (uint64_t)blk * F;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int nf = (int)((n - f0) < (uint64_t)F ? (n - f0) : (uint64_t)F);
+    if (t < 3)
+        cnt[t] = 0;
+
+    // phase 0: validate, classify (for the list passes), test streamability
+    int cls = -1;
+    uint64_t o = 0;
+    u32 len = 0;
+    if (t < nf) {
+        o = off[f0 + t];
+        len = lens[f0 + t];
+        const bool ok = (o & 15) == 0 && o <= frames_bytes && len <= frames_bytes - o;
+        if (!ok) {
+            codes[t] = COMPUTE ? GCS_TX_BAD_DESC : GCS_V_BAD_DESC;
+            if (COMPUTE)
+                csums[t] = 0;
+        } else {
+            soff[t] = o;
+            slen[t] = (uint16_t)len;
+            cls = len <= (u32)S::T0 ? 0 : (len <= (u32)S::T1 ? 1 : 2);
+        }
+    }
+    const u32 nch = (len + 15) >> 4;
+    // streamability, and each frame's place in the region (chunks from frame
+    // 0's start): its first chunk and the next frame's (the last frame: NCH)
+    const uint64_t r0 = off[f0];
+    u32 start = 0, snext = 0;
+    bool sok = t >= nf || (cls >= 0 && len > 0);
+    if (sok && t < nf) {
+        if (o < r0 || ((o - r0) >> 4) + nch > (uint64_t)T::RMAX) {
+            sok = false;
+        } else {
+            start = (u32)((o - r0) >> 4);
+            if (t + 1 < nf) {
+                const uint64_t on = off[f0 + t + 1], e = o + 16ull * nch;
+                sok = on >= e && on - e <= 64;
+                snext = (u32)((on - r0) >> 4);
+            } else {
+                sok = o + 16ull * nch <= frames_bytes;
+                snext = start + nch;
+                nchunks_s = snext;
+            }
+        }
+    }
+    for (int r = t; r < RW; r += kBlock)
+        bm[r] = 0;
+    // the three ordered class lists (desc_mixed's phase 0, R = 1)
+    {
+        const uint64_t below = (1ull << lane) - 1;
+        int rank = 0;
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            const uint64_t m = __ballot(cls == c);
+            if (lane == 0)
+                wcnt[c][w] = __popcll(m);
+            if (cls == c)
+                rank = __popcll(m & below);
+        }
+        const bool stream = __syncthreads_and(sok);
+        if (!stream) {
+            if (cls >= 0) {
+                int base = 0;
+                for (int k = 0; k < w; k++)
+                    base += wcnt[cls][k];
+                list[cls][base + rank] = (uint16_t)t;
+            }
+            if (t < 3) {
+                int tot = 0;
+                for (int k = 0; k < NW; k++)
+                    tot += wcnt[t][k];
+                cnt[t] = tot;
+            }
+            __syncthreads();
+            const int n0 = cnt[0], n1 = cnt[1], n2 = cnt[2];
+            uint4* stg = COMPUTE ? hdr : nullptr;
+            if (n0) desc_class<S::G0, S::U0, COMPUTE, false, false, S::WM, S::K0, S::NT>(frames, frames_bytes, soff, slen, list[0], n0, flags, codes, csums, Ext{}, nullptr, nullptr, stg);
+            if (n1) desc_class<S::G1, S::U1, COMPUTE, false, false, S::WM, S::K1, S::NT>(frames, frames_bytes, soff, slen, list[1], n1, flags, codes, csums, Ext{}, nullptr, nullptr, stg);
+            if (n2) desc_class<S::G2, S::U2, COMPUTE, true, false, S::WM, 1, S::NT>(frames, frames_bytes, soff, slen, list[2], n2, flags, codes, csums, Ext{}, nullptr, nullptr, stg);
+            __syncthreads();
+            desc_tail<S, COMPUTE, false>(frames, frames_bytes, f0, n, soff, slen, codes, csums,
+                                         nullptr, nullptr, hdr, out_code, out_csum, flags, Ext{});
+            return;
+        }
+    }
+
+    // phase 1: the region's first-chunk bitmap, per-frame metadata, and per
+    // 64-chunk row the number of frames starting before it (frame t owns the
+    // rows r with start_t < 64 r <= start_t+1)
+    const u32 NCH = nchunks_s, NR = (NCH + 63) >> 6;
+    if (t < nf) {
+        meta[t] = start << 16 | len;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if ((u32)k >= nch)
+                hdr[4 * t + k] = make_uint4(0, 0, 0, 0);
+        atomicOr((unsigned long long*)&bm[start >> 6], 1ull << (start & 63));
+        const u32 rhi = t + 1 < nf ? snext >> 6 : NR - 1;
+        for (u32 r = (start >> 6) + 1; r <= rhi; r++)
+            rbase[r] = (uint16_t)(t + 1);
+    }
+    if (t == 0)
+        rbase[0] = 0;
+    __syncthreads();
+
+    // phase 2: wave w streams chunks [w*QW, (w+1)*QW) of the region
+    {
+        const u32 QW = ((NCH + 4 * 64 - 1) / (4 * 64)) * 64;
+        const u32 lo = w * QW, hi = (lo + QW < NCH) ? lo + QW : NCH;
+        const uint8_t* reg = frames + r0;
+        u32 run = 0;
+        auto load_trip = [&](u32 base, uint4 (&v)[U]) {
+#pragma unroll
+            for (int j = 0; j < U; j++) {
+                const u32 c = base + 64 * j + lane;
+                v[j] = c < hi ? ldg16<S::NT>(reg + 16ull * c) : make_uint4(0, 0, 0, 0);
+            }
+        };
+        auto fold_trip = [&](u32 base, const uint4 (&v)[U]) {
+            if constexpr (T::PROBE == 1) {
+                u32 x = 0;
+#pragma unroll
+                for (int j = 0; j < U; j++)
+                    x ^= v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
+                run += x;
+                return;
+            }
+#pragma unroll
+            for (int j = 0; j < U; j++) {
+                const u32 row = (base >> 6) + j;
+                if (64 * row >= hi)           // wave-uniform
+                    break;
+                const u32 c = 64 * row + lane;
+                const u32 s = hsum4(v[j]);
+                const u32 incl = wave_incl_scan(s);
+                const u32 excl = run + incl - s;
+                run += (u32)__builtin_amdgcn_readlane((int)incl, 63);
+                const uint64_t bits = bm[row];
+                const u32 below = __builtin_amdgcn_mbcnt_hi((u32)(bits >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((u32)bits, 0u));
+                const int f = (int)rbase[row] + (int)below + (int)((bits >> lane) & 1u) - 1;
+                if (c < hi) {
+                    const u32 m = meta[f], fl = m & 0xFFFFu;
+                    const u32 k = c - (m >> 16), fn = (fl + 15) >> 4;
+                    if (k < 4 && k < fn)
+                        hdr[4 * f + k] = v[j];
+                    if (k == 0)
+                        pfirst[f] = excl;
+                    if (k + 1 == fn)
+                        qend[f] = excl + chunk_prefix_sum(v[j], (int)(fl - 16 * k));
+                }
+            }
+        };
+        if constexpr (T::PIPE) {
+            uint4 v[U], vn[U];
+            if (lo < hi)
+                load_trip(lo, v);
+            for (u32 base = lo; base < hi; base += 64 * U) {
+                const u32 nb = base + 64 * U;
+                if (nb < hi)
+                    load_trip(nb, vn);
+                fold_trip(base, v);
+#pragma unroll
+                for (int j = 0; j < U; j++)
+                    v[j] = vn[j];
+            }
+        } else {
+            for (u32 base = lo; base < hi; base += 64 * U) {
+                uint4 v[U];
+                load_trip(base, v);
+                fold_trip(base, v);
+            }
+        }
+        if (lane == 0)
+            wtot[w] = run;
+    }
+    __syncthreads();
+
+    if constexpr (T::PROBE != 0) {
+        if (t == 0 && wtot[0] == 0x9E3779B9u)
+            out_code[f0] = 0xEE;              // keeps the probe's loads alive
+        if constexpr (T::PROBE == 2)
+            return;
+    }
+    // phase 3: one lane per frame
+    {
+        const u32 QW = ((NCH + 4 * 64 - 1) / (4 * 64)) * 64;
+        const int tf = t < nf ? t : 0;
+        const uint4 h4[4] = {hdr[4 * tf], hdr[4 * tf + 1], hdr[4 * tf + 2], hdr[4 * tf + 3]};
+        Hdr h;
+        h.d3 = h4[0].w;
+        h.d4 = h4[1].x;
+        h.d5 = h4[1].y;
+        const int ihl = (int)((h.d3 >> 16) & 15u);
+        const int ts = 14 + 4 * ihl;
+        const int te = 14 + (int)bswap16(h.d4 & 0xFFFFu);
+        const bool fast = t < nf && ihl <= 8 && (te <= 64 || te == (int)len);
+        // wave-uniform: every fast frame of the wave has ihl == 5, so the word
+        // masks of chunks 0..3 are constants (masks5, as the group kernels);
+        // and when every one also has te >= 64, no segment end lies in them
+        const bool all5 = __all(!fast || ihl == 5);
+        const bool end64 = __all(!fast || te >= 64);
+        // RX: fast frames' verdicts go straight out (coalesced, frame order)
+        uint8_t* oc = (!COMPUTE && out_code) ? out_code + f0 + t : codes + t;
+        if (t < nf && !fast) {
+            list[2][atomicAdd(&cnt[2], 1)] = (uint16_t)t;
+        } else if (fast) {
+            Acc a = {0u, 0u, 0u};
+            if (all5 && end64) {
+#pragma unroll
+                for (int c = 0; c < 4; c++)
+                    accum_fast5<COMPUTE, true>(h4[c], c, 64, masks5<COMPUTE>(c), a);
+            } else if (all5) {
+#pragma unroll
+                for (int c = 0; c < 4; c++)
+                    accum_fast5<COMPUTE, true>(h4[c], c, te, masks5<COMPUTE>(c), a);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    accum_chunk<COMPUTE>(h4[j], 16 * j, ts, te, a);
+            }
+            if (te > 64) {
+                auto wbase = [&](u32 c) {
+                    const u32 q = c / QW;
+                    u32 b = 0;
+#pragma unroll
+                    for (int k = 0; k < NW - 1; k++)
+                        b += (u32)k < q ? wtot[k] : 0u;
+                    return b;
+                };
+                const u32 p0 = pfirst[t] + wbase(start);
+                const u32 p1 = qend[t] + wbase(start + nch - 1);
+                a.tcp += (p1 - p0) - (hsum4(h4[0]) + hsum4(h4[1]) + hsum4(h4[2]) + hsum4(h4[3]));
+            }
+            epilogue<1, 4, COMPUTE, S::WM, false>(
+                h, a, frames + o, len, (int64_t)(frames_bytes - o), true, 0, flags, oc,
+                COMPUTE ? csums + t : nullptr, true, h4, XFrame{},
+                COMPUTE ? reinterpret_cast<uint8_t*>(hdr + 4 * t) : nullptr);
+        }
+    }
+    __syncthreads();
+    const int ns = cnt[2];
+    if (ns)
+        desc_class<S::G2, S::U2, COMPUTE, true, false, S::WM, 1, S::NT>(
+            frames, frames_bytes, soff, slen, list[2], ns, flags, codes, csums, Ext{}, nullptr,
+            nullptr, COMPUTE ? hdr : nullptr);
+    if constexpr (COMPUTE) {
+        __syncthreads();
+        desc_tail<S, COMPUTE, false>(frames, frames_bytes, f0, n, soff, slen, codes, csums,
+                                     nullptr, nullptr, hdr, out_code, out_csum, flags, Ext{});
+    } else if (ns && out_code) {
+        __syncthreads();
+        for (int i = t; i < ns; i += kBlock) {
+            const int ft = list[2][i];
+            out_code[f0 + ft] = codes[ft];
+        }
+    }
+}
+
+template <class S, class T, bool COMPUTE, bool XCD>
+__global__ void __launch_bounds__(kBlock, T::OCC)
+k_desc_stream(uint8_t* __restrict__ frames, uint64_t frames_bytes,
+              const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens, u32 n,
+              uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags)
+{
+    desc_stream<S, T, COMPUTE, XCD>(frames, frames_bytes, off, lens, n, out_code, out_csum, flags);
+}
+
+// ---------------------------------------------------------------------------
 // TX payload copy + fill (SendTCPPacket, tcp_out.c:316-333:
 // memcpy of the payload behind the TCP header, then TCPCalcChecksum over
 // header + payload, then IPOutput's ip_fast_csum, ip_out.c:172).  One pass:
@@ -1604,6 +1937,17 @@ hipError_t launch_classify_fixed(uint8_t* frames, uint64_t stride, u32 frame_len
                                        s);
 }
 
+// The shipped prefix-sum stream (k_desc_stream; tools/kbench.hip imix, DESIGN.md
+// §4): 8 chunks per lane per trip, block regions up to 12,288 chunks (192 KiB per
+// 256 frames; C3 blocks span ~91 KiB), 6 waves per SIMD (26-27 KB of LDS, 80
+// VGPRs).  4M IMIX frames against the list kernel on the same boxes: verify
+// 253-258 vs 284-289 us, fill (fresh check fields) 358-366 vs 428-431 us.  NT
+// loads for both (the stream fill with temporal loads: 374 vs 325 us).
+using StreamShip = StreamShape<8, 12288, 6>;
+template <bool COMPUTE>
+using DescStreamShip = DescShape<4, 1, 16, 3, 32, 3, COMPUTE ? WM_SECTOR_NT : kWM, kBlock, true,
+                                 1, 1, COMPUTE, true>;
+
 template <bool COMPUTE>
 static hipError_t launch_desc(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
                               const uint16_t* len, u32 n, uint8_t* code, uint32_t* csums,
@@ -1615,8 +1959,9 @@ static hipError_t launch_desc(uint8_t* frames, uint64_t frames_bytes, const uint
         hipLaunchKernelGGL((k_desc_mixed_x<S, COMPUTE, kXCD, kDescOcc>), grid, dim3(kBlock), 0, s,
                            frames, frames_bytes, off, len, n, code, csums, flags, ext);
     else
-        hipLaunchKernelGGL((k_desc_mixed<S, COMPUTE, kXCD, kDescOcc>), grid, dim3(kBlock), 0, s,
-                           frames, frames_bytes, off, len, n, code, csums, flags);
+        hipLaunchKernelGGL((k_desc_stream<DescStreamShip<COMPUTE>, StreamShip, COMPUTE, kXCD>),
+                           grid, dim3(kBlock), 0, s, frames, frames_bytes, off, len, n, code,
+                           csums, flags);
     return hipGetLastError();
 }
 

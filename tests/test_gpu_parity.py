@@ -247,6 +247,126 @@ def test_fuzz_desc_vs_oracle(torch_dev, ctx, O):
     np.testing.assert_array_equal(host(d), ref)
 
 
+def stream_case_frames(n, align, seed):
+    """Packed TCP frames for the prefix-sum stream kernel (k_desc_stream):
+    mostly fast frames (ihl 5, te == len, any length incl. odd), plus ihl 6-8
+    (fast, general masks), ihl 9-15 (slow list), te < len with padding (slow
+    when te > 64), and segments ending inside the first 64 B."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(54, 1515, size=n).astype(np.uint16)
+    lens[rng.random(n) < 0.4] = 64
+    m = rng.random(n) < 0.1
+    lens[m] = rng.integers(54, 80, size=int(m.sum()))
+    off, total = synth.packed_offsets(lens, align)
+    buf = rng.integers(0, 256, size=total + 64, dtype=np.uint8)
+    kinds = rng.choice(8, size=n, p=[0.55, 0.08, 0.06, 0.06, 0.07, 0.06, 0.06, 0.06])
+    for i in range(n):
+        o, L = int(off[i]), int(lens[i])
+        f = buf[o:o + L]
+        k = int(kinds[i])
+        ihl = {1: 6, 2: 7, 3: 8, 4: int(rng.integers(9, 16))}.get(k, 5)
+        ts = 14 + 4 * ihl
+        if ts + 20 > L:
+            ihl, ts = 5, 34
+        tot = L - 14
+        if k == 5:
+            tot = max(4 * ihl + 20, L - 14 - int(rng.integers(1, 40)))     # padded: te < len
+        elif k == 6:
+            tot = max(4 * ihl + 20, min(L - 14, int(rng.integers(40, 51))))  # te <= 64
+        elif k == 7 and L > 64:
+            tot = min(L - 14, 64 - 14)                                         # te == 64 < len
+        f[12], f[13] = 0x08, 0x00
+        f[14] = 0x40 | ihl
+        f[16], f[17] = tot >> 8, tot & 0xFF
+        f[23] = 6 if rng.random() > 0.03 else 17                            # some IP-only
+        f[24] = f[25] = 0
+        f[ts + 12] = 5 << 4
+        f[ts + 16] = f[ts + 17] = 0
+    return buf, off, lens
+
+
+@pytest.mark.parametrize("align", [16, 64])
+def test_desc_stream_paths_vs_oracle(torch_dev, ctx, O, align):
+    """Every path of the stream kernel against the oracle, bit-exact: fast
+    frames (constant and general masks, Q(te) - Q(64) for te == len), the slow
+    list, and whole blocks that fall back to the class passes (a gap > 64 B,
+    descriptors out of order, an empty frame)."""
+    t = torch_dev
+    n = 256 * 24 + 77                                # a partial last block
+    buf, off, lens = stream_case_frames(n, align, seed=align)
+    off = off.copy()
+    # block 3: one gap > 64 B (frames shifted up by 128 B from frame 3*256+10 on)
+    off[3 * 256 + 10:] += 128
+    buf = np.concatenate([buf, np.zeros(128, np.uint8)])
+    src = buf.copy()
+    for i in range(3 * 256 + 10, n):
+        o, L = int(off[i]), int(lens[i])
+        buf[o:o + L] = src[o - 128:o - 128 + L]
+    # block 5: two descriptors swapped (out of offset order)
+    a, b = 5 * 256 + 7, 5 * 256 + 8
+    off[a], off[b] = off[b], off[a]
+    lens[a], lens[b] = lens[b], lens[a]
+    # block 7: an empty frame
+    lens[7 * 256 + 3] = 0
+    doff, dlen = dev(t, off.view(np.int64)), dev(t, lens.view(np.int16))
+    # TX
+    ref = buf.copy()
+    rst, rcs = O.compute_batch(ref, off, lens)
+    d = dev(t, buf)
+    st = t.zeros(n, dtype=t.uint8, device="cuda")
+    cs = t.zeros(n, dtype=t.int32, device="cuda")
+    ctx.compute(d, doff, dlen, n, st, cs)
+    ctx.sync()
+    np.testing.assert_array_equal(host(st), rst)
+    np.testing.assert_array_equal(host(cs).view(np.uint32), rcs)
+    np.testing.assert_array_equal(host(d), ref)
+    assert len(np.unique(rst)) >= 3
+    # RX, with and without the tcp_in.c:1237 side effect, after corruption
+    bad = synth.corrupt(ref, off, np.maximum(lens, 15), frac_log2=3, seed=align + 1)
+    for flags in (0, 1):
+        d = dev(t, ref)
+        v = t.full((n,), 0xEE, dtype=t.uint8, device="cuda")
+        ctx.verify(d, doff, dlen, n, v, flags=flags)
+        ctx.sync()
+        exp = ref.copy()
+        rv = O.verify_batch(exp, off, lens, flags=flags)
+        np.testing.assert_array_equal(host(v), rv)
+        np.testing.assert_array_equal(host(d), exp)
+        assert (rv[bad[lens[bad] > 0]] != 0).any()
+
+
+def test_desc_stream_region_at_buffer_end(torch_dev, ctx, O):
+    """A streaming block whose region ends exactly at frames_bytes (16 B-
+    aligned: streamed; not aligned: the block falls back to guarded loads)."""
+    t = torch_dev
+    lens = synth.imix_lengths(300, seed=8)
+    lens[-1] = 1504
+    buf, off, lens = synth.packed_frames(lens, seed=9)
+    for last in (1504, 1497):
+        L = lens.copy()
+        L[-1] = last
+        nb = int(off[-1]) + int(L[-1])
+        raw = buf[:nb].copy()
+        raw[int(off[-1]) + 16] = (L[-1] - 14) >> 8
+        raw[int(off[-1]) + 17] = (L[-1] - 14) & 0xFF
+        ref = raw.copy()
+        rst, rcs = O.compute_batch(ref, off, L)
+        d = dev(t, raw)
+        st = t.zeros(len(L), dtype=t.uint8, device="cuda")
+        cs = t.zeros(len(L), dtype=t.int32, device="cuda")
+        ctx.compute(d, dev(t, off.view(np.int64)), dev(t, L.view(np.int16)), len(L), st, cs,
+                    frames_bytes=nb)
+        ctx.sync()
+        np.testing.assert_array_equal(host(st), rst)
+        np.testing.assert_array_equal(host(cs).view(np.uint32), rcs)
+        np.testing.assert_array_equal(host(d), ref)
+        v = t.full((len(L),), 0xEE, dtype=t.uint8, device="cuda")
+        ctx.verify(d, dev(t, off.view(np.int64)), dev(t, L.view(np.int16)), len(L), v,
+                   frames_bytes=nb)
+        ctx.sync()
+        assert (host(v) == 0).all()
+
+
 def test_bad_descriptors(torch_dev, ctx):
     t = torch_dev
     buf = t.zeros(4096, dtype=t.uint8, device="cuda")

@@ -1424,6 +1424,34 @@ int imix_main(uint64_t n, int rounds)
             hipLaunchKernelGGL(k_zero_checks_desc, dim3((n + 255) / 256), dim3(256), 0, st, tx, doff, dlen, n);
         };
     }
+    // round 3c: the region as a prefix-sum stream (k_desc_stream)
+#define STREAMV(C_, TAG, U_, RMAX_, OCC_, NT_, PIPE_, PROBE_)                               \
+    vs.push_back({std::string(C_ ? "compute" : "verify ") + " stream " + TAG,               \
+                  C_ ? cb : vb, [&](hipStream_t st) {                                      \
+        using S_ = DescShape<4, 1, 16, 3, 32, 3, C_ ? WM_SECTOR_NT : kWM, 256, true, 1, 1,  \
+                             C_, NT_>;                                                     \
+        using T_ = StreamShape<U_, RMAX_, OCC_, PIPE_, PROBE_>;                            \
+        hipLaunchKernelGGL((k_desc_stream<S_, T_, C_, true>), dim3((n + 255) / 256),       \
+                           dim3(256), 0, st, C_ ? tx : rx, total, doff, dlen, (u32)n,       \
+                           C_ ? nullptr : v1, nullptr, 0u);                                 \
+    }});                                                                                    \
+    if (C_)                                                                                 \
+        vs.back().prep = [&](hipStream_t st) {                                              \
+            hipLaunchKernelGGL(k_zero_checks_desc, dim3((n + 255) / 256), dim3(256), 0, st, \
+                               tx, doff, dlen, n);                                          \
+        };
+    // measured r03 (first version, general masks in phase 3): U8/U4 occ5 nt 281/282 us,
+    // temporal 283, occ4 276, PIPE (next trip's loads before the fold) 282/292, phases
+    // 0-2 alone 251 (list kernel 278-286); fill nt FRESH 325-366 (temporal 374; list
+    // kernel 385-431 on the same boxes)
+    // second version (fast5 phase 3, one barrier less), occ 6: verify 253 / 255 (U8 / U4),
+    // U4 phases 0-2 alone 238, read ceiling 230; fill FRESH 359-361 (list kernel 428)
+    STREAMV(false, "U8 occ6 R12K nt", 8, 12288, 6, true, false, 0)
+    STREAMV(false, "U8 occ6 R12K nt PROBE no phase 3", 8, 12288, 6, true, false, 2)
+    STREAMV(false, "U4 occ6 R12K nt", 4, 12288, 6, true, false, 0)
+    STREAMV(false, "U4 occ6 R12K nt PROBE no phase 3", 4, 12288, 6, true, false, 2)
+    STREAMV(true, "U8 occ6 R12K nt FRESH", 8, 12288, 6, true, false, 0)
+    STREAMV(true, "U4 occ6 R12K nt FRESH", 4, 12288, 6, true, false, 0)
     vs.push_back({"verify  desc (launch_verify_desc)", vb, [&](hipStream_t st) {
         CK(launch_verify_desc(rx, total, doff, dlen, (u32)n, v1, 0u, st));
     }});
@@ -1493,18 +1521,24 @@ int imix_main(uint64_t n, int rounds)
         }
         rx = keep;
     }
-    // every compute variant alone on freshly zeroed check fields: verify accepts all
+    // every compute variant alone on freshly zeroed check fields: verify accepts
+    // all, and the filled buffer is byte-identical to launch_compute_desc's
+    std::vector<uint8_t> fref(total), fgot(total);
+    hipLaunchKernelGGL(k_hdr_desc, dim3((n + 255) / 256), dim3(256), 0, s, tx, doff, dlen, n);
+    CK(launch_compute_desc(tx, total, doff, dlen, (u32)n, nullptr, nullptr, 0u, s));
+    CK(hipMemcpy(fref.data(), tx, total, hipMemcpyDeviceToHost));
     for (auto& v : vs) {
         if (v.name.rfind("compute", 0) != 0 || v.name.find("no write") != std::string::npos)
             continue;
         hipLaunchKernelGGL(k_hdr_desc, dim3((n + 255) / 256), dim3(256), 0, s, tx, doff, dlen, n);
         v.run(s);
+        CK(hipMemcpy(fgot.data(), tx, total, hipMemcpyDeviceToHost));
         CK(launch_verify_desc(tx, total, doff, dlen, (u32)n, v1, 0u, s));
         CK(hipMemcpy(h.data(), v1, n, hipMemcpyDeviceToHost));
         bad = 0;
         for (auto b : h) bad += b != 0;
-        std::printf("check %-40s non-accept after a fill from zero: %zu (expect 0)\n",
-                    v.name.c_str(), bad);
+        std::printf("check %-40s non-accept after a fill from zero: %zu (expect 0), bytes %s\n",
+                    v.name.c_str(), bad, fgot == fref ? "equal" : "DIFFER");
     }
     return 0;
 }
