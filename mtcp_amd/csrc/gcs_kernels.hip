@@ -496,7 +496,7 @@ using DescShip = DescShape<4, 1, 16, 3, 32, 3, COMPUTE ? WM_SECTOR_NT : kWM, kBl
                            COMPUTE, !COMPUTE>;
 
 template <int G, int U, bool COMPUTE, bool LOOP, bool EXT, int WM, int K = 1, bool NT = kNT,
-          int PROBE = 0>
+          int PROBE = 0, int NTH = kBlock>
 __device__ __forceinline__ void desc_class(uint8_t* __restrict__ frames, uint64_t frames_bytes,
                                            const uint64_t* soff, const uint16_t* slen,
                                            const uint16_t* list, int count, u32 flags,
@@ -504,7 +504,7 @@ __device__ __forceinline__ void desc_class(uint8_t* __restrict__ frames, uint64_
                                            uint32_t* hashes, uint16_t* queues, uint4* stage)
 {
     static_assert(K == 1 || !LOOP, "K > 1 is for frames that fit one batch");
-    constexpr int GPB = kBlock / G;                    // groups per block
+    constexpr int GPB = NTH / G;                       // groups per block (NTH threads)
     const int g = threadIdx.x / G, sub = threadIdx.x & (G - 1);
     auto xframe_of = [&](int t) {
         return EXT ? XFrame{{ext.key[0], ext.key[1], ext.key[2], ext.key[3]},
@@ -553,7 +553,7 @@ __device__ __forceinline__ void desc_class(uint8_t* __restrict__ frames, uint64_
 
 // End of a descriptor block: the staged sector-0 write-backs, then the block's
 // per-frame outputs from LDS as coalesced stores.
-template <class S, bool COMPUTE, bool EXT>
+template <class S, bool COMPUTE, bool EXT, int NTH = kBlock>
 __device__ __forceinline__ void desc_tail(uint8_t* __restrict__ frames, uint64_t frames_bytes,
                                           uint64_t f0, u32 n, const uint64_t* soff,
                                           const uint16_t* slen, const uint8_t* codes,
@@ -563,7 +563,7 @@ __device__ __forceinline__ void desc_tail(uint8_t* __restrict__ frames, uint64_t
                                           uint32_t* __restrict__ out_csum, u32 flags,
                                           const Ext& ext)
 {
-    constexpr int F = S::F, NR = 4 * S::R;            // stage rounds: 4 chunks per frame
+    constexpr int F = S::F, NR = 4 * ((F + NTH - 1) / NTH);            // stage rounds: 4 chunks per frame
     const int t = threadIdx.x;
     if (COMPUTE && S::STAGE && !(flags & GCS_CF_NO_INPLACE)) {
         // STAGE: the frames' sector-0 write-backs leave together, in frame
@@ -575,7 +575,7 @@ __device__ __forceinline__ void desc_tail(uint8_t* __restrict__ frames, uint64_t
         uint64_t ob[NR];
 #pragma unroll
         for (int r = 0; r < NR; r++) {
-            const int q = r * kBlock + t, ft = q >> 2, c = q & 3;
+            const int q = r * NTH + t, ft = q >> 2, c = q & 3;
             go[r] = false;
             ob[r] = 0;
             if (ft >= F || f0 + ft >= n)
@@ -600,11 +600,11 @@ __device__ __forceinline__ void desc_tail(uint8_t* __restrict__ frames, uint64_t
 #pragma unroll
         for (int r = 0; r < NR; r++)
             if (go[r])
-                stg16<S::WM>(frames + ob[r], stage[r * kBlock + t]);
+                stg16<S::WM>(frames + ob[r], stage[r * NTH + t]);
     }
 #pragma unroll
-    for (int r = 0; r < S::R; r++) {
-        const int ft = r * kBlock + t;
+    for (int r = 0; r < (F + NTH - 1) / NTH; r++) {
+        const int ft = r * NTH + t;
         const uint64_t i = f0 + ft;
         if (ft < F && i < n) {
             if (out_code)

@@ -1198,6 +1198,256 @@ k_desc_ring_x(uint8_t* __restrict__ frames, uint64_t frames_bytes,
     desc_ring<S, R, COMPUTE, XCD, true>(frames, frames_bytes, off, lens, n, out_code, out_csum,
                                         flags, ext);
 }
+// ---------------------------------------------------------------------------
+// round 3: k_desc_stream with one wave per block (64 frames), measured against the
+// shipped 256-thread stream on the same boxes: verify 244-249 vs 248-256 us (box
+// noise decides), fill 373 vs 359-361 us; U8 spills at 6 waves (423 us).  Not shipped.
+// k_desc_stream with ONE wave per block and 64 frames per block: no
+// cross-wave dependencies, so no block barriers between the phases (a
+// one-wave s_barrier costs nothing), and ~7 KB of LDS per block instead of
+// 27 KB, so a CU holds as many blocks as it has wave slots.  Phase 2 batches
+// its LDS reads per trip (all rows' bitmap words, then all rows' frame
+// metadata) instead of two dependent round trips per row, and clamps the
+// addresses of loads past the region instead of branching around them.
+template <int U_, int RMAX_, int OCC_>
+struct WStreamShape {
+    static constexpr int U = U_;          // chunks per lane per trip
+    static constexpr int RMAX = RMAX_;    // region chunks a streaming block may span
+    static constexpr int OCC = OCC_;      // waves per SIMD
+    static_assert(RMAX % 64 == 0 && RMAX <= 65536, "start chunks fit 16 bits");
+};
+
+template <class S, class T, bool COMPUTE, bool XCD>
+__device__ __forceinline__ void desc_wstream(uint8_t* __restrict__ frames, uint64_t frames_bytes,
+                                             const uint64_t* __restrict__ off,
+                                             const uint16_t* __restrict__ lens, u32 n,
+                                             uint8_t* __restrict__ out_code,
+                                             uint32_t* __restrict__ out_csum, u32 flags)
+{
+    constexpr int F = 64, RW = T::RMAX / 64, U = T::U;
+    static_assert(S::F == F, "one frame per lane of one wave");
+    static_assert(!COMPUTE || S::STAGE, "TX stages sector 0 in hdr");
+    __shared__ uint64_t soff[F];
+    __shared__ uint16_t slen[F];
+    __shared__ uint16_t list[3][F];
+    __shared__ uint8_t codes[F];
+    __shared__ uint32_t csums[COMPUTE ? F : 1];
+    __shared__ uint4 hdr[4 * F];       // chunks 0..3 per frame; TX: the staged sector 0
+    __shared__ uint64_t bm[RW];        // bit c: a frame starts at region chunk c
+    __shared__ uint16_t rbase[RW];     // frames starting before chunk 64 * r
+    __shared__ u32 meta[F];            // start chunk << 16 | len
+    __shared__ u32 pfirst[F];          // prefix at the frame's first chunk
+    __shared__ u32 qend[F];            // Q(len)
+
+    const uint32_t blk = XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint64_t f0 = (uint64_t)blk * F;
+    const int t = threadIdx.x;
+    const int nf = (int)((n - f0) < (uint64_t)F ? (n - f0) : (uint64_t)F);
+    const uint64_t below = (1ull << t) - 1;
+
+    // phase 0: validate, classify, test streamability
+    int cls = -1;
+    uint64_t o = 0;
+    u32 len = 0;
+    if (t < nf) {
+        o = off[f0 + t];
+        len = lens[f0 + t];
+        const bool ok = (o & 15) == 0 && o <= frames_bytes && len <= frames_bytes - o;
+        if (!ok) {
+            codes[t] = COMPUTE ? GCS_TX_BAD_DESC : GCS_V_BAD_DESC;
+            if (COMPUTE)
+                csums[t] = 0;
+        } else {
+            soff[t] = o;
+            slen[t] = (uint16_t)len;
+            cls = len <= (u32)S::T0 ? 0 : (len <= (u32)S::T1 ? 1 : 2);
+        }
+    }
+    const u32 nch = (len + 15) >> 4;
+    const uint64_t r0 = off[f0];
+    u32 start = 0, snext = 0;
+    bool sok = t >= nf || (cls >= 0 && len > 0);
+    if (sok && t < nf) {
+        if (o < r0 || ((o - r0) >> 4) + nch > (uint64_t)T::RMAX) {
+            sok = false;
+        } else {
+            start = (u32)((o - r0) >> 4);
+            if (t + 1 < nf) {
+                const uint64_t on = off[f0 + t + 1], e = o + 16ull * nch;
+                sok = on >= e && on - e <= 64;
+                snext = (u32)((on - r0) >> 4);
+            } else {
+                sok = o + 16ull * nch <= frames_bytes;
+                snext = start + nch;
+            }
+        }
+    }
+    if (!__all(sok)) {
+        // the class passes (desc_mixed's, on one wave)
+        int nc[3];
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            const uint64_t m = __ballot(cls == c);
+            if (cls == c)
+                list[c][__popcll(m & below)] = (uint16_t)t;
+            nc[c] = __popcll(m);
+        }
+        __syncthreads();
+        uint4* stg = COMPUTE ? hdr : nullptr;
+        if (nc[0]) desc_class<S::G0, S::U0, COMPUTE, false, false, S::WM, S::K0, S::NT, 0, F>(frames, frames_bytes, soff, slen, list[0], nc[0], flags, codes, csums, Ext{}, nullptr, nullptr, stg);
+        if (nc[1]) desc_class<S::G1, S::U1, COMPUTE, false, false, S::WM, S::K1, S::NT, 0, F>(frames, frames_bytes, soff, slen, list[1], nc[1], flags, codes, csums, Ext{}, nullptr, nullptr, stg);
+        if (nc[2]) desc_class<S::G2, S::U2, COMPUTE, true, false, S::WM, 1, S::NT, 0, F>(frames, frames_bytes, soff, slen, list[2], nc[2], flags, codes, csums, Ext{}, nullptr, nullptr, stg);
+        __syncthreads();
+        desc_tail<S, COMPUTE, false, F>(frames, frames_bytes, f0, n, soff, slen, codes, csums,
+                                        nullptr, nullptr, hdr, out_code, out_csum, flags, Ext{});
+        return;
+    }
+
+    // phase 1: first-chunk bitmap, per-frame metadata, rows' frame counts
+    const u32 NCH = (u32)__shfl((int)snext, nf - 1, 64), NR = (NCH + 63) >> 6;
+    for (u32 r = t; r < NR; r += F)
+        bm[r] = 0;
+    __syncthreads();
+    if (t < nf) {
+        meta[t] = start << 16 | len;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if ((u32)k >= nch)
+                hdr[4 * t + k] = make_uint4(0, 0, 0, 0);
+        atomicOr((unsigned long long*)&bm[start >> 6], 1ull << (start & 63));
+        const u32 rhi = t + 1 < nf ? snext >> 6 : NR - 1;
+        for (u32 r = (start >> 6) + 1; r <= rhi; r++)
+            rbase[r] = (uint16_t)(t + 1);
+    }
+    if (t == 0)
+        rbase[0] = 0;
+    __syncthreads();
+
+    // phase 2: the region as one stream, 64 * U chunks per trip
+    {
+        const uint8_t* reg = frames + r0;
+        const u32 clast = NCH - 1;
+        u32 run = 0;
+        for (u32 base = 0; base < NCH; base += 64 * U) {
+            uint4 v[U];
+#pragma unroll
+            for (int j = 0; j < U; j++) {
+                const u32 c = base + 64 * j + t;
+                v[j] = ldg16<S::NT>(reg + 16ull * (c < clast ? c : clast));
+            }
+            u32 ex[U];
+#pragma unroll
+            for (int j = 0; j < U; j++) {
+                const u32 c = base + 64 * j + t;
+                const u32 sj = c < NCH ? hsum4(v[j]) : 0u;
+                const u32 incl = wave_incl_scan(sj);
+                ex[j] = run + incl - sj;
+                run += (u32)__builtin_amdgcn_readlane((int)incl, 63);
+            }
+            int fj[U];
+#pragma unroll
+            for (int j = 0; j < U; j++) {
+                u32 row = (base >> 6) + j;
+                row = row < NR ? row : NR - 1;
+                const uint64_t bits = bm[row];
+                const u32 bl = __builtin_amdgcn_mbcnt_hi((u32)(bits >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((u32)bits, 0u));
+                const int f = (int)rbase[row] + (int)bl + (int)((bits >> t) & 1u) - 1;
+                fj[j] = f < 0 ? 0 : (f < nf ? f : nf - 1);
+            }
+            u32 mj[U];
+#pragma unroll
+            for (int j = 0; j < U; j++)
+                mj[j] = meta[fj[j]];
+#pragma unroll
+            for (int j = 0; j < U; j++) {
+                const u32 c = base + 64 * j + t;
+                const int f = fj[j];
+                const u32 fl = mj[j] & 0xFFFFu;
+                const u32 k = c - (mj[j] >> 16), fn = (fl + 15) >> 4;
+                if (c < NCH) {
+                    if (k < 4 && k < fn)
+                        hdr[4 * f + k] = v[j];
+                    if (k == 0)
+                        pfirst[f] = ex[j];
+                    if (k + 1 == fn)
+                        qend[f] = ex[j] + chunk_prefix_sum(v[j], (int)(fl - 16 * k));
+                }
+            }
+        }
+    }
+    __syncthreads();
+
+    // phase 3: one lane per frame
+    const int tf = t < nf ? t : 0;
+    const uint4 h4[4] = {hdr[4 * tf], hdr[4 * tf + 1], hdr[4 * tf + 2], hdr[4 * tf + 3]};
+    Hdr h;
+    h.d3 = h4[0].w;
+    h.d4 = h4[1].x;
+    h.d5 = h4[1].y;
+    const int ihl = (int)((h.d3 >> 16) & 15u);
+    const int ts = 14 + 4 * ihl;
+    const int te = 14 + (int)bswap16(h.d4 & 0xFFFFu);
+    const bool fast = t < nf && ihl <= 8 && (te <= 64 || te == (int)len);
+    const bool all5 = __all(!fast || ihl == 5);
+    const bool end64 = __all(!fast || te >= 64);
+    const uint64_t sm = __ballot(t < nf && !fast);
+    const int ns = __popcll(sm);
+    uint8_t* oc = (!COMPUTE && out_code) ? out_code + f0 + t : codes + t;
+    if (t < nf && !fast) {
+        list[2][__popcll(sm & below)] = (uint16_t)t;
+    } else if (fast) {
+        Acc a = {0u, 0u, 0u};
+        if (all5 && end64) {
+#pragma unroll
+            for (int c = 0; c < 4; c++)
+                accum_fast5<COMPUTE, true>(h4[c], c, 64, masks5<COMPUTE>(c), a);
+        } else if (all5) {
+#pragma unroll
+            for (int c = 0; c < 4; c++)
+                accum_fast5<COMPUTE, true>(h4[c], c, te, masks5<COMPUTE>(c), a);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                accum_chunk<COMPUTE>(h4[j], 16 * j, ts, te, a);
+        }
+        if (te > 64)
+            a.tcp += (qend[t] - pfirst[t]) -
+                     (hsum4(h4[0]) + hsum4(h4[1]) + hsum4(h4[2]) + hsum4(h4[3]));
+        epilogue<1, 4, COMPUTE, S::WM, false>(
+            h, a, frames + o, len, (int64_t)(frames_bytes - o), true, 0, flags, oc,
+            COMPUTE ? csums + t : nullptr, true, h4, XFrame{},
+            COMPUTE ? reinterpret_cast<uint8_t*>(hdr + 4 * t) : nullptr);
+    }
+    if (ns) {
+        __syncthreads();
+        desc_class<S::G2, S::U2, COMPUTE, true, false, S::WM, 1, S::NT, 0, F>(
+            frames, frames_bytes, soff, slen, list[2], ns, flags, codes, csums, Ext{}, nullptr,
+            nullptr, COMPUTE ? hdr : nullptr);
+    }
+    if constexpr (COMPUTE) {
+        __syncthreads();
+        desc_tail<S, COMPUTE, false, F>(frames, frames_bytes, f0, n, soff, slen, codes, csums,
+                                        nullptr, nullptr, hdr, out_code, out_csum, flags, Ext{});
+    } else if (ns && out_code) {
+        __syncthreads();
+        if (t < ns) {
+            const int ft = list[2][t];
+            out_code[f0 + ft] = codes[ft];
+        }
+    }
+}
+
+template <class S, class T, bool COMPUTE, bool XCD>
+__global__ void __launch_bounds__(64, T::OCC)
+k_desc_wstream(uint8_t* __restrict__ frames, uint64_t frames_bytes,
+               const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens, u32 n,
+               uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags)
+{
+    desc_wstream<S, T, COMPUTE, XCD>(frames, frames_bytes, off, lens, n, out_code, out_csum,
+                                     flags);
+}
+
 // C3: IMIX 64/576/1500 at 7:4:1, pslib 64 B packing, descriptor kernels.
 int imix_main(uint64_t n, int rounds)
 {
@@ -1445,13 +1695,37 @@ int imix_main(uint64_t n, int rounds)
     // 0-2 alone 251 (list kernel 278-286); fill nt FRESH 325-366 (temporal 374; list
     // kernel 385-431 on the same boxes)
     // second version (fast5 phase 3, one barrier less), occ 6: verify 253 / 255 (U8 / U4),
-    // U4 phases 0-2 alone 238, read ceiling 230; fill FRESH 359-361 (list kernel 428)
-    STREAMV(false, "U8 occ6 R12K nt", 8, 12288, 6, true, false, 0)
-    STREAMV(false, "U8 occ6 R12K nt PROBE no phase 3", 8, 12288, 6, true, false, 2)
-    STREAMV(false, "U4 occ6 R12K nt", 4, 12288, 6, true, false, 0)
-    STREAMV(false, "U4 occ6 R12K nt PROBE no phase 3", 4, 12288, 6, true, false, 2)
-    STREAMV(true, "U8 occ6 R12K nt FRESH", 8, 12288, 6, true, false, 0)
-    STREAMV(true, "U4 occ6 R12K nt FRESH", 4, 12288, 6, true, false, 0)
+    // U4 phases 0-2 alone 238, read ceiling 230; fill FRESH 359-361 (list kernel 428);
+    // third (direct RX verdicts, constant te): 258 / 259, phases 0-2 247 (ceiling 239)
+    STREAMV(false, "U8 occ6 R12K nt (shipped)", 8, 12288, 6, true, false, 0)
+    STREAMV(true, "U8 occ6 R12K nt FRESH (shipped)", 8, 12288, 6, true, false, 0)
+    // one wave per block, 64 frames (k_desc_wstream)
+#define WSTREAMV(C_, TAG, U_, RMAX_, OCC_)                                                  \
+    vs.push_back({std::string(C_ ? "compute" : "verify ") + " wstream " + TAG,              \
+                  C_ ? cb : vb, [&](hipStream_t st) {                                      \
+        using S_ = DescShape<4, 1, 16, 3, 32, 3, C_ ? WM_SECTOR_NT : kWM, 64, true, 1, 1,   \
+                             C_, true>;                                                    \
+        using T_ = WStreamShape<U_, RMAX_, OCC_>;                                          \
+        hipLaunchKernelGGL((k_desc_wstream<S_, T_, C_, true>), dim3((n + 63) / 64),        \
+                           dim3(64), 0, st, C_ ? tx : rx, total, doff, dlen, (u32)n,        \
+                           C_ ? nullptr : v1, nullptr, 0u);                                 \
+    }});                                                                                    \
+    if (C_)                                                                                 \
+        vs.back().prep = [&](hipStream_t st) {                                              \
+            hipLaunchKernelGGL(k_zero_checks_desc, dim3((n + 255) / 256), dim3(256), 0, st, \
+                               tx, doff, dlen, n);                                          \
+        };
+    // measured: U8 occ6 (23 VGPRs spilled) 423, U4 occ6 (10 spilled) 249, U4 "occ8"
+    // (the compiler's 96 VGPRs, 5 waves) 244 vs the 256-thread stream 256 on one box
+    // (read ceiling 219); fill U4 occ6 374 vs 361.  Second box: U4 occ4 / occ5 / U2 /
+    // U8 occ4 249 / 256 / 272 / 258 vs the shipped stream 248; fills 373-374 vs 359
+    WSTREAMV(false, "U4 occ5 R6K", 4, 6144, 5)
+    WSTREAMV(false, "U2 occ5 R6K", 2, 6144, 5)
+    WSTREAMV(false, "U8 occ4 R6K", 8, 6144, 4)
+    WSTREAMV(false, "U4 occ4 R6K", 4, 6144, 4)
+    WSTREAMV(true, "U4 occ5 R6K FRESH", 4, 6144, 5)
+    WSTREAMV(true, "U2 occ5 R6K FRESH", 2, 6144, 5)
+    WSTREAMV(true, "U4 occ4 R6K FRESH", 4, 6144, 4)
     vs.push_back({"verify  desc (launch_verify_desc)", vb, [&](hipStream_t st) {
         CK(launch_verify_desc(rx, total, doff, dlen, (u32)n, v1, 0u, st));
     }});
