@@ -1422,7 +1422,11 @@ __device__ bool gro_cont(const uint8_t* p, const uint8_t* c, int pp, int pc)
 // W = the largest window the instantiation takes (LDS is sized by it): W = 64
 // needs ~9 KiB of LDS per block instead of ~36 KiB, so a CU holds twice the
 // blocks (8 instead of 4) and twice the run-building waves.
-template <int U, int W = kGroW, int OCC = 1>
+// FLAT (W <= 64): phase D as one stream over the window's output instead of
+// one wave per run -- see the comment at phase D2.
+enum { SEG_HDR = 0, SEG_PAY = 1, SEG_WHOLE = 2 };
+
+template <int U, int W = kGroW, int OCC = 1, bool FLAT = false>
 __global__ void __launch_bounds__(kBlock, OCC)
 k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restrict__ off,
       const uint16_t* __restrict__ lens, const uint8_t* __restrict__ verdict, u32 n, u32 window,
@@ -1447,6 +1451,16 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
     __shared__ uint32_t rl_at[W];
     __shared__ uint16_t ridx[W];
     __shared__ uint32_t wsum[kBlock / 64][2];
+    __shared__ uint32_t nout_s;     // the window's output bytes (runs at 16 B-aligned offsets)
+    constexpr int NS = FLAT ? 2 * W : 1, NRF = FLAT ? W : 1;
+    __shared__ uint32_t sg_st[NS];  // FLAT: segments of the output, in output order
+    __shared__ uint32_t sg_len[NS];
+    __shared__ uint64_t sg_src[NS]; // input offset (SEG_HDR: the head's window index)
+    __shared__ uint8_t sg_kind[NS];
+    __shared__ uint8_t sg_run[NS];
+    __shared__ int nseg_s;
+    __shared__ uint4 rstash[NRF][4];   // FLAT: chunks 0..3 of each merged run
+    __shared__ uint32_t rpf[NRF], rqe[NRF], wtot[kBlock / 64];
 
     const int t = threadIdx.x;
     const uint64_t w0 = (uint64_t)blockIdx.x * window;
@@ -1542,8 +1556,10 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
         }
         xs = bs + is - xs;                             // exclusive
         xl = bl + il - xl;
-        if (t == kBlock - 1)
+        if (t == kBlock - 1) {
             nruns = (int)(bs + is);
+            nout_s = bl + il;
+        }
     }
     const uint64_t o0 = cnt ? soff[0] : 0;
     if (rs) {
@@ -1560,6 +1576,246 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
         head[w0 + t] = (uint32_t)(w0 + hk);
         out_off[w0 + t] = run_off[r];
         out_len[w0 + t] = hk == t ? (uint16_t)run_len[r] : (uint16_t)0;
+    }
+
+    if constexpr (FLAT) {
+        static_assert(W <= 64, "the window's frames sit in wave 0");
+        // D1: the output as segments: a merged run's head headers (from LDS),
+        // each member's payload, or a single frame as it is
+        if (t < 64) {
+            int ns = 0, k0 = SEG_HDR;
+            u32 st0 = 0, ln0 = 0, ln1 = 0;
+            uint64_t sr0 = 0, sr1 = 0;
+            int rr = 0;
+            if (t < cnt) {
+                const int hk = rhead[t];
+                rr = ridx[hk];
+                const int nm = run_n[rr];
+                const u32 rel = (u32)(run_off[rr] - o0);
+                if (nm == 1) {
+                    if (run_len[rr] > 0) {
+                        ns = 1;
+                        k0 = SEG_WHOLE;
+                        st0 = rel;
+                        ln0 = run_len[rr];
+                        sr0 = soff[t];
+                    }
+                } else {
+                    const u32 hl = 34 + 4 * (hdr[hk][46] >> 4);
+                    if (t == hk) {
+                        ns = 2;
+                        k0 = SEG_HDR;
+                        st0 = rel;
+                        ln0 = hl;
+                        sr0 = (uint64_t)hk;
+                        ln1 = (u32)pay[t];
+                        sr1 = soff[t] + hl;
+                    } else {
+                        ns = 1;
+                        k0 = SEG_PAY;
+                        st0 = rel + hl + pref[t];
+                        ln0 = (u32)pay[t];
+                        sr0 = soff[t] + hl;
+                    }
+                }
+            }
+            const u32 incl = wave_incl_scan((u32)ns);
+            const int e = (int)(incl - (u32)ns);
+            if (ns >= 1) {
+                sg_st[e] = st0;
+                sg_len[e] = ln0;
+                sg_src[e] = sr0;
+                sg_kind[e] = (uint8_t)k0;
+                sg_run[e] = (uint8_t)rr;
+            }
+            if (ns == 2) {
+                sg_st[e + 1] = st0 + ln0;
+                sg_len[e + 1] = ln1;
+                sg_src[e + 1] = sr1;
+                sg_kind[e + 1] = SEG_PAY;
+                sg_run[e + 1] = (uint8_t)rr;
+            }
+            if (t == 63)
+                nseg_s = (int)incl;
+        }
+        __syncthreads();
+        // D2: the window's output chunks as one stream, wave w a quarter of
+        // them, 64 * U per trip.  A chunk finds its segment by binary search
+        // (7 steps over <= 128 starts in LDS) and is one unaligned load, or
+        // two at a segment boundary, or (tiny payloads, the input's end) a
+        // byte loop.  Each lane folds its chunk to one word sum and a DPP
+        // wave scan makes prefixes; a merged run's checks are then
+        // Q(end) - Q(start) plus its header chunks (D3), as in
+        // k_desc_stream.  Chunks 0..3 of merged runs wait in LDS for D3.
+        const int nseg = nseg_s, wave = t >> 6, lane = t & 63;
+        const u32 NOUT = nout_s >> 4;
+        const u32 QW = ((NOUT + 4 * 64 - 1) / (4 * 64)) * 64;
+        const u32 lo = wave * QW, hi = lo + QW < NOUT ? lo + QW : NOUT;
+        uint8_t* ob = out + o0;
+        const int64_t wl_all = o0 <= out_bytes ? (int64_t)(out_bytes - o0) : 0;
+        const uint8_t* in_end = in + in_bytes;
+        u32 run = 0;
+        for (u32 base = lo; base < hi; base += 64 * U) {
+            uint4 x[U], y[U];
+            int sj[U], pl[U];
+#pragma unroll
+            for (int j = 0; j < U; j++) {
+                const u32 c = base + 64 * j + lane, p = 16 * c;
+                int sgi = 0;
+#pragma unroll
+                for (int step = 64; step > 0; step >>= 1)
+                    if (sgi + step < nseg && sg_st[sgi + step] <= p)
+                        sgi += step;
+                sj[j] = sgi;
+                x[j] = z;
+                y[j] = z;
+                int plan = AS_ZERO;
+                if (c < hi) {
+                    const u32 ss = sg_st[sgi], sl = sg_len[sgi], kd = sg_kind[sgi];
+                    const int r = sg_run[sgi];
+                    const u32 rend = (u32)(run_off[r] - o0) + run_len[r];
+                    const u32 offs = p - ss, rem = sl - offs;
+                    const u32 need = rend - p < 16u ? rend - p : 16u;
+                    const uint8_t* pa = in + sg_src[sgi] + offs;
+                    if (kd == SEG_HDR && offs + 16 <= (u32)kGroHdr) {
+                        x[j] = *reinterpret_cast<const uint4*>(&hdr[sg_src[sgi]][offs]);
+                        plan = AS_ONE;
+                    } else if (kd != SEG_HDR && pa + 16 <= in_end) {
+                        x[j] = ldg16u(pa);
+                        plan = AS_ONE;
+                    } else {
+                        plan = AS_BYTES;
+                    }
+                    if (plan == AS_ONE && rem < need) {
+                        const int s2 = sgi + 1;
+                        const uint8_t* pb = in + sg_src[s2];
+                        if (s2 < nseg && sg_run[s2] == r && sg_st[s2] == ss + sl &&
+                            sg_kind[s2] == SEG_PAY && sg_len[s2] >= need - rem && pb + 16 <= in_end) {
+                            y[j] = ldg16u(pb);
+                            plan = AS_TWO;
+                        } else {
+                            plan = AS_BYTES;
+                        }
+                    }
+                }
+                pl[j] = plan;
+            }
+#pragma unroll
+            for (int j = 0; j < U; j++) {
+                const u32 c = base + 64 * j + lane, p = 16 * c;
+                const int sgi = sj[j], r = sg_run[sgi];
+                const u32 ss = sg_st[sgi], sl = sg_len[sgi];
+                const u32 rrel = (u32)(run_off[r] - o0), rend = rrel + run_len[r];
+                const bool merged = sg_kind[sgi] != SEG_WHOLE;
+                if (pl[j] == AS_TWO) {
+                    x[j] = blend(x[j], bytes_up(y[j], (int)(ss + sl - p)),
+                                 byte_mask((int)(ss + sl - p), 16));
+                } else if (pl[j] == AS_BYTES) {
+                    u32 wv[4] = {0u, 0u, 0u, 0u};
+                    int s2 = sgi;
+                    for (int k = 0; k < 16; k++) {
+                        const u32 q = p + k;
+                        if (q >= rend)
+                            break;
+                        while (s2 + 1 < nseg && q >= sg_st[s2] + sg_len[s2])
+                            s2++;
+                        if (q < sg_st[s2] || q >= sg_st[s2] + sg_len[s2])
+                            continue;
+                        const u32 b = sg_kind[s2] == SEG_HDR
+                                          ? (u32)hdr[sg_src[s2]][q - sg_st[s2]]
+                                          : (in + sg_src[s2] + (q - sg_st[s2]) < in_end
+                                                 ? (u32)in[sg_src[s2] + (q - sg_st[s2])] : 0u);
+                        wv[k >> 2] |= b << (8 * (k & 3));
+                    }
+                    x[j] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+                }
+                if (merged && pl[j] != AS_ZERO && rend - p < 16u)       // nothing past the run
+                    x[j] = blend(z, x[j], byte_mask(0, (int)(rend - p)));
+                const u32 sum = pl[j] != AS_ZERO ? hsum4(x[j]) : 0u;
+                const u32 incl = wave_incl_scan(sum);
+                const u32 excl = run + incl - sum;
+                run += (u32)__builtin_amdgcn_readlane((int)incl, 63);
+                if (pl[j] == AS_ZERO)
+                    continue;
+                const u32 kr = (p - rrel) >> 4;
+                if (merged) {
+                    if (kr == 0)
+                        rpf[r] = excl;
+                    if (p + 16 >= rend)
+                        rqe[r] = excl + sum;                   // Q at the run's end
+                    if (kr < 4) {
+                        rstash[r][kr] = x[j];
+                        continue;
+                    }
+                }
+                if ((int64_t)p + 16 <= wl_all) {
+                    stg16<WM_SECTOR>(ob + p, x[j]);
+                } else {
+                    for (int k = 0; k < 16 && (int64_t)(p + k) < wl_all && (!merged || p + k < rend); k++)
+                        ob[p + k] = (uint8_t)chunk_byte(x[j], k);
+                }
+            }
+        }
+        if (lane == 0)
+            wtot[wave] = run;
+        __syncthreads();
+        // D3: one thread per merged run: tot_len and PSH into the head's
+        // headers, the checks from chunks 0..3 and the prefix difference, then
+        // chunks 0..3 out
+        if (t < nruns && run_n[t] > 1) {
+            const int r = t, k0 = run_t[r], nm = run_n[r];
+            const u32 mlen = run_len[r], rrel = (u32)(run_off[r] - o0);
+            uint4 sc[4] = {rstash[r][0], rstash[r][1], rstash[r][2], rstash[r][3]};
+            const u32 raw = hsum4(sc[0]) + hsum4(sc[1]) + hsum4(sc[2]) + hsum4(sc[3]);
+            uint8_t psh = 0;
+            for (int k = k0; k < k0 + nm; k++)
+                psh |= hdr[k][47] & 0x08;
+            sc[1].x = (sc[1].x & 0xFFFF0000u) | bswap16((mlen - 14) & 0xFFFFu);
+            sc[2].w |= (u32)psh << 24;
+            Hdr h;
+            h.d3 = sc[0].w;
+            h.d4 = sc[1].x;
+            h.d5 = sc[1].y;
+            const int te = (int)mlen;
+            Acc a = {0u, 0u, 0u};
+#pragma unroll
+            for (int c = 0; c < 4; c++)
+                accum_fast5<true, true>(sc[c], c, te, masks5<true>(c), a);
+            if (te > 64) {
+                auto wbase = [&](u32 ch) {
+                    const u32 q = ch / QW;
+                    u32 b = 0;
+#pragma unroll
+                    for (int k = 0; k < kBlock / 64 - 1; k++)
+                        b += (u32)k < q ? wtot[k] : 0u;
+                    return b;
+                };
+                const u32 p0 = rpf[r] + wbase(rrel >> 4);
+                const u32 p1 = rqe[r] + wbase((rrel + mlen - 1) >> 4);
+                a.tcp += (p1 - p0) - raw;
+            }
+            uint8_t st = 0;
+            uint32_t cs = 0;
+            epilogue<1, 4, true, WM_SECTOR, false>(h, a, ob + rrel, mlen, 0, true, 0,
+                                                   GCS_CF_NO_INPLACE, &st, &cs, true, sc);
+            if (st == GCS_TX_OK || st == GCS_TX_IP_ONLY || st == GCS_TX_BAD_TCPLEN)
+                sc[1].z = (sc[1].z & 0xFFFF0000u) | (cs & 0xFFFFu);          // bytes 24-25
+            if (st == GCS_TX_OK)
+                sc[3].x = (sc[3].x & 0x0000FFFFu) | (cs & 0xFFFF0000u);      // bytes 50-51
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const u32 p = rrel + 16 * c;
+                if (16 * c >= (int)mlen)
+                    break;
+                if ((int64_t)p + 16 <= wl_all) {
+                    stg16<WM_SECTOR>(ob + p, sc[c]);
+                } else {
+                    for (int k = 0; k < 16 && (int64_t)(p + k) < wl_all && 16 * c + k < (int)mlen; k++)
+                        ob[p + k] = (uint8_t)chunk_byte(sc[c], k);
+                }
+            }
+        }
+        return;
     }
 
     // D: build the runs, one wave per run
@@ -2054,13 +2310,15 @@ hipError_t launch_gro(const uint8_t* in, uint64_t in_bytes, const uint64_t* off,
                       u32 max_len, uint8_t* out, uint64_t out_bytes, uint64_t* out_off,
                       uint16_t* out_len, uint32_t* head, hipStream_t s)
 {
-    // windows of <= 64 frames on the small-LDS instantiation, 6 waves per SIMD
-    // (<= 80 VGPRs): 1M x 1500 B in runs of 8, 928 us (LDS-bound, 4 blocks per
-    // CU) -> 809 (89 VGPRs, 5 per SIMD) -> 772 us (tools/kbench lro)
+    // windows of <= 64 frames on the small-LDS instantiation: 1M x 1500 B in
+    // runs of 8, 928 us (LDS-bound, 4 blocks per CU) -> 809 (89 VGPRs, 5 per
+    // SIMD) -> 772 us (<= 80 VGPRs, 6 per SIMD) -> 687 us with phase D as one
+    // stream over the window's output (FLAT; 53 VGPRs, 8 waves per SIMD; the
+    // run-per-wave form 761 us on the same box; tools/kbench lro)
     if (window <= 64)
-        hipLaunchKernelGGL((k_gro<2, 64, 6>), dim3((n + window - 1) / window), dim3(kBlock), 0, s, in,
-                           in_bytes, off, len, verdict, n, window, max_len, out, out_bytes,
-                           out_off, out_len, head);
+        hipLaunchKernelGGL((k_gro<2, 64, 8, true>), dim3((n + window - 1) / window), dim3(kBlock),
+                           0, s, in, in_bytes, off, len, verdict, n, window, max_len, out,
+                           out_bytes, out_off, out_len, head);
     else
         hipLaunchKernelGGL((k_gro<2, kGroW>), dim3((n + window - 1) / window), dim3(kBlock), 0, s,
                            in, in_bytes, off, len, verdict, n, window, max_len, out, out_bytes,

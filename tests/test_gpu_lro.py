@@ -118,12 +118,13 @@ def test_gro_mixed_traffic_and_bad_descriptors(torch_dev, ctx, O):
         buf[int(off[k]) + 23] = 1                             # ICMP: not ACCEPT
     off = off.copy()
     off[5] += 8                                               # misaligned descriptor
-    vd = verdicts(t, ctx, buf, off, lens)
+    off[128] += 8                                             # ... first of its window: the
+    vd = verdicts(t, ctx, buf, off, lens)                     # window's output base moves too
     for out_bytes in (None, buf.nbytes // 2 + 3):
         gpu = run_gro(t, ctx, buf, off, lens, vd, 64, 16384, out_bytes=out_bytes)
         ref = O.gro_batch(buf, off, lens, vd, 64, 16384, out_bytes=out_bytes)
         compare(buf, off, lens, gpu, ref)
-        assert gpu[2][5] == 0
+        assert gpu[2][5] == 0 and gpu[2][128] == 0
 
 
 def test_gro_rejects_bad_arguments(torch_dev, ctx):

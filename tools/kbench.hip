@@ -2360,7 +2360,7 @@ int lro_main(uint64_t n, int rounds)
         hipLaunchKernelGGL((k_gro<U_, W_, O_>), dim3((n + 63) / 64), dim3(256), 0, st, in, n * stride, \
                            off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd);  \
     }});
-    GROO(2, 64, 6)
+    GROO(2, 64, 6)          // the run-per-wave form shipped until round 3c
     // round 3: more bytes in flight per wave (U) against waves per SIMD (OCC)
     if (getenv("KB_GRO_SHAPES")) {   // measured r03: none faster (kbench_lro_shapes.log)
     GROO(3, 64, 5) GROO(3, 64, 6) GROO(4, 64, 4) GROO(4, 64, 5) GROO(2, 64, 8) GROO(4, 64, 6)
@@ -2369,6 +2369,16 @@ int lro_main(uint64_t n, int rounds)
     // issued before batch b is assembled, folded and stored) measured 929-1766 us
     // against 766 us (spills: 32-176 B per lane; profiles/r03/kbench_lro_pipe.log);
     // removed from the kernel
+    // round 3c: phase D as one stream over the window's output (k_gro FLAT)
+#define GROF(U_, O_)                                                                         \
+    vs.push_back({"k_gro<" #U_ ",64," #O_ ",FLAT> (window 64, max 16384)", bytes, [&](hipStream_t st) { \
+        hipLaunchKernelGGL((k_gro<U_, 64, O_, true>), dim3((n + 63) / 64), dim3(256), 0, st, in, \
+                           n * stride, off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd); \
+    }});
+    // measured r03: <2,6> 715, <4,6> 711, <4,5> 713, <8,4> (41 VGPRs spilled) 970 vs shipped 761
+    // <4,6> 712, <2,8> 687 (shipped), <2,7> 692, <3,7> 686, <3,6> 708 (run-per-wave 761,
+    // D2D 637); <1,10> / <2,10> (the compiler gives 7 waves) 722 / 714, <1,8> 693
+    GROF(2, 8) GROF(3, 7)
     vs.push_back({"verify (launch_verify_desc) for scale", (double)n * (L + 1), [&](hipStream_t st) {
         CK(launch_verify_desc(in, n * stride, off, lens, (u32)n, vd, 0u, st));
     }});
