@@ -1426,7 +1426,7 @@ __device__ bool gro_cont(const uint8_t* p, const uint8_t* c, int pp, int pc)
 // one wave per run -- see the comment at phase D2.
 enum { SEG_HDR = 0, SEG_PAY = 1, SEG_WHOLE = 2 };
 
-template <int U, int W = kGroW, int OCC = 1, bool FLAT = false>
+template <int U, int W = kGroW, int OCC = 1, bool FLAT = false, int PROBE = 0>
 __global__ void __launch_bounds__(kBlock, OCC)
 k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restrict__ off,
       const uint16_t* __restrict__ lens, const uint8_t* __restrict__ verdict, u32 n, u32 window,
@@ -1459,6 +1459,8 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
     __shared__ uint8_t sg_kind[NS];
     __shared__ uint8_t sg_run[NS];
     __shared__ int nseg_s;
+    constexpr int NROW = FLAT ? 1024 : 1;   // 64-chunk output rows with a start entry (1 MiB)
+    __shared__ uint8_t sg_row[NROW];   // FLAT: the segment holding each row's first byte
     __shared__ uint4 rstash[NRF][4];   // FLAT: chunks 0..3 of each merged run
     __shared__ uint32_t rpf[NRF], rqe[NRF], wtot[kBlock / 64];
 
@@ -1639,6 +1641,24 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
                 nseg_s = (int)incl;
         }
         __syncthreads();
+        {
+            // per 64-chunk row of the output, the segment holding its first byte
+            // (one binary search per row here instead of one per chunk in D2)
+            const int nsg = nseg_s;
+            const u32 nrow = ((nout_s >> 4) + 63) >> 6;
+            for (u32 rw = t; rw < nrow && rw < (u32)NROW; rw += kBlock) {
+                const u32 p = rw << 10;
+                int sgi = 0;
+#pragma unroll
+                for (int step = 64; step > 0; step >>= 1)
+                    if (sgi + step < nsg && sg_st[sgi + step] <= p)
+                        sgi += step;
+                sg_row[rw] = (uint8_t)sgi;
+            }
+        }
+        __syncthreads();
+        if constexpr (PROBE == 1)           // A/B (kbench): phases A-C and D1 only
+            return;
         // D2: the window's output chunks as one stream, wave w a quarter of
         // them, 64 * U per trip.  A chunk finds its segment by binary search
         // (7 steps over <= 128 starts in LDS) and is one unaligned load, or
@@ -1661,11 +1681,22 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
 #pragma unroll
             for (int j = 0; j < U; j++) {
                 const u32 c = base + 64 * j + lane, p = 16 * c;
-                int sgi = 0;
+                // from the row's first segment: a row (1 KiB) spans few segments
+                const u32 rw = (c < hi ? c : hi - 1) >> 6;
+                int sgi = rw < (u32)NROW && PROBE != 2 ? sg_row[rw] : 0;   // past the table: search
+                                                           // (PROBE 2, A/B: always search)
 #pragma unroll
-                for (int step = 64; step > 0; step >>= 1)
-                    if (sgi + step < nseg && sg_st[sgi + step] <= p)
-                        sgi += step;
+                for (int k = 0; k < 3; k++)
+                    if (sgi + 1 < nseg && sg_st[sgi + 1] <= p)
+                        sgi++;
+                if (sgi + 1 < nseg && sg_st[sgi + 1] <= p) {   // tiny segments: search on
+                    int lo2 = sgi + 1, hi2 = nseg - 1;
+                    while (lo2 < hi2) {
+                        const int mid = (lo2 + hi2 + 1) >> 1;
+                        if (sg_st[mid] <= p) lo2 = mid; else hi2 = mid - 1;
+                    }
+                    sgi = lo2;
+                }
                 sj[j] = sgi;
                 x[j] = z;
                 y[j] = z;

@@ -2379,6 +2379,14 @@ int lro_main(uint64_t n, int rounds)
     // <4,6> 712, <2,8> 687 (shipped), <2,7> 692, <3,7> 686, <3,6> 708 (run-per-wave 761,
     // D2D 637); <1,10> / <2,10> (the compiler gives 7 waves) 722 / 714, <1,8> 693
     GROF(2, 8) GROF(3, 7)
+    vs.push_back({"k_gro<2,64,8,FLAT> without the row table", bytes, [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_gro<2, 64, 8, true, 2>), dim3((n + 63) / 64), dim3(256), 0, st, in,
+                           n * stride, off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd);
+    }});
+    vs.push_back({"probe: FLAT <2,64,8> phases A-C + D1 only", bytes, [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_gro<2, 64, 8, true, 1>), dim3((n + 63) / 64), dim3(256), 0, st, in,
+                           n * stride, off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd);
+    }});
     vs.push_back({"verify (launch_verify_desc) for scale", (double)n * (L + 1), [&](hipStream_t st) {
         CK(launch_verify_desc(in, n * stride, off, lens, (u32)n, vd, 0u, st));
     }});
