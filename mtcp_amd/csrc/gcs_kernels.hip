@@ -2229,11 +2229,14 @@ hipError_t launch_classify_fixed(uint8_t* frames, uint64_t stride, u32 frame_len
 // 256 frames; C3 blocks span ~91 KiB), 6 waves per SIMD (26-27 KB of LDS, 80
 // VGPRs).  4M IMIX frames against the list kernel on the same boxes: verify
 // 253-258 vs 284-289 us, fill (fresh check fields) 358-366 vs 428-431 us.  NT
-// loads for both (the stream fill with temporal loads: 374 vs 325 us).
+// loads for both (the stream fill with temporal loads: 374 vs 325 us).  The
+// fill's staged sectors leave with sc1 stores: 340 vs 372 us interleaved, 348
+// vs 364 blocked against nt (plain 345-349, sc0 sc1 344-347), where the list
+// kernel preferred nt (kbench_imix_stream_wm*.log).
 using StreamShip = StreamShape<8, 12288, 6>;
 template <bool COMPUTE>
-using DescStreamShip = DescShape<4, 1, 16, 3, 32, 3, COMPUTE ? WM_SECTOR_NT : kWM, kBlock, true,
-                                 1, 1, COMPUTE, true>;
+using DescStreamShip = DescShape<4, 1, 16, 3, 32, 3, WM_SECTOR_SC1, kBlock, true, 1, 1, COMPUTE,
+                                 true>;
 
 template <bool COMPUTE>
 static hipError_t launch_desc(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,

@@ -1699,6 +1699,19 @@ int imix_main(uint64_t n, int rounds)
     // third (direct RX verdicts, constant te): 258 / 259, phases 0-2 247 (ceiling 239)
     STREAMV(false, "U8 occ6 R12K nt (shipped)", 8, 12288, 6, true, false, 0)
     STREAMV(true, "U8 occ6 R12K nt FRESH (shipped)", 8, 12288, 6, true, false, 0)
+    // the fill's staged write-back policy (shipped: nt)
+#define STREAMWM(TAG, WM_)                                                                  \
+    vs.push_back({"compute stream WM " TAG " FRESH", cb, [&](hipStream_t st) {               \
+        using S_ = DescShape<4, 1, 16, 3, 32, 3, WM_, 256, true, 1, 1, true, true>;          \
+        hipLaunchKernelGGL((k_desc_stream<S_, StreamShape<8, 12288, 6>, true, true>),      \
+                           dim3((n + 255) / 256), dim3(256), 0, st, tx, total, doff, dlen,  \
+                           (u32)n, nullptr, nullptr, 0u);                                   \
+    }});                                                                                    \
+    vs.back().prep = [&](hipStream_t st) {                                                  \
+        hipLaunchKernelGGL(k_zero_checks_desc, dim3((n + 255) / 256), dim3(256), 0, st, tx,  \
+                           doff, dlen, n);                                                  \
+    };
+    STREAMWM("sc1", WM_SECTOR_SC1) STREAMWM("plain", WM_SECTOR) STREAMWM("sc0sc1", WM_SECTOR_SC01)
     // one wave per block, 64 frames (k_desc_wstream)
 #define WSTREAMV(C_, TAG, U_, RMAX_, OCC_)                                                  \
     vs.push_back({std::string(C_ ? "compute" : "verify ") + " wstream " + TAG,              \
