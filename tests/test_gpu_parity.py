@@ -247,7 +247,7 @@ def test_fuzz_desc_vs_oracle(torch_dev, ctx, O):
     np.testing.assert_array_equal(host(d), ref)
 
 
-def stream_case_frames(n, align, seed):
+def stream_case_frames(n, align, seed, jumbo=0.0, dense_block=None):
     """Packed TCP frames for the prefix-sum stream kernel (k_desc_stream):
     mostly fast frames (ihl 5, te == len, any length incl. odd), plus ihl 6-8
     (fast, general masks), ihl 9-15 (slow list), te < len with padding (slow
@@ -257,6 +257,11 @@ def stream_case_frames(n, align, seed):
     lens[rng.random(n) < 0.4] = 64
     m = rng.random(n) < 0.1
     lens[m] = rng.integers(54, 80, size=int(m.sum()))
+    pj = np.full(n, jumbo)
+    if dense_block is not None:
+        pj[256 * dense_block:256 * dense_block + 256] = 0.3
+    m = rng.random(n) < pj                        # long segments (a block may exceed the region cap)
+    lens[m] = rng.integers(1515, 9001, size=int(m.sum()))
     off, total = synth.packed_offsets(lens, align)
     buf = rng.integers(0, 256, size=total + 64, dtype=np.uint8)
     kinds = rng.choice(8, size=n, p=[0.55, 0.08, 0.06, 0.06, 0.07, 0.06, 0.06, 0.06])
@@ -285,15 +290,18 @@ def stream_case_frames(n, align, seed):
     return buf, off, lens
 
 
-@pytest.mark.parametrize("align", [16, 64])
-def test_desc_stream_paths_vs_oracle(torch_dev, ctx, O, align):
+@pytest.mark.parametrize("align,jumbo", [(16, 0.0), (64, 0.0), (16, 0.015)])
+def test_desc_stream_paths_vs_oracle(torch_dev, ctx, O, align, jumbo):
     """Every path of the stream kernel against the oracle, bit-exact: fast
     frames (constant and general masks, Q(te) - Q(64) for te == len), the slow
     list, and whole blocks that fall back to the class passes (a gap > 64 B,
     descriptors out of order, an empty frame)."""
     t = torch_dev
     n = 256 * 24 + 77                                # a partial last block
-    buf, off, lens = stream_case_frames(n, align, seed=align)
+    buf, off, lens = stream_case_frames(n, align, seed=align + int(jumbo * 1000), jumbo=jumbo,
+                                        dense_block=10 if jumbo else None)
+    if jumbo:   # block 10 spans more than the stream's region cap (12,288 chunks): class passes
+        assert ((lens[2560:2816].astype(int) + 15) // 16).sum() > 12288
     off = off.copy()
     # block 3: one gap > 64 B (frames shifted up by 128 B from frame 3*256+10 on)
     off[3 * 256 + 10:] += 128
