@@ -1419,6 +1419,44 @@ __device__ bool gro_cont(const uint8_t* p, const uint8_t* c, int pp, int pc)
     return lds_be32(c + 38) == lds_be32(p + 38) + (u32)pp;
 }
 
+// gro_cont on 32-bit LDS words (rows are 16 B-aligned): the same tests as
+// gro_cont, ~30 dword reads instead of ~80 byte reads per pair.
+__device__ bool gro_cont32(const uint8_t* p, const uint8_t* c, int pp, int pc)
+{
+    if (pp <= 0 || pc <= 0)
+        return false;
+    const u32* P = reinterpret_cast<const u32*>(p);
+    const u32* C = reinterpret_cast<const u32*>(c);
+    if ((P[3] ^ C[3]) & 0xFF000000u)                   // byte 15 (tos)
+        return false;
+    if (((P[5] ^ C[5]) & 0x00FFFFFFu) || (P[5] & 0xFF3Fu))   // bytes 20-22; frag bits
+        return false;
+    if (((P[6] ^ C[6]) & 0xFFFF0000u) || P[7] != C[7] || P[8] != C[8])   // 26..35
+        return false;
+    const u32 idp = bswap16(P[4] >> 16), idc = bswap16(C[4] >> 16);
+    if (idc != idp && idc != ((idp + 1) & 0xFFFFu))
+        return false;
+    if (((P[9] ^ C[9]) & 0x0000FFFFu) || ((P[10] ^ C[10]) & 0xFFFF0000u))   // 36-37, 42-43
+        return false;
+    if (((P[11] ^ C[11]) & 0x00FFFFFFu) || ((P[11] >> 16) & 0x0Fu))   // 44-46; 46's low nibble
+        return false;
+    if (((P[12] ^ C[12]) & 0x0000FFFFu) || (P[13] & 0xFFFFu) || (C[13] & 0xFFFFu))   // 48-49; 52-53
+        return false;
+    const u32 fp = P[11] >> 24, fc = C[11] >> 24;      // byte 47 (flags)
+    if (fp != 0x10u || (fc != 0x10u && fc != 0x18u))
+        return false;
+    const int hl = 34 + 4 * (int)((P[11] >> 20) & 0x0Fu);
+#pragma unroll
+    for (int d = 13; d < 24; d++) {                    // options: bytes [54, hl)
+        const int a = 4 * d < 54 ? 54 : 4 * d, b = 4 * d + 4 < hl ? 4 * d + 4 : hl;
+        if (a < b && ((P[d] ^ C[d]) & (low_mask(b - 4 * d) & ~low_mask(a - 4 * d))))
+            return false;
+    }
+    const u32 sp = __builtin_bswap32((P[9] >> 16) | (P[10] << 16));
+    const u32 sc = __builtin_bswap32((C[9] >> 16) | (C[10] << 16));
+    return sc == sp + (u32)pp;
+}
+
 // W = the largest window the instantiation takes (LDS is sized by it): W = 64
 // needs ~9 KiB of LDS per block instead of ~36 KiB, so a CU holds twice the
 // blocks (8 instead of 4) and twice the run-building waves.
@@ -1426,7 +1464,8 @@ __device__ bool gro_cont(const uint8_t* p, const uint8_t* c, int pp, int pc)
 // one wave per run -- see the comment at phase D2.
 enum { SEG_HDR = 0, SEG_PAY = 1, SEG_WHOLE = 2 };
 
-template <int U, int W = kGroW, int OCC = 1, bool FLAT = false, int PROBE = 0>
+template <int U, int W = kGroW, int OCC = 1, bool FLAT = false, int PROBE = 0,
+          int FWM = WM_SECTOR, bool ACX = false>
 __global__ void __launch_bounds__(kBlock, OCC)
 k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restrict__ off,
       const uint16_t* __restrict__ lens, const uint8_t* __restrict__ verdict, u32 n, u32 window,
@@ -1494,7 +1533,8 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
     __syncthreads();
     // B: continuation
     if (t < cnt)
-        cont[t] = t > 0 && gro_cont(hdr[t - 1], hdr[t], pay[t - 1], pay[t]);
+        cont[t] = t > 0 && (ACX ? gro_cont32(hdr[t - 1], hdr[t], pay[t - 1], pay[t])
+                                : gro_cont(hdr[t - 1], hdr[t], pay[t - 1], pay[t]));
     __syncthreads();
     // C: runs.  A chain is a maximal sequence of frames that each continue the
     // previous one (cont); every frame of a chain is mergeable, so runs are
@@ -1504,7 +1544,37 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
     // (One thread walking the whole window took ~1/3 of the kernel.)
     uint32_t rl = 0;                                   // this thread's run length if it heads one
     bool rs = false;                                   // ... and whether it does
-    if (t < cnt && (t == 0 || !cont[t])) {
+    bool walk = true;                                  // this chain needs the sequential walk
+    if constexpr (ACX) {
+        static_assert(W <= 64, "a window's frames sit in wave 0");
+        // A chain whose whole payload fits max_len is one run: its members'
+        // payload offsets are a segmented scan of the wave, no walk.
+        if (t < 64) {
+            const bool valid = t < cnt, start = !valid || t == 0 || !cont[t];
+            const uint64_t sm = __ballot(start);
+            const uint64_t upto = t == 63 ? ~0ull : ((2ull << t) - 1);
+            const int sh = 63 - __clzll(sm & upto);                 // chain head
+            const uint64_t above = sm & ~upto;
+            const int se = above ? __ffsll((long long)above) - 2 : 63;   // chain's last lane
+            const u32 pv = valid && pay[t] > 0 ? (u32)pay[t] : 0u;
+            const u32 incl = wave_incl_scan(pv), excl = incl - pv;
+            const u32 hx = (u32)__shfl((int)excl, sh, 64);
+            const u32 tot = (u32)__shfl((int)incl, se, 64) - hx;      // the chain's payload
+            const int hp = __shfl(valid ? pay[t] : -1, sh, 64);
+            const u32 hhl = 34 + 4 * (hdr[sh][46] >> 4);
+            const bool fits = hp > 0 && hhl + tot <= max_len;
+            walk = !fits;
+            if (valid && fits) {
+                pref[t] = excl - hx;
+                rhead[t] = (uint16_t)sh;
+                if (t == sh) {
+                    rn_at[t] = (uint16_t)(se - sh + 1);
+                    rl_at[t] = hhl + tot;
+                }
+            }
+        }
+    }
+    if (walk && t < cnt && (t == 0 || !cont[t])) {
         int cur = t;
         u32 mlen = pay[t] > 0 ? 34 + 4 * (hdr[t][46] >> 4) + (u32)pay[t]
                               : (dok[t] ? (u32)lens[w0 + t] : 0u);     // a bad descriptor: nothing
@@ -1780,7 +1850,7 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
                     }
                 }
                 if ((int64_t)p + 16 <= wl_all) {
-                    stg16<WM_SECTOR>(ob + p, x[j]);
+                    stg16<FWM>(ob + p, x[j]);
                 } else {
                     for (int k = 0; k < 16 && (int64_t)(p + k) < wl_all && (!merged || p + k < rend); k++)
                         ob[p + k] = (uint8_t)chunk_byte(x[j], k);
@@ -1839,7 +1909,7 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
                 if (16 * c >= (int)mlen)
                     break;
                 if ((int64_t)p + 16 <= wl_all) {
-                    stg16<WM_SECTOR>(ob + p, sc[c]);
+                    stg16<FWM>(ob + p, sc[c]);
                 } else {
                     for (int k = 0; k < 16 && (int64_t)(p + k) < wl_all && 16 * c + k < (int)mlen; k++)
                         ob[p + k] = (uint8_t)chunk_byte(sc[c], k);
@@ -2348,11 +2418,15 @@ hipError_t launch_gro(const uint8_t* in, uint64_t in_bytes, const uint64_t* off,
     // runs of 8, 928 us (LDS-bound, 4 blocks per CU) -> 809 (89 VGPRs, 5 per
     // SIMD) -> 772 us (<= 80 VGPRs, 6 per SIMD) -> 687 us with phase D as one
     // stream over the window's output (FLAT; 53 VGPRs, 8 waves per SIMD; the
-    // run-per-wave form 761 us on the same box; tools/kbench lro)
+    // run-per-wave form 761 us on the same box) -> 671-674 us with the word-wise
+    // continuation test and scanned chains (ACX; phases A-C 121 -> 90 us) ->
+    // 646 us back to back with nt stores (678 interleaved behind other kernels,
+    // where sc0 sc1 stores measured 655; plain 671-674 both ways; tools/kbench lro)
     if (window <= 64)
-        hipLaunchKernelGGL((k_gro<2, 64, 8, true>), dim3((n + window - 1) / window), dim3(kBlock),
-                           0, s, in, in_bytes, off, len, verdict, n, window, max_len, out,
-                           out_bytes, out_off, out_len, head);
+        hipLaunchKernelGGL((k_gro<2, 64, 8, true, 0, WM_SECTOR_NT, true>),
+                           dim3((n + window - 1) / window), dim3(kBlock), 0, s, in, in_bytes, off,
+                           len, verdict, n, window, max_len, out, out_bytes, out_off, out_len,
+                           head);
     else
         hipLaunchKernelGGL((k_gro<2, kGroW>), dim3((n + window - 1) / window), dim3(kBlock), 0, s,
                            in, in_bytes, off, len, verdict, n, window, max_len, out, out_bytes,

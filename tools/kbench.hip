@@ -2392,6 +2392,30 @@ int lro_main(uint64_t n, int rounds)
     // <4,6> 712, <2,8> 687 (shipped), <2,7> 692, <3,7> 686, <3,6> 708 (run-per-wave 761,
     // D2D 637); <1,10> / <2,10> (the compiler gives 7 waves) 722 / 714, <1,8> 693
     GROF(2, 8) GROF(3, 7)
+#define GROFWM(TAG, WM_)                                                                     \
+    vs.push_back({"k_gro<2,64,8,FLAT> stores " TAG, bytes, [&](hipStream_t st) {            \
+        hipLaunchKernelGGL((k_gro<2, 64, 8, true, 0, WM_>), dim3((n + 63) / 64), dim3(256), 0, st, \
+                           in, n * stride, off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, \
+                           oo, ol, hd);                                                     \
+    }});
+    GROFWM("sc1", WM_SECTOR_SC1) GROFWM("nt", WM_SECTOR_NT) GROFWM("sc0sc1", WM_SECTOR_SC01)
+    vs.push_back({"k_gro<2,64,8,FLAT> ACX (word compares, scanned chains)", bytes, [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_gro<2, 64, 8, true, 0, WM_SECTOR, true>), dim3((n + 63) / 64),
+                           dim3(256), 0, st, in, n * stride, off, lens, vd, (u32)n, 64u, 16384u,
+                           out, n * stride, oo, ol, hd);
+    }});
+#define GROACX(TAG, WM_)                                                                     \
+    vs.push_back({"k_gro<2,64,8,FLAT> ACX stores " TAG, bytes, [&](hipStream_t st) {        \
+        hipLaunchKernelGGL((k_gro<2, 64, 8, true, 0, WM_, true>), dim3((n + 63) / 64),         \
+                           dim3(256), 0, st, in, n * stride, off, lens, vd, (u32)n, 64u, 16384u, \
+                           out, n * stride, oo, ol, hd);                                    \
+    }});
+    GROACX("nt", WM_SECTOR_NT) GROACX("sc0sc1", WM_SECTOR_SC01)
+    vs.push_back({"probe: FLAT <2,64,8> ACX phases A-C + D1 only", bytes, [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_gro<2, 64, 8, true, 1, WM_SECTOR, true>), dim3((n + 63) / 64),
+                           dim3(256), 0, st, in, n * stride, off, lens, vd, (u32)n, 64u, 16384u,
+                           out, n * stride, oo, ol, hd);
+    }});
     vs.push_back({"k_gro<2,64,8,FLAT> without the row table", bytes, [&](hipStream_t st) {
         hipLaunchKernelGGL((k_gro<2, 64, 8, true, 2>), dim3((n + 63) / 64), dim3(256), 0, st, in,
                            n * stride, off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd);
