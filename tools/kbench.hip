@@ -2411,6 +2411,13 @@ int lro_main(uint64_t n, int rounds)
                            out, n * stride, oo, ol, hd);                                    \
     }});
     GROACX("nt", WM_SECTOR_NT) GROACX("sc0sc1", WM_SECTOR_SC01)
+#define GROPF(PF_)                                                                           \
+    vs.push_back({"k_gro<2,64,8,FLAT> ACX nt PF" #PF_, bytes, [&](hipStream_t st) {          \
+        hipLaunchKernelGGL((k_gro<2, 64, 8, true, 0, WM_SECTOR_NT, true, PF_>), dim3((n + 63) / 64), \
+                           dim3(256), 0, st, in, n * stride, off, lens, vd, (u32)n, 64u, 16384u, \
+                           out, n * stride, oo, ol, hd);                                    \
+    }});
+    GROPF(4) GROPF(8)
     vs.push_back({"probe: FLAT <2,64,8> ACX phases A-C + D1 only", bytes, [&](hipStream_t st) {
         hipLaunchKernelGGL((k_gro<2, 64, 8, true, 1, WM_SECTOR, true>), dim3((n + 63) / 64),
                            dim3(256), 0, st, in, n * stride, off, lens, vd, (u32)n, 64u, 16384u,
