@@ -1514,7 +1514,9 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
     if constexpr (PF > 0) {
         if (t >= 64 && cnt > 0) {
             const uint64_t a = off[w0] & ~15ull, l = off[w0 + cnt - 1] + lens[w0 + cnt - 1];
-            const uint64_t b = l < in_bytes ? l : in_bytes;
+            uint64_t b = l < in_bytes ? l : in_bytes;
+            if (b > a && b - a > 64ull * 4096)         // not a packed window: no prefetch
+                b = a;
             u32 x = 0;
             for (uint64_t base = a + 16ull * (t - 64); base < b; base += 16ull * 192 * PF) {
                 uint4 v[PF];
