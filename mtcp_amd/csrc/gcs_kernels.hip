@@ -1240,7 +1240,7 @@ __device__ __forceinline__ void cf_assemble(int base, int sub, int hl, int te, c
 // constant-mask path (accum_fast5).  1M x 1500 B: 706-711 -> 576-624 us
 // against the earlier form (88 VGPRs, first batch copied; kbench copy,
 // profiles/r02/kbench_copy_fill2*.log).
-template <int G, int U, int OCC = 1>
+template <int G, int U, int OCC = 1, int CWM = WM_SECTOR>
 __global__ void __launch_bounds__(kBlock, OCC)
 k_copy_fill(uint8_t* __restrict__ frames, uint64_t frames_bytes,
              const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens,
@@ -1319,7 +1319,7 @@ k_copy_fill(uint8_t* __restrict__ frames, uint64_t frames_bytes,
                 if (c >= nchunks || cb >= te)
                     continue;
                 if (cb + 16 <= avail) {
-                    stg16<WM_SECTOR>(f + cb, x[j]);
+                    stg16<CWM>(f + cb, x[j]);
                 } else {
                     for (int k = 0; k < 16 && cb + k < te; k++)
                         f[cb + k] = (uint8_t)chunk_byte(x[j], k);
@@ -1351,7 +1351,7 @@ k_copy_fill(uint8_t* __restrict__ frames, uint64_t frames_bytes,
             if (c < 8 || c >= nchunks || cb >= te)
                 continue;
             if (cb + 16 <= avail) {
-                stg16<WM_SECTOR>(f + cb, x[j]);
+                stg16<CWM>(f + cb, x[j]);
             } else {
                 for (int k = 0; k < 16 && cb + k < te; k++)
                     f[cb + k] = (uint8_t)chunk_byte(x[j], k);
@@ -2426,9 +2426,12 @@ hipError_t launch_copy_fill(uint8_t* frames, uint64_t frames_bytes, const uint64
                             u32 flags, hipStream_t s)
 {
     // 16 lanes x 6 chunks per frame (124 VGPRs, 4 waves per SIMD, no spills):
-    // as fast as <32,3> at 6 waves, which spills (576-624 us per 1M x 1500 B)
+    // as fast as <32,3> at 6 waves, which spills (576-624 us per 1M x 1500 B).
+    // Payload chunks leave with nt stores: 602 vs 625 us back to back, 627 vs
+    // 625 interleaved (sc0 sc1: 621 / 616; tools/kbench copy, kbench_cf_wm*.log)
     constexpr int G = 16, U = 6, FPB = kBlock / G;
-    hipLaunchKernelGGL((k_copy_fill<G, U>), dim3((n + FPB - 1) / FPB), dim3(kBlock), 0, s, frames,
+    hipLaunchKernelGGL((k_copy_fill<G, U, 1, WM_SECTOR_NT>), dim3((n + FPB - 1) / FPB),
+                       dim3(kBlock), 0, s, frames,
                        frames_bytes, off, len, src, src_bytes, src_off, n, status, csums, flags);
     return hipGetLastError();
 }

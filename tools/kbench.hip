@@ -2228,7 +2228,14 @@ int copy_main(uint64_t n, int rounds)
                            dim3(256), 0, st_, tx, n * stride, off, lens, src, n * plen + 64, soff, \
                            (u32)n, st, nullptr, 0u);                                           \
     }});
-    CF2(32, 3, 6) CF2(16, 6, 1) CF2(16, 6, 4) CF2(32, 3, 5)
+    CF2(16, 6, 1)
+#define CFWM(TAG, WM_)                                                                       \
+    vs.push_back({"fused copy + fill <16,6> stores " TAG, bytes, [&](hipStream_t st_) {     \
+        hipLaunchKernelGGL((k_copy_fill<16, 6, 1, WM_>), dim3((n + 15) / 16), dim3(256), 0, st_, \
+                           tx, n * stride, off, lens, src, n * plen + 64, soff, (u32)n, st,    \
+                           nullptr, 0u);                                                     \
+    }});
+    CFWM("nt", WM_SECTOR_NT) CFWM("sc0sc1", WM_SECTOR_SC01) CFWM("sc1", WM_SECTOR_SC1)
     uint8_t *asrc, *cdst;                     // copy ceilings write cdst, never tx
     CK(hipMalloc(&asrc, n * stride));
     CK(hipMalloc(&cdst, n * stride));
