@@ -343,6 +343,33 @@ def test_desc_stream_paths_vs_oracle(torch_dev, ctx, O, align, jumbo):
         assert (rv[bad[lens[bad] > 0]] != 0).any()
 
 
+def test_desc_no_inplace_and_null_outputs(torch_dev, ctx, O):
+    """Descriptor batches (the stream kernel and its fallback blocks):
+    GCS_CF_NO_INPLACE leaves the frames untouched and still returns the checks;
+    a fill with no status / csum outputs still fills in place."""
+    t = torch_dev
+    n = 256 * 6 + 5
+    buf, off, lens = stream_case_frames(n, 64, seed=77)
+    off = off.copy()
+    a, b = 2 * 256 + 3, 2 * 256 + 4                  # block 2 falls back (descriptors swapped)
+    off[a], off[b] = off[b], off[a]
+    lens[a], lens[b] = lens[b], lens[a]
+    doff, dlen = dev(t, off.view(np.int64)), dev(t, lens.view(np.int16))
+    ref = buf.copy()
+    rst, rcs = O.compute_batch(ref, off, lens)
+    d = dev(t, buf)
+    st = t.zeros(n, dtype=t.uint8, device="cuda")
+    cs = t.zeros(n, dtype=t.int32, device="cuda")
+    ctx.compute(d, doff, dlen, n, st, cs, flags=K["GCS_CF_NO_INPLACE"])
+    ctx.sync()
+    np.testing.assert_array_equal(host(d), buf)
+    np.testing.assert_array_equal(host(st), rst)
+    np.testing.assert_array_equal(host(cs).view(np.uint32), rcs)
+    ctx.compute(d, doff, dlen, n)
+    ctx.sync()
+    np.testing.assert_array_equal(host(d), ref)
+
+
 def test_desc_stream_region_at_buffer_end(torch_dev, ctx, O):
     """A streaming block whose region ends exactly at frames_bytes (16 B-
     aligned: streamed; not aligned: the block falls back to guarded loads)."""
