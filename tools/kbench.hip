@@ -1712,6 +1712,18 @@ int imix_main(uint64_t n, int rounds)
                            doff, dlen, n);                                                  \
     };
     STREAMWM("sc1", WM_SECTOR_SC1) STREAMWM("plain", WM_SECTOR) STREAMWM("sc0sc1", WM_SECTOR_SC01)
+#define STREAMWMT(TAG, WM_)                                                                 \
+    vs.push_back({"compute stream WM " TAG " temporal loads FRESH", cb, [&](hipStream_t st) { \
+        using S_ = DescShape<4, 1, 16, 3, 32, 3, WM_, 256, true, 1, 1, true, false>;         \
+        hipLaunchKernelGGL((k_desc_stream<S_, StreamShape<8, 12288, 6>, true, true>),      \
+                           dim3((n + 255) / 256), dim3(256), 0, st, tx, total, doff, dlen,  \
+                           (u32)n, nullptr, nullptr, 0u);                                   \
+    }});                                                                                    \
+    vs.back().prep = [&](hipStream_t st) {                                                  \
+        hipLaunchKernelGGL(k_zero_checks_desc, dim3((n + 255) / 256), dim3(256), 0, st, tx,  \
+                           doff, dlen, n);                                                  \
+    };
+    STREAMWMT("sc1", WM_SECTOR_SC1) STREAMWMT("sc0sc1", WM_SECTOR_SC01)
     // one wave per block, 64 frames (k_desc_wstream)
 #define WSTREAMV(C_, TAG, U_, RMAX_, OCC_)                                                  \
     vs.push_back({std::string(C_ ? "compute" : "verify ") + " wstream " + TAG,              \
@@ -2425,6 +2437,21 @@ int lro_main(uint64_t n, int rounds)
                            out, n * stride, oo, ol, hd);                                    \
     }});
     GROPF(4) GROPF(8)
+    vs.push_back({"k_gro<2,64,8,FLAT> ACX sc0sc1 PF8", bytes, [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_gro<2, 64, 8, true, 0, WM_SECTOR_SC01, true, 8>), dim3((n + 63) / 64),
+                           dim3(256), 0, st, in, n * stride, off, lens, vd, (u32)n, 64u, 16384u,
+                           out, n * stride, oo, ol, hd);
+    }});
+    vs.push_back({"k_gro<3,64,7,FLAT> ACX nt PF8", bytes, [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_gro<3, 64, 7, true, 0, WM_SECTOR_NT, true, 8>), dim3((n + 63) / 64),
+                           dim3(256), 0, st, in, n * stride, off, lens, vd, (u32)n, 64u, 16384u,
+                           out, n * stride, oo, ol, hd);
+    }});
+    vs.push_back({"k_gro<2,64,8,FLAT> ACX nt PF16", bytes, [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_gro<2, 64, 8, true, 0, WM_SECTOR_NT, true, 16>), dim3((n + 63) / 64),
+                           dim3(256), 0, st, in, n * stride, off, lens, vd, (u32)n, 64u, 16384u,
+                           out, n * stride, oo, ol, hd);
+    }});
     vs.push_back({"probe: FLAT <2,64,8> ACX phases A-C + D1 only", bytes, [&](hipStream_t st) {
         hipLaunchKernelGGL((k_gro<2, 64, 8, true, 1, WM_SECTOR, true>), dim3((n + 63) / 64),
                            dim3(256), 0, st, in, n * stride, off, lens, vd, (u32)n, 64u, 16384u,
