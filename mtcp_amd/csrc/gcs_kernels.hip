@@ -5,6 +5,7 @@
 #include "gcs_internal.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace gcs {
 
@@ -773,8 +774,9 @@ k_desc_mixed_x(uint8_t* __restrict__ frames, uint64_t frames_bytes,
 // gaps <= 64 B, and the region (<= RMAX chunks) ends inside the buffer;
 // otherwise it runs desc_mixed's three class passes.  Reference layout:
 // PSIO's packed chunk (pslib.c:132-156, ps.h:181-213).
-template <int U_, int RMAX_, int OCC_, bool PIPE_ = false, int PROBE_ = 0>
+template <int U_, int RMAX_, int OCC_, bool PIPE_ = false, int PROBE_ = 0, bool HDR3_ = false>
 struct StreamShape {
+    static constexpr bool HDR3 = HDR3_;   // RX: stash chunks 0..2 only (ihl = 5 fast frames)
     static constexpr int U = U_;          // chunks per lane per trip (64 * U per wave)
     static constexpr int RMAX = RMAX_;    // region chunks a streaming block may span
     static constexpr int OCC = OCC_;
@@ -793,6 +795,7 @@ __device__ __forceinline__ void desc_stream(uint8_t* __restrict__ frames, uint64
     static_assert(S::F == kBlock && S::R == 1, "one descriptor per thread");
     static_assert(!COMPUTE || S::STAGE, "TX stages sector 0 in hdr");
     constexpr int F = kBlock, NW = kBlock / 64, RW = T::RMAX / 64, U = T::U;
+    constexpr int NH = (!COMPUTE && T::HDR3) ? 3 : 4;   // header chunks stashed per frame
     __shared__ uint64_t soff[F];
     __shared__ uint16_t slen[F];
     __shared__ uint16_t list[3][F];
@@ -800,7 +803,7 @@ __device__ __forceinline__ void desc_stream(uint8_t* __restrict__ frames, uint64
     __shared__ int wcnt[3][NW];
     __shared__ uint8_t codes[F];
     __shared__ uint32_t csums[COMPUTE ? F : 1];
-    __shared__ uint4 hdr[4 * F];       // chunks 0..3 per frame; TX: the staged sector 0
+    __shared__ uint4 hdr[NH * F];      // chunks 0..NH-1 per frame; TX: the staged sector 0
     __shared__ uint64_t bm[RW];        // bit c: a frame starts at region chunk c
     __shared__ uint16_t rbase[RW];     // frames starting before chunk 64 * w
     __shared__ u32 meta[F];            // start chunk << 16 | len
@@ -904,9 +907,9 @@ __device__ __forceinline__ void desc_stream(uint8_t* __restrict__ frames, uint64
     if (t < nf) {
         meta[t] = start << 16 | len;
 #pragma unroll
-        for (int k = 0; k < 4; k++)
+        for (int k = 0; k < NH; k++)
             if ((u32)k >= nch)
-                hdr[4 * t + k] = make_uint4(0, 0, 0, 0);
+                hdr[NH * t + k] = make_uint4(0, 0, 0, 0);
         atomicOr((unsigned long long*)&bm[start >> 6], 1ull << (start & 63));
         const u32 rhi = t + 1 < nf ? snext >> 6 : NR - 1;
         for (u32 r = (start >> 6) + 1; r <= rhi; r++)
@@ -955,8 +958,8 @@ __device__ __forceinline__ void desc_stream(uint8_t* __restrict__ frames, uint64
                 if (c < hi) {
                     const u32 m = meta[f], fl = m & 0xFFFFu;
                     const u32 k = c - (m >> 16), fn = (fl + 15) >> 4;
-                    if (k < 4 && k < fn)
-                        hdr[4 * f + k] = v[j];
+                    if (k < (u32)NH && k < fn)
+                        hdr[NH * f + k] = v[j];
                     if (k == 0)
                         pfirst[f] = excl;
                     if (k + 1 == fn)
@@ -999,7 +1002,8 @@ __device__ __forceinline__ void desc_stream(uint8_t* __restrict__ frames, uint64
     {
         const u32 QW = ((NCH + 4 * 64 - 1) / (4 * 64)) * 64;
         const int tf = t < nf ? t : 0;
-        const uint4 h4[4] = {hdr[4 * tf], hdr[4 * tf + 1], hdr[4 * tf + 2], hdr[4 * tf + 3]};
+        const uint4 h4[4] = {hdr[NH * tf], hdr[NH * tf + 1], hdr[NH * tf + 2],
+                             NH == 4 ? hdr[NH * tf + 3] : make_uint4(0, 0, 0, 0)};
         Hdr h;
         h.d3 = h4[0].w;
         h.d4 = h4[1].x;
@@ -1007,12 +1011,17 @@ __device__ __forceinline__ void desc_stream(uint8_t* __restrict__ frames, uint64
         const int ihl = (int)((h.d3 >> 16) & 15u);
         const int ts = 14 + 4 * ihl;
         const int te = 14 + (int)bswap16(h.d4 & 0xFFFFu);
-        const bool fast = t < nf && ihl <= 8 && (te <= 64 || te == (int)len);
+        // NH = 3 (RX): chunk 3 is not stashed; words [48, te) come from the
+        // prefixes, and doff (byte ts + 12) must lie in chunk 2: ihl == 5
+        constexpr int HB = 16 * NH;                  // header bytes held per frame
+        const bool fast = t < nf && (NH == 4 ? ihl <= 8 : ihl == 5) &&
+                          (te <= HB || te == (int)len);
         // wave-uniform: every fast frame of the wave has ihl == 5, so the word
-        // masks of chunks 0..3 are constants (masks5, as the group kernels);
-        // and when every one also has te >= 64, no segment end lies in them
+        // masks of the stashed chunks are constants (masks5, as the group
+        // kernels); and when every one also has te >= HB, no segment end lies
+        // in them
         const bool all5 = __all(!fast || ihl == 5);
-        const bool end64 = __all(!fast || te >= 64);
+        const bool end64 = __all(!fast || te >= HB);
         // RX: fast frames' verdicts go straight out (coalesced, frame order)
         uint8_t* oc = (!COMPUTE && out_code) ? out_code + f0 + t : codes + t;
         if (t < nf && !fast) {
@@ -1021,18 +1030,18 @@ __device__ __forceinline__ void desc_stream(uint8_t* __restrict__ frames, uint64
             Acc a = {0u, 0u, 0u};
             if (all5 && end64) {
 #pragma unroll
-                for (int c = 0; c < 4; c++)
-                    accum_fast5<COMPUTE, true>(h4[c], c, 64, masks5<COMPUTE>(c), a);
+                for (int c = 0; c < NH; c++)
+                    accum_fast5<COMPUTE, true>(h4[c], c, HB, masks5<COMPUTE>(c), a);
             } else if (all5) {
 #pragma unroll
-                for (int c = 0; c < 4; c++)
-                    accum_fast5<COMPUTE, true>(h4[c], c, te, masks5<COMPUTE>(c), a);
+                for (int c = 0; c < NH; c++)
+                    accum_fast5<COMPUTE, true>(h4[c], c, te < HB ? te : HB, masks5<COMPUTE>(c), a);
             } else {
 #pragma unroll
-                for (int j = 0; j < 4; j++)
-                    accum_chunk<COMPUTE>(h4[j], 16 * j, ts, te, a);
+                for (int j = 0; j < NH; j++)
+                    accum_chunk<COMPUTE>(h4[j], 16 * j, ts, te < HB ? te : HB, a);
             }
-            if (te > 64) {
+            if (te > HB) {
                 auto wbase = [&](u32 c) {
                     const u32 q = c / QW;
                     u32 b = 0;
@@ -1043,7 +1052,8 @@ __device__ __forceinline__ void desc_stream(uint8_t* __restrict__ frames, uint64
                 };
                 const u32 p0 = pfirst[t] + wbase(start);
                 const u32 p1 = qend[t] + wbase(start + nch - 1);
-                a.tcp += (p1 - p0) - (hsum4(h4[0]) + hsum4(h4[1]) + hsum4(h4[2]) + hsum4(h4[3]));
+                a.tcp += (p1 - p0) - (hsum4(h4[0]) + hsum4(h4[1]) + hsum4(h4[2]) +
+                                      (NH == 4 ? hsum4(h4[3]) : 0u));
             }
             epilogue<1, 4, COMPUTE, S::WM, false>(
                 h, a, frames + o, len, (int64_t)(frames_bytes - o), true, 0, flags, oc,
@@ -2327,7 +2337,12 @@ hipError_t launch_classify_fixed(uint8_t* frames, uint64_t stride, u32 frame_len
 // fill's staged sectors leave with sc1 stores: 340 vs 372 us interleaved, 348
 // vs 364 blocked against nt (plain 345-349, sc0 sc1 344-347), where the list
 // kernel preferred nt (kbench_imix_stream_wm*.log).
-using StreamShip = StreamShape<8, 12288, 6>;
+// RX stashes chunks 0..2 only (HDR3: ihl = 5 fast frames; LDS 27 -> 22 KB)
+// and runs 7 waves per SIMD (72 VGPRs): 240.7-245.7 vs 249-255 us interleaved,
+// 244.0 vs 244.6 blocked (kbench_imix_stream_h3*.log).
+template <bool COMPUTE>
+using StreamShip = typename std::conditional<COMPUTE, StreamShape<8, 12288, 6>,
+                                             StreamShape<8, 12288, 7, false, 0, true>>::type;
 template <bool COMPUTE>
 using DescStreamShip = DescShape<4, 1, 16, 3, 32, 3, WM_SECTOR_SC1, kBlock, true, 1, 1, COMPUTE,
                                  true>;
@@ -2343,7 +2358,8 @@ static hipError_t launch_desc(uint8_t* frames, uint64_t frames_bytes, const uint
         hipLaunchKernelGGL((k_desc_mixed_x<S, COMPUTE, kXCD, kDescOcc>), grid, dim3(kBlock), 0, s,
                            frames, frames_bytes, off, len, n, code, csums, flags, ext);
     else
-        hipLaunchKernelGGL((k_desc_stream<DescStreamShip<COMPUTE>, StreamShip, COMPUTE, kXCD>),
+        hipLaunchKernelGGL((k_desc_stream<DescStreamShip<COMPUTE>, StreamShip<COMPUTE>, COMPUTE,
+                                          kXCD>),
                            grid, dim3(kBlock), 0, s, frames, frames_bytes, off, len, n, code,
                            csums, flags);
     return hipGetLastError();

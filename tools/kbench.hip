@@ -1698,6 +1698,14 @@ int imix_main(uint64_t n, int rounds)
     // U4 phases 0-2 alone 238, read ceiling 230; fill FRESH 359-361 (list kernel 428);
     // third (direct RX verdicts, constant te): 258 / 259, phases 0-2 247 (ceiling 239)
     STREAMV(false, "U8 occ6 R12K nt (shipped)", 8, 12288, 6, true, false, 0)
+#define STREAMH3(TAG, OCC_)                                                                 \
+    vs.push_back({"verify  stream HDR3 " TAG, vb, [&](hipStream_t st) {                     \
+        using S_ = DescShape<4, 1, 16, 3, 32, 3, kWM, 256, true, 1, 1, false, true>;        \
+        using T_ = StreamShape<8, 12288, OCC_, false, 0, true>;                            \
+        hipLaunchKernelGGL((k_desc_stream<S_, T_, false, true>), dim3((n + 255) / 256),    \
+                           dim3(256), 0, st, rx, total, doff, dlen, (u32)n, v1, nullptr, 0u); \
+    }});
+    STREAMH3("occ6", 6) STREAMH3("occ7", 7) STREAMH3("occ8", 8)
     STREAMV(true, "U8 occ6 R12K nt FRESH (shipped)", 8, 12288, 6, true, false, 0)
     // the fill's staged write-back policy (shipped: nt)
 #define STREAMWM(TAG, WM_)                                                                  \
