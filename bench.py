@@ -300,6 +300,15 @@ def c1_small_frames(ctx, torch, n=1 << 20, steps=20):
     key = "cache_resident_gbs_algorithmic" if n * stride <= (128 << 20) else \
         "hbm_gbs_algorithmic"
     out[key] = n * (L + 1) / (ms * 1e-3) / 1e9
+    # one launch at a time, each after a cache scrub: the HBM-resident figure
+    # at this size (the back-to-back rate above reads a cached batch)
+    cms = _launch_ms_cold(torch, lambda: ctx.verify_fixed(buf, stride, L, n, v, stream=stream))
+    assert int((v != 0).sum()) == 0
+    out["cold_ms"] = cms
+    out["cold_gpkt_per_s"] = n / cms / 1e6
+    out["cold_frac_peak"] = n * (L + 1) / (cms * 1e-3) / 1e9 / HBM_PEAK_GBS
+    out["cold_note"] = ("single launches, each after an untimed write + read of 1 GiB "
+                        "(4x the Infinity Cache): no line of the batch cached")
     return out
 
 
@@ -338,22 +347,51 @@ def _launch_ms(torch, fn, reps=20, warm=3):
     return e0.elapsed_time(e1) / reps
 
 
-def _launch_ms_fresh(torch, fn, prep, reps=20):
+SCRUB_BYTES = 1 << 30   # 4x the 256 MB Infinity Cache (MI355X_MICROARCH.md)
+_scrub_buf = []
+
+
+def _scrub(torch):
+    """Untimed: write, then read, 1 GiB that no measured kernel touches, so
+    neither the L2s nor the Infinity Cache hold any line of the batch -- and
+    none of the scrub's own lines is dirty -- when the next launch starts.
+    The read pass evicts the write pass's dirty lines (written back here,
+    before the timed region), leaving only clean lines behind."""
+    if not _scrub_buf:
+        _scrub_buf.append(torch.empty(SCRUB_BYTES // 4, dtype=torch.int32, device="cuda"))
+    b = _scrub_buf[0]
+    b.fill_(int(time.perf_counter_ns() & 0x7FFF))
+    return b.sum()   # a device scalar: stays on the stream, no host sync
+
+
+def _launch_ms_fresh(torch, fn, prep, reps=20, scrub=False):
     """Mean HIP-event time of `fn()` timed launch by launch, with the untimed
     `prep()` before each: a TX fill over frames whose check fields are zero,
     as mTCP hands them over (ip_out.c:153, tcp_out.c:323), instead of a refill
-    of the checks it wrote last time (unchanged bytes write back cheaper)."""
-    _settle(torch, lambda: (prep(), fn()))
+    of the checks it wrote last time (unchanged bytes write back cheaper).
+    scrub: after prep() and before the timed launch, `_scrub` the caches
+    (cache-cold: prep's zeroed sectors are written back to HBM and evicted,
+    so the launch reads and writes every line from and to HBM)."""
+    _settle(torch, lambda: (prep and prep(), fn()))
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(reps)]
     torch.cuda.synchronize()
     for e0, e1 in evs:
-        prep()
+        if prep is not None:
+            prep()
+        if scrub:
+            _scrub(torch)
         e0.record()
         fn()
         e1.record()
     torch.cuda.synchronize()
     return float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+
+
+def _launch_ms_cold(torch, fn, reps=20):
+    """Mean HIP-event time of single launches of `fn()`, each after a cache
+    scrub (`_scrub`): no line of its batch is cached when it starts."""
+    return _launch_ms_fresh(torch, fn, None, reps=reps, scrub=True)
 
 
 def c2_max_frame(ctx, torch, n=1 << 20, L=1514):
@@ -392,21 +430,35 @@ def c3_imix(ctx, torch, n=4 << 20):
 
     fms = _launch_ms_fresh(torch, lambda: ctx.compute(buf, off, ln, n, stream=stream),
                            zero_checks)
+    # the same with the caches scrubbed between the zeroing and the launch:
+    # zero_checks dirties exactly the 64 B sectors the fill then reads and
+    # writes (268 MB, about the Infinity Cache's size)
+    fcold = _launch_ms_fresh(torch, lambda: ctx.compute(buf, off, ln, n, stream=stream),
+                             zero_checks, scrub=True)
     ctx.verify(buf, off, ln, n, v, stream=stream)
     torch.cuda.synchronize()
     assert int((v != 0).sum()) == 0
+    vcold = _launch_ms_cold(torch, lambda: ctx.verify(buf, off, ln, n, v, stream=stream))
+    assert int((v != 0).sum()) == 0
     nbytes = int(lens.astype(np.int64).sum())
+    tx_alg, rx_alg = nbytes + n * 14, nbytes + n * 11
     return {"workload": f"C3: {n} IMIX frames (mean {nbytes / n:.1f} B), {total / 1e9:.2f} GB "
                         "packed at 64 B, descriptor batch",
             "verify_ms": vms, "compute_ms": fms, "compute_refill_ms": cms,
+            "compute_ms_cold": fcold, "verify_ms_cold": vcold,
             "compute_note": "compute_ms: check fields zeroed (untimed) before each launch, as "
-                            "mTCP hands frames over; compute_refill_ms: back-to-back refills of "
-                            "the same batch (its sector write-back rewrites unchanged bytes)",
+                            "mTCP hands frames over; compute_ms_cold: the same, with the caches "
+                            "scrubbed (1 GiB written + read, untimed) after the zeroing; "
+                            "compute_refill_ms: back-to-back refills of the same batch (its "
+                            "sector write-back rewrites unchanged bytes); verify_ms_cold: single "
+                            "launches after a scrub",
             "verify_gpkt_per_s": n / vms / 1e6, "compute_gpkt_per_s": n / fms / 1e6,
-            "verify_hbm_gbs_algorithmic": (nbytes + n * 11) / (vms * 1e-3) / 1e9,
-            "compute_hbm_gbs_algorithmic": (nbytes + n * 14) / (fms * 1e-3) / 1e9,
-            "verify_frac_peak": (nbytes + n * 11) / (vms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-            "compute_frac_peak": (nbytes + n * 14) / (fms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+            "verify_hbm_gbs_algorithmic": rx_alg / (vms * 1e-3) / 1e9,
+            "compute_hbm_gbs_algorithmic": tx_alg / (fms * 1e-3) / 1e9,
+            "verify_frac_peak": rx_alg / (vms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "compute_frac_peak": tx_alg / (fms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "compute_cold_frac_peak": tx_alg / (fcold * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "verify_cold_frac_peak": rx_alg / (vcold * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
 def rows_8f(ctx, torch, n=1 << 20, L=1500):
@@ -492,6 +544,38 @@ def c2_sector_wb(ctx, torch, tx, stride, L, n):
             "sector_frac_peak": n * (L + 4) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "line_compute_ms": line_ms,
             "line_frac_peak": n * (L + 4) / (line_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+
+
+def c2_fresh_cold(ctx, torch, tx, stride, L, n):
+    """The C2 TX fill over check fields zeroed before each launch (as mTCP
+    hands frames over, ip_out.c:153, tcp_out.c:244, 323), with the caches
+    scrubbed between the zeroing and the timed launch (`_scrub`), in the
+    library's default write-back and with sector write-back forced; and the
+    RX verify as single scrubbed launches."""
+    stream = torch.cuda.current_stream().cuda_stream
+    rows = tx.view(n, stride)
+
+    def zero_checks():
+        rows[:, 24:26] = 0      # iph->check (ETH 14 + 10)
+        rows[:, 50:52] = 0      # tcph->check (ETH 14 + IP 20 + 16)
+
+    flag = gpucsum_K()["GCS_CF_SECTOR_WB"]
+    dflt = _launch_ms_fresh(torch, lambda: ctx.compute_fixed(tx, stride, L, n, stream=stream),
+                            zero_checks, scrub=True)
+    sect = _launch_ms_fresh(torch, lambda: ctx.compute_fixed(tx, stride, L, n, flags=flag,
+                                                             stream=stream),
+                            zero_checks, scrub=True)
+    v = torch.empty(n, dtype=torch.uint8, device="cuda")
+    vms = _launch_ms_cold(torch, lambda: ctx.verify_fixed(tx, stride, L, n, v, stream=stream))
+    assert int((v != 0).sum()) == 0
+    return {"workload": f"{n} x {L}B, stride {stride}: TX fill of zeroed check fields and RX "
+                        "verify, single launches, each after a cache scrub",
+            "compute_ms": dflt, "tx_write_mode": tx_write_mode(n, stride),
+            "compute_frac_peak": n * (L + 4) / (dflt * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "sector_compute_ms": sect,
+            "sector_frac_peak": n * (L + 4) / (sect * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "verify_ms": vms,
+            "verify_frac_peak": n * (L + 1) / (vms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
 def c4_shard(ctx, torch, steps, warmup, settle_s, n=4 << 20, L=1500):
@@ -780,6 +864,8 @@ def main():
             line["c2_sector_wb"] = c2_sector_wb(ctx, torch, tx, stride, L, n)
             sec = line["c2_sector_wb"]
             line["roofline"]["sector_wb_frac"] = sec["sector_frac_peak"]
+            line["c2_fresh_cold"] = c2_fresh_cold(ctx, torch, tx, stride, L, n)
+            line["roofline"]["fresh_cold_frac"] = line["c2_fresh_cold"]["compute_frac_peak"]
             del tx, rx
             torch.cuda.empty_cache()
             line["c4_shard"] = c4_shard(ctx, torch, args.steps, args.warmup, args.settle_s)

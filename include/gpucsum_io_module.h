@@ -130,7 +130,9 @@ extern io_module_func gpucsum_module_func;
 
 /* Set the inner module the decorator wraps.  Call before load_module().
  * Resets the inner caps: GPUCSUM_INNER_TX_EAGER if inner is netmap_module_func,
- * GPUCSUM_INNER_RX_CHAINED if it is dpdk_module_func, else none. */
+ * GPUCSUM_INNER_RX_CHAINED if it is dpdk_module_func (GPUCSUM_INNER_RX_ONCE
+ * instead when the program defines dpdk_module_ip_defrag = 1, which the
+ * integration patch adds to a dpdk_module.c built with IP_DEFRAG), else none. */
 int gpucsum_set_inner(io_module_func *inner);
 /* The inner module (NULL if none): for mTCP's module-identity checks, e.g. the
  * ENABLELRO gather test at tcp_ring_buffer.c:18. */

@@ -282,6 +282,11 @@ class ServerHub {
         // skipped as done
         for (auto& sl : mb_->ring[k].slot)
             sl.a.seq = start;
+        // ... and every block's ack reads as `start` (nothing served yet): an
+        // ack left at 0 would read as NEWER than a request >= 2^31 past it,
+        // and complete an in-place request before its release fence
+        for (auto& a : mb_->ring[k].ack)
+            a.v = start;
         // the ring starts at `start` on the device too: nothing claimed yet
         uint32_t prog[gcs::kServerBlocks];
         for (auto& p : prog)
@@ -1611,7 +1616,22 @@ int async_wait(gcs_ctx* ctx, uint32_t q)
     DeviceGuard g(ctx->device);
     if (ctx->server) {
         int rc = ctx->server->wait(q);
-        if (rc) return rc;
+        if (rc) {
+            // The server did not answer: cancel every pending async fill, so
+            // that no later wait writes an old request's checks into buffers
+            // the caller has since reused (the caller treats the frames as
+            // unfilled; the library forgets their addresses here).  The
+            // staging slot itself is reused only after its server request
+            // completes (BurstServer::post waits for it first).
+            for (auto& a : ctx->areq)
+                if (a.pending) {
+                    a.pending = false;
+                    std::fill(a.ptrs.begin(), a.ptrs.end(), nullptr);
+                    a.status = nullptr;
+                    a.csums = nullptr;
+                }
+            return rc;
+        }
     }
     for (auto& a : ctx->areq)
         if (a.pending && (int32_t)(q - a.q) >= 0)
@@ -1688,6 +1708,12 @@ try {
                 std::memcpy(a.h_stage + used, pkts[i], len[i]);
             used += (len[i] + kSlotAlign - 1) / kSlotAlign * kSlotAlign;
         }
+        // Device staging is mapped write-combining over the BAR: drain the WC
+        // buffers before post() publishes seq (a release store is a plain mov
+        // on x86 and orders nothing against WC stores), so the server never
+        // sees the request before its frame bytes.
+        if (a.stage_dev)
+            __builtin_ia32_sfence();
         frames_d = a.d_stage;
         bytes = (used + 15) / 16 * 16;
     } else {

@@ -62,6 +62,7 @@ struct gthr {
 	uint32_t tx_group;      /* async TX fill: post every tx_group completed frames (0: off) */
 	struct rx_if *rx[GPUCSUM_MAX_IFS];
 	struct tx_if *tx[GPUCSUM_MAX_IFS];
+	struct tx_if *last_tx;  /* the queue of the most recent get_wptr */
 	struct gpucsum_stats st;
 	int rss;                /* RSS steering check on */
 	int own_queue;
@@ -75,6 +76,10 @@ extern io_module_func netmap_module_func __attribute__((weak));
  * 112-135), so any longer frame is an LRO chain (BUF_SIZE 16384, :44-48)
  * and RX_CHAINED is safe to assume for it either way. */
 extern io_module_func dpdk_module_func __attribute__((weak));
+/* ... defined by the integration patch in a DPDK module built with IP_DEFRAG,
+ * whose get_rptr feeds the reassembly table on every call (dpdk_module.c:
+ * 474-513, 527-529): then the inner get_rptr is called once per index. */
+extern const int dpdk_module_ip_defrag __attribute__((weak));
 
 static io_module_func *g_inner;
 static uint32_t g_caps;
@@ -93,7 +98,8 @@ int gpucsum_set_inner(io_module_func *inner)
 	if (&netmap_module_func && inner == &netmap_module_func)
 		g_caps = GPUCSUM_INNER_TX_EAGER;
 	if (&dpdk_module_func && inner == &dpdk_module_func)
-		g_caps = GPUCSUM_INNER_RX_CHAINED;
+		g_caps = (&dpdk_module_ip_defrag && dpdk_module_ip_defrag) ? GPUCSUM_INNER_RX_ONCE
+		                                                           : GPUCSUM_INNER_RX_CHAINED;
 	g_seg_max = GPUCSUM_DEFAULT_SEG_MAX;
 	return GCS_OK;
 }
@@ -374,6 +380,7 @@ static uint8_t *gpucsum_get_wptr(struct mtcp_thread_context *ctx, int ifidx, uin
 	q->ptr[q->n] = p;
 	q->len[q->n] = len;
 	q->n++;
+	g->last_tx = q;
 	return p;
 }
 
@@ -560,11 +567,16 @@ static int32_t gpucsum_dev_ioctl(struct mtcp_thread_context *ctx, int nif, int c
 	switch (cmd) {
 	case PKT_TX_TCPIP_CSUM:       /* tcp_out.c:206, :326               */
 		/* asked after the segment's headers and payload are written: the
-		 * port's most recent get_wptr frame is complete (an ICMP frame's
-		 * PKT_TX_IP_CSUM comes before its ICMP part: not a signal) */
+		 * thread's most recent get_wptr frame is complete (an ICMP frame's
+		 * PKT_TX_IP_CSUM comes before its ICMP part: not a signal).  nif is
+		 * the route's ifindex (sndvar->nif_out), NOT the eidx get_wptr got
+		 * (CONFIG.nif_to_eidx[nif], eth_out.c:52): the two differ unless the
+		 * configured ports are 0..n-1, so the queue is the one of the last
+		 * get_wptr (SendTCPPacket asks right after filling the frame that
+		 * IPOutput -> EthernetOutput took, tcp_out.c:244-326). */
 		{
 			struct gthr *g = ctx ? lookup(ctx) : NULL;
-			struct tx_if *q = (g && nif >= 0 && nif < GPUCSUM_MAX_IFS) ? g->tx[nif] : NULL;
+			struct tx_if *q = g ? g->last_tx : NULL;
 			if (q && q->n)
 				tx_complete(g, q, q->n);
 		}

@@ -3,6 +3,7 @@
  * references weakly (dpdk_module_func, netmap_module_func), exported from the
  * executable (-rdynamic) as they would be from a linked mTCP, and prints the
  * caps gpucsum_set_inner picks for each inner module.  No GPU call is made.
+ * -DWITH_IP_DEFRAG: the DPDK module of an IP_DEFRAG build (RX_ONCE).
  */
 #include <stdio.h>
 
@@ -11,6 +12,10 @@
 
 io_module_func dpdk_module_func;
 io_module_func netmap_module_func;
+#ifdef WITH_IP_DEFRAG
+/* what the integration patch adds to a dpdk_module.c built with IP_DEFRAG */
+const int dpdk_module_ip_defrag = 1;
+#endif
 static io_module_func other_module;
 
 int main(void)

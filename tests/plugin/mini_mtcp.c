@@ -272,6 +272,12 @@ int mini_tx_timed(io_module_func *iom, struct mtcp_thread_context *ctx, int ifid
 	return mini_tx_impl(iom, ctx, ifidx, buf, off, len, n, burst, send_us, burst_us);
 }
 
+/* mTCP's TX ioctls name the route's interface (ifindex: sndvar->nif_out,
+ * tcp_out.c:206, 326) while get_wptr / send_pkts take the configured port's
+ * eidx (CONFIG.nif_to_eidx[nif], eth_out.c:52; core.c:846).  They differ
+ * whenever the configured ports are not 0..n-1; the loop models that. */
+#define MINI_NIF(eidx) ((eidx) + 3)
+
 static int mini_tx_impl(io_module_func *iom, struct mtcp_thread_context *ctx, int ifidx,
                         const uint8_t *buf, const uint64_t *off, const uint16_t *len,
                         uint32_t n, uint32_t burst, double *send_us, double *burst_us)
@@ -297,7 +303,7 @@ static int mini_tx_impl(io_module_func *iom, struct mtcp_thread_context *ctx, in
 		memcpy(f, src, 14 + 4 * ihl);
 		f[24] = f[25] = 0;
 		if (iom->dev_ioctl)                                /* ip_out.c:157-166 */
-			rc = iom->dev_ioctl(ctx, ifidx, src[23] == 6 ? PKT_TX_TCPIP_CSUM_PEEK
+			rc = iom->dev_ioctl(ctx, MINI_NIF(ifidx), src[23] == 6 ? PKT_TX_TCPIP_CSUM_PEEK
 			                                             : PKT_TX_IP_CSUM, f + 14);
 		if (rc == -1) {
 			uint16_t c = ref_ip_fast_csum(f + 14, ihl);  /* ip_out.c:168 */
@@ -311,7 +317,7 @@ static int mini_tx_impl(io_module_func *iom, struct mtcp_thread_context *ctx, in
 			tcph[16] = tcph[17] = 0;
 			rc = -1;
 			if (iom->dev_ioctl)                        /* tcp_out.c:325-327 */
-				rc = iom->dev_ioctl(ctx, ifidx, PKT_TX_TCPIP_CSUM, NULL);
+				rc = iom->dev_ioctl(ctx, MINI_NIF(ifidx), PKT_TX_TCPIP_CSUM, NULL);
 			if (rc == -1) {
 				uint16_t c = ref_tcp_calc_checksum(tcph, (uint16_t)(ip_len - 4 * ihl),
 				                                   ld32(f + 26), ld32(f + 30));

@@ -105,20 +105,25 @@ def test_product_does_not_link_oracle():
     assert not any(s.startswith(("ref_", "refx_", "TCPCalcChecksum")) for s in syms)
 
 
-def test_set_inner_picks_caps_for_mtcp_modules(tmp_path):
+@pytest.mark.parametrize("defrag", [False, True], ids=["dpdk", "dpdk_IP_DEFRAG"])
+def test_set_inner_picks_caps_for_mtcp_modules(tmp_path, defrag):
     """gpucsum_set_inner recognises mTCP's own modules through weak references:
     netmap's get_wptr transmits (TX_EAGER, netmap_module.c:149-160); DPDK frames
     over one MTU frame are ENABLELRO chains (RX_CHAINED, dpdk_module.c:44-48,
-    112-135).  The modules are defined in an -rdynamic executable, as a linked
-    mTCP exports them; no GPU call is made."""
+    112-135); a DPDK module built with IP_DEFRAG (the integration patch defines
+    dpdk_module_ip_defrag there) feeds its reassembly table on every get_rptr
+    call (dpdk_module.c:474-529), so it gets RX_ONCE.  The modules are defined
+    in an -rdynamic executable, as a linked mTCP exports them; no GPU call is
+    made."""
     exe = str(tmp_path / "inner_caps")
-    subprocess.run(["gcc", "-O1", "-rdynamic", "-I", os.path.join(ROOT, "include"),
-                    os.path.join(ROOT, "tests", "plugin", "inner_caps.c"),
+    subprocess.run(["gcc", "-O1", "-rdynamic", "-I", os.path.join(ROOT, "include")] +
+                   (["-DWITH_IP_DEFRAG"] if defrag else []) +
+                   [os.path.join(ROOT, "tests", "plugin", "inner_caps.c"),
                     "-L", os.path.dirname(gpucsum.LIB_PATH), "-lmtcp_gpucsum",
                     "-Wl,-rpath," + os.path.dirname(gpucsum.LIB_PATH), "-o", exe], check=True)
     out = subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()
     got = dict(zip(out[0::2], map(int, out[1::2])))
-    assert got == {"dpdk": 2, "netmap": 1, "other": 0, "set": 2}
+    assert got == {"dpdk": 4 if defrag else 2, "netmap": 1, "other": 0, "set": 2}
 
 
 def test_host_register_rejects_bad_regions():

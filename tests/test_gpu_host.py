@@ -172,13 +172,21 @@ def test_burst_server_yields_to_large_batches(torch_dev):
         np.testing.assert_array_equal(v, O.verify_batch(buf.copy(), off, lens))
 
 
-@pytest.mark.parametrize("server", [False, True])
-def test_registered_rooms_in_place(torch_dev, server):
+@pytest.mark.parametrize("server,start", [(False, None), (True, None), (True, 0x80000002),
+                                          (True, 0xFFFFFFFF - 4)],
+                         ids=["direct", "server", "server_seq_2^31", "server_seq_wrap"])
+def test_registered_rooms_in_place(torch_dev, monkeypatch, server, start):
     """Frames in one registered region (an mbuf pool) are verified and filled
     in place over PCIe -- no gather, no scatter -- with the same results; a
     frame outside the region, or misaligned, sends the batch down the staged
-    path, also exact."""
+    path, also exact.  The server's in-place requests complete on the serving
+    blocks' acks; with the request numbers starting >= 2^31 past 0 or at the
+    32-bit wrap, an ack the ring joined with at 0 would read as newer than the
+    request and complete it before its release: every result must
+    still equal the oracle."""
     import ctypes as C
+    if start is not None:
+        monkeypatch.setenv("GCS_SERVER_SEQ_START", str(start))
     L = gpucsum.lib()
     O = Oracle()
     n = 64
