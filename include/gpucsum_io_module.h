@@ -79,6 +79,23 @@
  * pinned memory (gcs_ctx_set_burst_server), unless the environment sets
  * GPUCSUM_BURST_SERVER=0 (then: one kernel launch per burst).  Up to 16
  * threads per GPU share the grid; a 17th launches per burst.
+ * GPU failures (no CPU fallback: a context that cannot reach its GPU exits at
+ * init_handle as dpdk_module.c:243-247 does).  A failed call after init is
+ * counted in gpu_failures and reported on stderr, and its frames are:
+ *   RX          returned as NULL by get_rptr (rx_errors, rx_unverified) --
+ *               unverified frames never reach ProcessPacket;
+ *   TX in place (dpdk, onvm, psio)  sent by the inner send_pkts as they are:
+ *               the io_module API cannot withdraw a get_wptr buffer, and
+ *               mTCP left both check fields 0 (ip_out.c:153, tcp_out.c:323),
+ *               which the receiver's checks reject (ip_in.c:35, tcp_in.c:1231),
+ *               so TCP retransmits them (tx_unfilled_sent);
+ *   TX_EAGER    (netmap shadow slots) withheld from the inner module
+ *               (tx_unfilled_dropped);
+ *   async fill  a failed post turns fill-as-you-go off for the context and
+ *               send_pkts fills the frames synchronously; a failed wait leaves
+ *               the posted frames unfilled (as above).
+ * GPUCSUM_ON_GPU_FAIL=exit makes any such failure fatal instead (exit, as
+ * init failures are).
  * Threading (core.c:1153-1245): load_module once on the main thread; every
  * other call from the owning mTCP thread.  Per-thread state is keyed by the
  * mtcp_thread_context pointer; mTCP thread k uses GPU k mod n_gpus (override:
@@ -167,6 +184,14 @@ struct gpucsum_stats {
 	uint64_t rx_rptr_changed;/* inner get_rptr changed a frame after its verify   */
 	uint64_t tx_inner_full;  /* TX_EAGER: inner get_wptr had no buffer: frame lost  */
 	uint64_t tx_posts;       /* async TX fill posts (GPUCSUM_TX_GROUP)            */
+	/* GPU failures (gpu_failures counts the failed calls; these the frames):  */
+	uint64_t tx_unfilled_sent;    /* in-place inner: frames the inner sent with the
+	                               * check fields as mTCP left them (0, ip_out.c:153,
+	                               * tcp_out.c:323): the receiver's checks drop them */
+	uint64_t tx_unfilled_dropped; /* TX_EAGER (shadow) inner: frames withheld       */
+	uint64_t rx_unverified;       /* RX frames returned as NULL (and counted in
+	                               * rx_errors) because their burst's verify failed */
+	uint64_t rx_posts;            /* async RX verify posts (GPUCSUM_RX_GROUP)    */
 };
 int gpucsum_get_stats(struct mtcp_thread_context *ctx, struct gpucsum_stats *out);
 

@@ -308,6 +308,18 @@ int gcs_compute_ptrs(gcs_ctx *ctx, uint8_t *const *pkts, const uint16_t *len,
  * gcs_wait(ctx, 0) does nothing. */
 int gcs_compute_ptrs_async(gcs_ctx *ctx, uint8_t *const *pkts, const uint16_t *len,
                            uint32_t n, uint8_t *status, uint32_t *csums, uint64_t *ticket);
+/* Asynchronous RX verify of a host burst (the plugin verifies a burst in
+ * groups as recv_pkts returns, and mTCP's get_rptr(i) waits only for the group
+ * holding frame i, core.c:789-795).  As gcs_compute_ptrs_async: posted to the
+ * burst server when it is on (*ticket != 0), verdict[] written -- and, with
+ * GCS_VF_ZERO_BAD_TCP_CHECK, tcph->check zeroed in bad frames (tcp_in.c:1237)
+ * -- by the gcs_wait that completes it; frames and verdict[] must stay valid
+ * and the frames unmodified until then.  Flags other than
+ * GCS_VF_ZERO_BAD_TCP_CHECK, no server, or more than one request's frames:
+ * verified synchronously, *ticket = 0.  Async fills and verifies share the
+ * context's request ring and complete in posting order. */
+int gcs_verify_ptrs_async(gcs_ctx *ctx, uint8_t *const *pkts, const uint16_t *len,
+                          uint32_t n, uint8_t *verdict, uint32_t flags, uint64_t *ticket);
 int gcs_wait(gcs_ctx *ctx, uint64_t ticket);
 
 /* Host-memory RX verify + RSS steering (see gcs_classify_dev); hash or queue

@@ -20,6 +20,7 @@
 #include <new>
 #include <system_error>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "gcs_internal.h"
@@ -656,6 +657,10 @@ struct gcs_ctx {
     struct AsyncReq {
         bool pending = false;
         bool staged = false;
+        bool compute = true;                // a TX fill, or an RX verify
+        bool cancelled = false;             // a failed wait dropped it: the next wait
+                                            // covering it reports the failure
+        uint32_t flags = 0;                 // verify: GCS_VF_ZERO_BAD_TCP_CHECK (applied by the host)
         uint32_t q = 0, n = 0;
         uint8_t* status = nullptr;          // the caller's outputs (nullable)
         uint32_t* csums = nullptr;
@@ -670,7 +675,14 @@ struct gcs_ctx {
         bool stage_dev = false;             // staging is device memory (hipFree)
     };
     bool async_stage_dev = false;           // GCS_ASYNC_STAGE=device
+    // test-only: GCS_FAULT_INJECT was set (to anything) when the context was
+    // made, so the per-burst entry points look up its value per call; an
+    // unarmed context never reads the environment on the burst path
+    bool faults = false;
     AsyncReq areq[gcs::kServerSlots];
+    // descriptor launches' fallback lists (gcs_internal.h DescFb), one per
+    // stream: launches on one stream run in order, so they may share one
+    std::unordered_map<hipStream_t, gcs::DescFb> fbs;
 
     // Copy work for `count` frames / `bytes` bytes: inline when small, else
     // spread over the gather pool.
@@ -712,6 +724,29 @@ struct DeviceGuard {
 hipStream_t pick_stream(gcs_ctx* ctx, void* stream)
 {
     return stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
+}
+
+// The fallback list for a descriptor launch of n frames on stream s: one per
+// stream of the context, grown (after the stream's earlier launches are done
+// with the old one) when n outgrows it.
+int desc_fb(gcs_ctx* ctx, hipStream_t s, uint32_t n, gcs::DescFb** out)
+{
+    gcs::DescFb& fb = ctx->fbs[s];
+    if (!fb.d || fb.cap_frames < n) {
+        const uint32_t cap = std::max<uint32_t>(n, 1u << 16);
+        if (fb.d) {
+            HIP_TRY(hipStreamSynchronize(s));
+            HIP_TRY(hipFree(fb.d));
+            fb.d = nullptr;
+        }
+        const size_t bytes = gcs::desc_fb_words(cap) * sizeof(uint32_t);
+        HIP_TRY(hipMalloc((void**)&fb.d, bytes));
+        HIP_TRY(hipMemset(fb.d, 0, bytes));
+        fb.cap_frames = cap;
+        fb.epoch = 0;
+    }
+    *out = &fb;
+    return GCS_OK;
 }
 
 void free_slot(Slot& s)
@@ -1106,8 +1141,11 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
             HIP_TRY(gcs::launch_compute_desc_spread(frames_d, used, off_d, len_d, cnt, code_d,
                                                     csum_d, GCS_CF_NO_INPLACE, s.stream));
         } else if (compute) {
+            gcs::DescFb* fb = nullptr;
+            int rc = desc_fb(ctx, s.stream, cnt, &fb);
+            if (rc) return rc;
             HIP_TRY(gcs::launch_compute_desc(frames_d, used, off_d, len_d, cnt, code_d, csum_d,
-                                             GCS_CF_NO_INPLACE, s.stream));
+                                             GCS_CF_NO_INPLACE, fb, s.stream));
             if (!direct)
                 HIP_TRY(hipMemcpyAsync(s.h_csum, s.d_csum, cnt * sizeof(uint32_t),
                                        hipMemcpyDeviceToHost, s.stream));
@@ -1126,8 +1164,11 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
                                                    flags & GCS_VF_ICMP, s.stream));
         } else {
             // the tcp_in.c:1237 side effect is applied on the host copy below
+            gcs::DescFb* fb = nullptr;
+            int rc = desc_fb(ctx, s.stream, cnt, &fb);
+            if (rc) return rc;
             HIP_TRY(gcs::launch_verify_desc(frames_d, used, off_d, len_d, cnt, code_d,
-                                            flags & GCS_VF_ICMP, s.stream));
+                                            flags & GCS_VF_ICMP, fb, s.stream));
         }
         if (!direct)
             HIP_TRY(hipMemcpyAsync(s.h_code, s.d_code, cnt, hipMemcpyDeviceToHost, s.stream));
@@ -1211,6 +1252,7 @@ try {
         ctx->direct_spread = std::atoi(e) != 0;
     if (const char* e = std::getenv("GCS_ASYNC_STAGE"))
         ctx->async_stage_dev = std::strcmp(e, "device") == 0;
+    ctx->faults = std::getenv("GCS_FAULT_INJECT") != nullptr;
     if (const char* e = std::getenv("GCS_BURST_SERVER")) {
         // a context beyond the grid's kHubRings runs without it (GCS_ERANGE)
         if (std::atoi(e) != 0 && (rc = gcs_ctx_set_burst_server(ctx, 1)) != GCS_OK &&
@@ -1249,6 +1291,14 @@ try {
                 (void)hipStreamSynchronize(s.stream);
             free_slot(s);
         }
+        for (auto& kv : ctx->fbs) {
+            // a caller's stream may be gone already: wait for the device instead
+            if (kv.second.d) {
+                (void)hipDeviceSynchronize();
+                (void)hipFree(kv.second.d);
+            }
+        }
+        ctx->fbs.clear();
         if (ctx->stream) {
             (void)hipStreamSynchronize(ctx->stream);
             (void)hipStreamDestroy(ctx->stream);
@@ -1394,8 +1444,12 @@ try {
     if (n == 0)
         return GCS_OK;
     DeviceGuard g(ctx->device);
-    HIP_TRY(gcs::launch_verify_desc(d_frames, frames_bytes, d_off, d_len, n, d_verdict, flags,
-                                    pick_stream(ctx, stream)));
+    const hipStream_t st = pick_stream(ctx, stream);
+    gcs::DescFb* fb = nullptr;
+    int rc = desc_fb(ctx, st, n, &fb);
+    if (rc) return rc;
+    HIP_TRY(gcs::launch_verify_desc(d_frames, frames_bytes, d_off, d_len, n, d_verdict, flags, fb,
+                                    st));
     return GCS_OK;
 } GCS_CATCH
 
@@ -1408,8 +1462,12 @@ try {
     if (n == 0)
         return GCS_OK;
     DeviceGuard g(ctx->device);
+    const hipStream_t st = pick_stream(ctx, stream);
+    gcs::DescFb* fb = nullptr;
+    int rc = desc_fb(ctx, st, n, &fb);
+    if (rc) return rc;
     HIP_TRY(gcs::launch_compute_desc(d_frames, frames_bytes, d_off, d_len, n, d_status, d_csums,
-                                     flags, pick_stream(ctx, stream)));
+                                     flags, fb, st));
     return GCS_OK;
 } GCS_CATCH
 
@@ -1578,6 +1636,8 @@ int gcs_classify_ptrs(gcs_ctx* ctx, uint8_t* const* pkts, const uint16_t* len, u
 try {
     if (!hash && !queue)
         return GCS_EINVAL;
+    if (ctx && ctx->faults && n && fault("verify_ptrs"))   // test-only (plugin RX failure)
+        return hip_fail(hipErrorLaunchFailure, "injected (verify_ptrs)");
     return run_host_batch(ctx, nullptr, nullptr, pkts, len, n, verdict, nullptr, flags, false,
                           hash, queue);
 } GCS_CATCH
@@ -1599,9 +1659,20 @@ namespace {
 constexpr uint64_t kAsyncStageBytes = 256u << 10;   // per server slot
 
 // Finish async request a: its server request is done (results in a.st /
-// a.cs); write the caller's outputs and the frames' check fields.
+// a.cs).  A fill: the caller's statuses / checks and the frames' check fields.
+// A verify: the caller's verdicts, and the tcp_in.c:1237 side effect
+// (GCS_VF_ZERO_BAD_TCP_CHECK) on the frames themselves.
 void async_finish(gcs_ctx::AsyncReq& a)
 {
+    if (!a.compute) {
+        if (a.status)
+            std::memcpy(a.status, a.st.data(), a.n);
+        if (a.flags & GCS_VF_ZERO_BAD_TCP_CHECK)
+            zero_bad_tcp_checks(a.st.data(), a.n,
+                                [&](uint32_t i) -> uint8_t* { return a.ptrs[i]; }, a.lens.data());
+        a.pending = false;
+        return;
+    }
     for (uint32_t i = 0; i < a.n; i++) {
         if (a.status) a.status[i] = a.st[i];
         if (a.csums) a.csums[i] = a.cs[i];
@@ -1615,7 +1686,9 @@ int async_wait(gcs_ctx* ctx, uint32_t q)
 {
     DeviceGuard g(ctx->device);
     if (ctx->server) {
-        int rc = ctx->server->wait(q);
+        // test-only GCS_FAULT_INJECT=wait: the server "gives no answer"
+        int rc = ctx->faults && fault("wait") ? hip_fail(hipErrorLaunchFailure, "injected (wait)")
+                               : ctx->server->wait(q);
         if (rc) {
             // The server did not answer: cancel every pending async fill, so
             // that no later wait writes an old request's checks into buffers
@@ -1626,6 +1699,7 @@ int async_wait(gcs_ctx* ctx, uint32_t q)
             for (auto& a : ctx->areq)
                 if (a.pending) {
                     a.pending = false;
+                    a.cancelled = true;
                     std::fill(a.ptrs.begin(), a.ptrs.end(), nullptr);
                     a.status = nullptr;
                     a.csums = nullptr;
@@ -1633,24 +1707,44 @@ int async_wait(gcs_ctx* ctx, uint32_t q)
             return rc;
         }
     }
-    for (auto& a : ctx->areq)
+    // A request a failed wait cancelled stays "lost" for every later wait
+    // covering it until its slot is reused: fills and verifies share the ring,
+    // so each of their waiters learns that a request it may own was dropped.
+    bool lost = false;
+    for (auto& a : ctx->areq) {
+        if (a.cancelled && (int32_t)(q - a.q) >= 0)
+            lost = true;
         if (a.pending && (int32_t)(q - a.q) >= 0)
             async_finish(a);
+    }
+    if (lost) {
+        std::snprintf(g_hip_err, sizeof g_hip_err,
+                      "async request cancelled by an earlier failed wait");
+        return GCS_EHIP;
+    }
     return GCS_OK;
 }
 
 }  // namespace
 
-int gcs_compute_ptrs_async(gcs_ctx* ctx, uint8_t* const* pkts, const uint16_t* len, uint32_t n,
-                           uint8_t* status, uint32_t* csums, uint64_t* ticket)
-try {
-    if (!ctx || !ticket || (n && (!pkts || !len)))
-        return GCS_EINVAL;
-    *ticket = 0;
-    if (n == 0)
-        return GCS_OK;
-    if (!ctx->server || n > (uint32_t)gcs::kSlotFrames)
-        return run_host_batch(ctx, nullptr, nullptr, pkts, len, n, status, csums, 0u, true);
+namespace {
+
+// One async request on the context's burst server: a TX fill (compute) or an
+// RX verify.  Frames all in one registered region at 16 B-aligned addresses
+// are read where they are; others are staged in the request slot's pinned
+// (or, GCS_ASYNC_STAGE=device, device) staging.  *ticket = 0 when the batch
+// could not be posted and ran synchronously instead.
+int post_async(gcs_ctx* ctx, uint8_t* const* pkts, const uint16_t* len, uint32_t n, bool compute,
+               uint32_t flags, uint8_t* out8, uint32_t* csums, uint64_t* ticket)
+{
+    auto sync = [&]() {
+        return compute ? run_host_batch(ctx, nullptr, nullptr, pkts, len, n, out8, csums, 0u, true)
+                       : run_host_batch(ctx, nullptr, nullptr, pkts, len, n, out8, nullptr, flags,
+                                        false);
+    };
+    if (!ctx->server || n > (uint32_t)gcs::kSlotFrames ||
+        (!compute && (flags & ~(uint32_t)GCS_VF_ZERO_BAD_TCP_CHECK)))
+        return sync();
     DeviceGuard g(ctx->device);
     // in place: every frame inside one registered region, 16 B-aligned
     RegRegion reg{};
@@ -1667,13 +1761,14 @@ try {
                       ((uintptr_t)p & 15) == 0;
     }
     if (!inplace && staged > kAsyncStageBytes)
-        return run_host_batch(ctx, nullptr, nullptr, pkts, len, n, status, csums, 0u, true);
+        return sync();
     const uint32_t q = gcs::server_next(ctx->server->posted());
     gcs_ctx::AsyncReq& a = ctx->areq[q % gcs::kServerSlots];
-    if (a.pending) {                     // the slot's previous async fill: finish it first
+    if (a.pending) {                     // the slot's previous async request: finish it first
         int rc = async_wait(ctx, a.q);
         if (rc) return rc;
     }
+    a.cancelled = false;                 // nobody waited for that one: the slot is reused
     if (a.st.size() < (size_t)gcs::kSlotFrames) {
         a.ptrs.resize(gcs::kSlotFrames);
         a.lens.resize(gcs::kSlotFrames);
@@ -1727,23 +1822,54 @@ try {
         a.lens[i] = len[i];
     }
     a.n = n;
-    a.status = status;
+    a.compute = compute;
+    a.flags = flags;
+    a.status = out8;
     a.csums = csums;
-    // The kernel never writes the frames: it returns the checks in the
-    // records and gcs_wait writes them into the frames from the host.  For
-    // frames in a registered region that saves the kernel's 64 B sector
-    // writes over PCIe and the release + ack round trip an in-place
-    // completion waits for (64 x 1500 B, tools/tx_async_probe.py: send_pkts
-    // blocked 9.2 us in place vs ~6 us with host-side checks).
+    // The kernel never writes the frames: a fill returns the checks in the
+    // records and gcs_wait writes them into the frames from the host; a
+    // verify's tcp_in.c:1237 side effect is applied there too.  For frames in
+    // a registered region that saves the kernel's writes over PCIe and the
+    // release + ack round trip an in-place completion waits for (64 x 1500 B,
+    // tools/tx_async_probe.py: send_pkts blocked 9.2 us in place vs ~6 us with
+    // host-side checks).
     uint32_t got = 0;
-    int rc = ctx->server->post(frames_d, bytes, a.off.data(), a.dlen.data(), n, true,
-                               GCS_CF_NO_INPLACE, a.st.data(), a.cs.data(),
-                               /*in_place=*/false, &got);
+    int rc = ctx->server->post(frames_d, bytes, a.off.data(), a.dlen.data(), n, compute,
+                               compute ? (uint32_t)GCS_CF_NO_INPLACE : 0u, a.st.data(),
+                               compute ? a.cs.data() : nullptr, /*in_place=*/false, &got);
     if (rc) return rc;
     a.q = got;
     a.pending = true;
     *ticket = got;
     return GCS_OK;
+}
+
+}  // namespace
+
+int gcs_compute_ptrs_async(gcs_ctx* ctx, uint8_t* const* pkts, const uint16_t* len, uint32_t n,
+                           uint8_t* status, uint32_t* csums, uint64_t* ticket)
+try {
+    if (!ctx || !ticket || (n && (!pkts || !len)))
+        return GCS_EINVAL;
+    *ticket = 0;
+    if (n == 0)
+        return GCS_OK;
+    if (ctx->faults && fault("compute_async"))   // test-only (plugin async-post failure)
+        return hip_fail(hipErrorLaunchFailure, "injected (compute_async)");
+    return post_async(ctx, pkts, len, n, true, 0u, status, csums, ticket);
+} GCS_CATCH
+
+int gcs_verify_ptrs_async(gcs_ctx* ctx, uint8_t* const* pkts, const uint16_t* len, uint32_t n,
+                          uint8_t* verdict, uint32_t flags, uint64_t* ticket)
+try {
+    if (!ctx || !ticket || (n && (!pkts || !len || !verdict)))
+        return GCS_EINVAL;
+    *ticket = 0;
+    if (n == 0)
+        return GCS_OK;
+    if (ctx->faults && (fault("verify_async") || fault("verify_ptrs")))   // test-only
+        return hip_fail(hipErrorLaunchFailure, "injected (verify_async)");
+    return post_async(ctx, pkts, len, n, false, flags, verdict, nullptr, ticket);
 } GCS_CATCH
 
 int gcs_wait(gcs_ctx* ctx, uint64_t ticket)
@@ -1758,12 +1884,16 @@ try {
 int gcs_verify_ptrs(gcs_ctx* ctx, uint8_t* const* pkts, const uint16_t* len, uint32_t n,
                     uint8_t* verdict, uint32_t flags)
 try {
+    if (ctx && ctx->faults && n && fault("verify_ptrs"))   // test-only (plugin RX failure)
+        return hip_fail(hipErrorLaunchFailure, "injected (verify_ptrs)");
     return run_host_batch(ctx, nullptr, nullptr, pkts, len, n, verdict, nullptr, flags, false);
 } GCS_CATCH
 
 int gcs_compute_ptrs(gcs_ctx* ctx, uint8_t* const* pkts, const uint16_t* len, uint32_t n,
                      uint8_t* status, uint32_t* csums)
 try {
+    if (ctx && ctx->faults && n && fault("compute_ptrs"))  // test-only (plugin TX failure)
+        return hip_fail(hipErrorLaunchFailure, "injected (compute_ptrs)");
     return run_host_batch(ctx, nullptr, nullptr, pkts, len, n, status, csums, 0u, true);
 } GCS_CATCH
 

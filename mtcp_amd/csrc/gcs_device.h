@@ -735,9 +735,6 @@ __device__ __forceinline__ void epilogue(const Hdr& h, Acc a, uint8_t* __restric
 // first batch is kept for the TX write-back).  `active` = false: a padding
 // group of a block-uniform loop -- it loads nothing and writes nothing but
 // still takes part in the wave's cross-lane steps.
-#ifndef GCS_FIRST_LINE_TEMPORAL
-#define GCS_FIRST_LINE_TEMPORAL 0   // A/B switch (tools/kbench.hip): chunks 0..7 without NT
-#endif
 template <int G, int U, bool SAFE, bool NT>
 __device__ __forceinline__ void load_first(const uint8_t* __restrict__ f, int nchunks,
                                            int64_t avail, int sub, uint4 (&v)[U])
@@ -745,12 +742,8 @@ __device__ __forceinline__ void load_first(const uint8_t* __restrict__ f, int nc
 #pragma unroll
     for (int j = 0; j < U; j++) {
         int c = j * G + sub;
-        if (GCS_FIRST_LINE_TEMPORAL && NT && j * G < 8 && c < 8)
-            v[j] = c < nchunks ? load_chunk<SAFE, false>(f + 16 * c, avail - 16 * c)
-                               : make_uint4(0, 0, 0, 0);
-        else
-            v[j] = c < nchunks ? load_chunk<SAFE, NT>(f + 16 * c, avail - 16 * c)
-                               : make_uint4(0, 0, 0, 0);
+        v[j] = c < nchunks ? load_chunk<SAFE, NT>(f + 16 * c, avail - 16 * c)
+                           : make_uint4(0, 0, 0, 0);
     }
 }
 

@@ -469,12 +469,9 @@ hipError_t launch_burst_server(HubMailbox* mb, HubPub* pub, int groups, uint64_t
 // keeps K = 1 (profiles/r02/kbench_imix_K.log; other class shapes:
 // kbench_imix_shapes2.log).
 template <int G0_, int U0_, int G1_, int U1_, int G2_, int U2_, int WM_ = kWM, int F_ = kBlock,
-          bool ORDERED_ = true, int K0_ = 1, int K1_ = 1, bool STAGE_ = false, bool NT_ = kNT,
-          int RELOAD_ = 0, int PROBE_ = 0>
+          bool ORDERED_ = true, int K0_ = 1, int K1_ = 1, bool STAGE_ = false, bool NT_ = kNT>
 struct DescShape {
     static constexpr bool NT = NT_;
-    static constexpr int PROBE = PROBE_;     // A/B (kbench): 1 = the list passes' loads only, no fold
-    static constexpr int RELOAD = RELOAD_;   // A/B: re-read each staged sector before its store
     static constexpr int G0 = G0_, U0 = U0_, G1 = G1_, U1 = U1_, G2 = G2_, U2 = U2_, WM = WM_;
     static constexpr int F = F_;
     static constexpr bool ORDERED = ORDERED_;
@@ -497,7 +494,7 @@ using DescShip = DescShape<4, 1, 16, 3, 32, 3, COMPUTE ? WM_SECTOR_NT : kWM, kBl
                            COMPUTE, !COMPUTE>;
 
 template <int G, int U, bool COMPUTE, bool LOOP, bool EXT, int WM, int K = 1, bool NT = kNT,
-          int PROBE = 0, int NTH = kBlock>
+          int NTH = kBlock>
 __device__ __forceinline__ void desc_class(uint8_t* __restrict__ frames, uint64_t frames_bytes,
                                            const uint64_t* soff, const uint16_t* slen,
                                            const uint16_t* list, int count, u32 flags,
@@ -525,18 +522,6 @@ __device__ __forceinline__ void desc_class(uint8_t* __restrict__ frames, uint64_
             const uint64_t o = soff[t];                  // LDS: no dependent global load
             const int nch = active ? (int)((slen[t] + 15u) >> 4) : 0;
             load_first<G, U, true, NT>(frames + o, nch, (int64_t)(frames_bytes - o), sub, v[k]);
-        }
-        if constexpr (PROBE == 1) {
-            // loads only: keep them alive through a test that never holds
-            u32 x = 0;
-#pragma unroll
-            for (int k = 0; k < K; k++)
-#pragma unroll
-                for (int j = 0; j < U; j++)
-                    x ^= v[k][j].x ^ v[k][j].y ^ v[k][j].z ^ v[k][j].w;
-            if (x == 0x9E3779B9u && tk[0] >= 0)
-                codes[tk[0]] = 0xEE;
-            continue;
         }
 #pragma unroll
         for (int k = 0; k < K; k++) {
@@ -589,15 +574,6 @@ __device__ __forceinline__ void desc_tail(uint8_t* __restrict__ frames, uint64_t
             ob[r] = soff[ft] + 16 * c;
             go[r] = ob[r] + 16 <= frames_bytes;
         }
-        if constexpr (S::RELOAD != 0) {
-            // A/B probe: bring each sector's line into L2 right before its store
-            u32 keep = 0;
-#pragma unroll
-            for (int r = 0; r < NR; r++)
-                if (go[r])
-                    keep ^= ldg16<S::RELOAD == 2>(frames + ob[r]).x;
-            asm volatile("" : : "v"(keep));
-        }
 #pragma unroll
         for (int r = 0; r < NR; r++)
             if (go[r])
@@ -622,13 +598,13 @@ __device__ __forceinline__ void desc_tail(uint8_t* __restrict__ frames, uint64_t
     }
 }
 
-template <class S, bool COMPUTE, bool XCD, bool EXT>
+template <class S, bool COMPUTE, bool EXT>
 __device__ __forceinline__ void desc_mixed(uint8_t* __restrict__ frames, uint64_t frames_bytes,
                                            const uint64_t* __restrict__ off,
                                            const uint16_t* __restrict__ lens, u32 n,
                                            uint8_t* __restrict__ out_code,
                                            uint32_t* __restrict__ out_csum, u32 flags,
-                                           const Ext& ext)
+                                           const Ext& ext, uint32_t blk)
 {
     constexpr int F = S::F;
     __shared__ uint64_t soff[F];
@@ -642,7 +618,6 @@ __device__ __forceinline__ void desc_mixed(uint8_t* __restrict__ frames, uint64_
     __shared__ uint32_t hashes[EXT && !COMPUTE ? F : 1];
     __shared__ uint16_t queues[EXT && !COMPUTE ? F : 1];
     __shared__ uint4 stage[COMPUTE && S::STAGE ? 4 * F : 1];   // sector 0 of each frame
-    const uint32_t blk = XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
     const uint64_t f0 = (uint64_t)blk * F;
     const int t = threadIdx.x;
     if (t < 3)
@@ -717,9 +692,9 @@ __device__ __forceinline__ void desc_mixed(uint8_t* __restrict__ frames, uint64_
         uint32_t* hl = EXT && !COMPUTE ? hashes : nullptr;
         uint16_t* ql = EXT && !COMPUTE ? queues : nullptr;
         uint4* stg = COMPUTE && S::STAGE ? stage : nullptr;
-        if (n0) desc_class<S::G0, S::U0, COMPUTE, false, EXT, S::WM, S::K0, S::NT, S::PROBE>(frames, frames_bytes, soff, slen, list[0], n0, flags, codes, csums, ext, hl, ql, stg);
-        if (n1) desc_class<S::G1, S::U1, COMPUTE, false, EXT, S::WM, S::K1, S::NT, S::PROBE>(frames, frames_bytes, soff, slen, list[1], n1, flags, codes, csums, ext, hl, ql, stg);
-        if (n2) desc_class<S::G2, S::U2, COMPUTE, true, EXT, S::WM, 1, S::NT, S::PROBE>(frames, frames_bytes, soff, slen, list[2], n2, flags, codes, csums, ext, hl, ql, stg);
+        if (n0) desc_class<S::G0, S::U0, COMPUTE, false, EXT, S::WM, S::K0, S::NT>(frames, frames_bytes, soff, slen, list[0], n0, flags, codes, csums, ext, hl, ql, stg);
+        if (n1) desc_class<S::G1, S::U1, COMPUTE, false, EXT, S::WM, S::K1, S::NT>(frames, frames_bytes, soff, slen, list[1], n1, flags, codes, csums, ext, hl, ql, stg);
+        if (n2) desc_class<S::G2, S::U2, COMPUTE, true, EXT, S::WM, 1, S::NT>(frames, frames_bytes, soff, slen, list[2], n2, flags, codes, csums, ext, hl, ql, stg);
     }
     __syncthreads();
     desc_tail<S, COMPUTE, EXT>(frames, frames_bytes, f0, n, soff, slen, codes, csums, hashes, queues,
@@ -732,8 +707,8 @@ k_desc_mixed(uint8_t* __restrict__ frames, uint64_t frames_bytes,
              const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens, u32 n,
              uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags)
 {
-    desc_mixed<S, COMPUTE, XCD, false>(frames, frames_bytes, off, lens, n, out_code, out_csum,
-                                       flags, Ext{});
+    desc_mixed<S, COMPUTE, false>(frames, frames_bytes, off, lens, n, out_code, out_csum, flags,
+                                  Ext{}, XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x);
 }
 
 template <class S, bool COMPUTE, bool XCD, int OCC = 1>
@@ -743,8 +718,8 @@ k_desc_mixed_x(uint8_t* __restrict__ frames, uint64_t frames_bytes,
                uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags,
                Ext ext)
 {
-    desc_mixed<S, COMPUTE, XCD, true>(frames, frames_bytes, off, lens, n, out_code, out_csum,
-                                      flags, ext);
+    desc_mixed<S, COMPUTE, true>(frames, frames_bytes, off, lens, n, out_code, out_csum, flags,
+                                 ext, XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -757,92 +732,92 @@ k_desc_mixed_x(uint8_t* __restrict__ frames, uint64_t frames_bytes,
 // streams (one per wave, 1 KiB per load instruction, no per-frame group
 // shapes, no class passes): each lane folds its chunk to one word sum, a DPP
 // wave scan turns the sums into chunk prefixes, and the lanes holding a
-// frame's first chunks or last chunk park what the per-frame step needs in
-// LDS -- chunks 0..3 (the headers, and for TX the sector that is written
-// back), the prefix at the frame's first chunk, and Q at the frame's end.
-// Then one lane per frame parses its headers from LDS, folds chunks 0..3 with
-// the list kernels' exact masks (accum_chunk) and adds the words [64, te) as
-// Q(te) - Q(64), then runs the shared epilogue (verdict, or fill into the
-// staged sector).  Per-frame results are identical as integers to the group
-// kernels' (the same words, the same u32 sums).
+// frame's first chunks or its chunk NH or its last chunk park what the
+// per-frame step needs in LDS -- chunks 0..NH-1 (the headers; for TX the
+// sector that is written back) and Q(len) - Q(16 NH), the frame's words past
+// the stash, accumulated by two LDS adds.  Then one lane per frame parses its
+// headers from LDS, folds the stashed chunks with the group kernels' exact
+// masks and adds the words [16 NH, te) from the stash-less tail, then runs
+// the shared epilogue (verdict, or fill into the staged sector).  Per-frame
+// results are identical as integers to the group kernels' (the same words,
+// the same u32 sums).
 //
-// Fast frames: ihl <= 8 (IP header, doff byte and tcph->check inside chunks
-// 0..3) and te <= 64 or te == len (the segment ends at the frame's end, as
-// every frame mTCP builds).  Other frames of the block go to one list pass on
-// 32 x 3 lanes (desc_class, as desc_mixed's class 2).  A block streams only
-// when its frames are valid, non-empty, in offset order, chunk-disjoint with
-// gaps <= 64 B, and the region (<= RMAX chunks) ends inside the buffer;
-// otherwise it runs desc_mixed's three class passes.  Reference layout:
-// PSIO's packed chunk (pslib.c:132-156, ps.h:181-213).
-template <int U_, int RMAX_, int OCC_, bool PIPE_ = false, int PROBE_ = 0, bool HDR3_ = false>
+// A block streams when its frames are valid, non-empty, in offset order,
+// chunk-disjoint with gaps <= 64 B, the region (<= RMAX chunks) ends inside
+// the buffer, and every frame is "fast": ihl <= 8 (TX, NH = 4: IP header,
+// doff byte and tcph->check inside chunks 0..3) or ihl == 5 (RX, NH = 3), and
+// te <= 16 NH or te == len (the segment ends at the frame's end, as every
+// frame mTCP builds).  Any other block writes nothing, puts its id on the
+// launch's fallback list and leaves; k_desc_fallback then runs desc_mixed's
+// three class passes over it.  Keeping those passes (and their 80 VGPRs) out
+// of this kernel is what lets it run 8 waves per SIMD (round 4; before: 6
+// waves for the fill, 7 for the verify, with the passes inside).  Reference
+// layout: PSIO's packed chunk (pslib.c:132-156, ps.h:181-213).
+template <int U_, int RMAX_, int OCC_, int NH_>
 struct StreamShape {
-    static constexpr bool HDR3 = HDR3_;   // RX: stash chunks 0..2 only (ihl = 5 fast frames)
     static constexpr int U = U_;          // chunks per lane per trip (64 * U per wave)
     static constexpr int RMAX = RMAX_;    // region chunks a streaming block may span
-    static constexpr int OCC = OCC_;
-    static constexpr bool PIPE = PIPE_;   // issue trip k+1's loads before folding trip k
-    static constexpr int PROBE = PROBE_;  // A/B (kbench): 1 = phase 2 loads only, 2 = no phase 3
+    static constexpr int OCC = OCC_;      // waves per SIMD asked of the compiler
+    static constexpr int NH = NH_;        // header chunks stashed per frame
     static_assert(RMAX % 64 == 0 && RMAX <= 65536, "start chunks fit 16 bits");
+    static_assert(NH == 3 || NH == 4, "stash: chunks 0..2 (RX, ihl = 5) or 0..3 (TX sector)");
 };
 
-template <class S, class T, bool COMPUTE, bool XCD>
-__device__ __forceinline__ void desc_stream(uint8_t* __restrict__ frames, uint64_t frames_bytes,
-                                            const uint64_t* __restrict__ off,
-                                            const uint16_t* __restrict__ lens, u32 n,
-                                            uint8_t* __restrict__ out_code,
-                                            uint32_t* __restrict__ out_csum, u32 flags)
+// A block of a descriptor launch that k_desc_stream does not stream goes on
+// the launch's fallback list (gcs_internal.h DescFb): the head is epoch << 32
+// | blocks listed, and the first push of a launch restarts an older epoch's
+// count at 0 -- no launch ever clears the list.
+__device__ __forceinline__ void fb_push(uint32_t* fb, uint32_t epoch, uint32_t blk)
 {
-    static_assert(S::F == kBlock && S::R == 1, "one descriptor per thread");
-    static_assert(!COMPUTE || S::STAGE, "TX stages sector 0 in hdr");
-    constexpr int F = kBlock, NW = kBlock / 64, RW = T::RMAX / 64, U = T::U;
-    constexpr int NH = (!COMPUTE && T::HDR3) ? 3 : 4;   // header chunks stashed per frame
-    __shared__ uint64_t soff[F];
-    __shared__ uint16_t slen[F];
-    __shared__ uint16_t list[3][F];
-    __shared__ int cnt[3];
-    __shared__ int wcnt[3][NW];
-    __shared__ uint8_t codes[F];
-    __shared__ uint32_t csums[COMPUTE ? F : 1];
-    __shared__ uint4 hdr[NH * F];      // chunks 0..NH-1 per frame; TX: the staged sector 0
-    __shared__ uint64_t bm[RW];        // bit c: a frame starts at region chunk c
-    __shared__ uint16_t rbase[RW];     // frames starting before chunk 64 * w
-    __shared__ u32 meta[F];            // start chunk << 16 | len
-    __shared__ u32 pfirst[F];          // wave-local prefix at the first chunk
-    __shared__ u32 qend[F];            // wave-local Q(len)
+    unsigned long long* head = reinterpret_cast<unsigned long long*>(fb);
+    unsigned long long v = __hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+        const unsigned long long want =
+            (uint32_t)(v >> 32) == epoch ? v + 1 : ((unsigned long long)epoch << 32) | 1ull;
+        if (__hip_atomic_compare_exchange_strong(head, &v, want, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            break;                             // v: the head it replaced
+    }
+    fb[kFbHead + ((uint32_t)(v >> 32) == epoch ? (uint32_t)v : 0u)] = blk;
+}
+
+template <class T, bool COMPUTE, int WM, bool XCD>
+__global__ void __launch_bounds__(kBlock, T::OCC)
+k_desc_stream(uint8_t* __restrict__ frames, uint64_t frames_bytes,
+              const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens, u32 n,
+              uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags,
+              uint32_t* __restrict__ fb, u32 epoch)
+{
+    constexpr int F = kBlock, NW = kBlock / 64, RW = T::RMAX / 64, U = T::U, NH = T::NH;
+    constexpr int HB = 16 * NH;            // header bytes stashed per frame
+    static_assert(!COMPUTE || NH == 4, "TX stages sector 0 (chunks 0..3) in hdr");
+    __shared__ uint4 hdr[NH * F];          // chunks 0..NH-1 per frame; TX: the staged sector 0
+    __shared__ u32 meta[F];                // start chunk << 16 | len
+    __shared__ u32 tail[F];                // wave-local Q(len) - Q(HB): words [HB, len)
+    __shared__ uint64_t bm[RW];            // bit c: a frame starts at region chunk c
+    __shared__ uint16_t rbase[RW];         // frames starting before chunk 64 * row
     __shared__ u32 wtot[NW];
+    __shared__ uint8_t codes[F];           // TX statuses (the write-back's test); RX spare
     __shared__ u32 nchunks_s;
 
     const uint32_t blk = XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
     const uint64_t f0 = (uint64_t)blk * F;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int nf = (int)((n - f0) < (uint64_t)F ? (n - f0) : (uint64_t)F);
-    if (t < 3)
-        cnt[t] = 0;
 
-    // phase 0: validate, classify (for the list passes), test streamability
-    int cls = -1;
+    // phase 0: validate; streamability, and each frame's place in the region
+    // (chunks from frame 0's start): its first chunk and the next frame's
     uint64_t o = 0;
-    u32 len = 0;
+    u32 len = 0, start = 0;
+    bool sok = true;
     if (t < nf) {
         o = off[f0 + t];
         len = lens[f0 + t];
-        const bool ok = (o & 15) == 0 && o <= frames_bytes && len <= frames_bytes - o;
-        if (!ok) {
-            codes[t] = COMPUTE ? GCS_TX_BAD_DESC : GCS_V_BAD_DESC;
-            if (COMPUTE)
-                csums[t] = 0;
-        } else {
-            soff[t] = o;
-            slen[t] = (uint16_t)len;
-            cls = len <= (u32)S::T0 ? 0 : (len <= (u32)S::T1 ? 1 : 2);
-        }
+        sok = (o & 15) == 0 && o <= frames_bytes && len <= frames_bytes - o && len > 0;
     }
     const u32 nch = (len + 15) >> 4;
-    // streamability, and each frame's place in the region (chunks from frame
-    // 0's start): its first chunk and the next frame's (the last frame: NCH)
     const uint64_t r0 = off[f0];
-    u32 start = 0, snext = 0;
-    bool sok = t >= nf || (cls >= 0 && len > 0);
+    u32 snext = 0;
     if (sok && t < nf) {
         if (o < r0 || ((o - r0) >> 4) + nch > (uint64_t)T::RMAX) {
             sok = false;
@@ -861,43 +836,10 @@ __device__ __forceinline__ void desc_stream(uint8_t* __restrict__ frames, uint64
     }
     for (int r = t; r < RW; r += kBlock)
         bm[r] = 0;
-    // the three ordered class lists (desc_mixed's phase 0, R = 1)
-    {
-        const uint64_t below = (1ull << lane) - 1;
-        int rank = 0;
-#pragma unroll
-        for (int c = 0; c < 3; c++) {
-            const uint64_t m = __ballot(cls == c);
-            if (lane == 0)
-                wcnt[c][w] = __popcll(m);
-            if (cls == c)
-                rank = __popcll(m & below);
-        }
-        const bool stream = __syncthreads_and(sok);
-        if (!stream) {
-            if (cls >= 0) {
-                int base = 0;
-                for (int k = 0; k < w; k++)
-                    base += wcnt[cls][k];
-                list[cls][base + rank] = (uint16_t)t;
-            }
-            if (t < 3) {
-                int tot = 0;
-                for (int k = 0; k < NW; k++)
-                    tot += wcnt[t][k];
-                cnt[t] = tot;
-            }
-            __syncthreads();
-            const int n0 = cnt[0], n1 = cnt[1], n2 = cnt[2];
-            uint4* stg = COMPUTE ? hdr : nullptr;
-            if (n0) desc_class<S::G0, S::U0, COMPUTE, false, false, S::WM, S::K0, S::NT>(frames, frames_bytes, soff, slen, list[0], n0, flags, codes, csums, Ext{}, nullptr, nullptr, stg);
-            if (n1) desc_class<S::G1, S::U1, COMPUTE, false, false, S::WM, S::K1, S::NT>(frames, frames_bytes, soff, slen, list[1], n1, flags, codes, csums, Ext{}, nullptr, nullptr, stg);
-            if (n2) desc_class<S::G2, S::U2, COMPUTE, true, false, S::WM, 1, S::NT>(frames, frames_bytes, soff, slen, list[2], n2, flags, codes, csums, Ext{}, nullptr, nullptr, stg);
-            __syncthreads();
-            desc_tail<S, COMPUTE, false>(frames, frames_bytes, f0, n, soff, slen, codes, csums,
-                                         nullptr, nullptr, hdr, out_code, out_csum, flags, Ext{});
-            return;
-        }
+    if (!__syncthreads_and(sok)) {
+        if (t == 0)
+            fb_push(fb, epoch, blk);
+        return;                            // block-uniform: nothing written
     }
 
     // phase 1: the region's first-chunk bitmap, per-frame metadata, and per
@@ -906,6 +848,7 @@ __device__ __forceinline__ void desc_stream(uint8_t* __restrict__ frames, uint64
     const u32 NCH = nchunks_s, NR = (NCH + 63) >> 6;
     if (t < nf) {
         meta[t] = start << 16 | len;
+        tail[t] = 0;
 #pragma unroll
         for (int k = 0; k < NH; k++)
             if ((u32)k >= nch)
@@ -920,26 +863,17 @@ __device__ __forceinline__ void desc_stream(uint8_t* __restrict__ frames, uint64
     __syncthreads();
 
     // phase 2: wave w streams chunks [w*QW, (w+1)*QW) of the region
+    const u32 QW = ((NCH + 4 * 64 - 1) / (4 * 64)) * 64;
     {
-        const u32 QW = ((NCH + 4 * 64 - 1) / (4 * 64)) * 64;
         const u32 lo = w * QW, hi = (lo + QW < NCH) ? lo + QW : NCH;
         const uint8_t* reg = frames + r0;
         u32 run = 0;
-        auto load_trip = [&](u32 base, uint4 (&v)[U]) {
+        for (u32 base = lo; base < hi; base += 64 * U) {
+            uint4 v[U];
 #pragma unroll
             for (int j = 0; j < U; j++) {
                 const u32 c = base + 64 * j + lane;
-                v[j] = c < hi ? ldg16<S::NT>(reg + 16ull * c) : make_uint4(0, 0, 0, 0);
-            }
-        };
-        auto fold_trip = [&](u32 base, const uint4 (&v)[U]) {
-            if constexpr (T::PROBE == 1) {
-                u32 x = 0;
-#pragma unroll
-                for (int j = 0; j < U; j++)
-                    x ^= v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
-                run += x;
-                return;
+                v[j] = c < hi ? ldg16<true>(reg + 16ull * c) : make_uint4(0, 0, 0, 0);
             }
 #pragma unroll
             for (int j = 0; j < U; j++) {
@@ -947,9 +881,9 @@ __device__ __forceinline__ void desc_stream(uint8_t* __restrict__ frames, uint64
                 if (64 * row >= hi)           // wave-uniform
                     break;
                 const u32 c = 64 * row + lane;
-                const u32 s = hsum4(v[j]);
-                const u32 incl = wave_incl_scan(s);
-                const u32 excl = run + incl - s;
+                const u32 s4 = hsum4(v[j]);
+                const u32 incl = wave_incl_scan(s4);
+                const u32 excl = run + incl - s4;
                 run += (u32)__builtin_amdgcn_readlane((int)incl, 63);
                 const uint64_t bits = bm[row];
                 const u32 below = __builtin_amdgcn_mbcnt_hi((u32)(bits >> 32),
@@ -960,31 +894,16 @@ __device__ __forceinline__ void desc_stream(uint8_t* __restrict__ frames, uint64
                     const u32 k = c - (m >> 16), fn = (fl + 15) >> 4;
                     if (k < (u32)NH && k < fn)
                         hdr[NH * f + k] = v[j];
-                    if (k == 0)
-                        pfirst[f] = excl;
-                    if (k + 1 == fn)
-                        qend[f] = excl + chunk_prefix_sum(v[j], (int)(fl - 16 * k));
+                    if (fn > (u32)NH) {       // words [HB, len): Q(len) - Q(HB)
+                        if (k == (u32)NH)
+                            __hip_atomic_fetch_add(&tail[f], 0u - excl, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+                        if (k + 1 == fn)
+                            __hip_atomic_fetch_add(&tail[f],
+                                                   excl + chunk_prefix_sum(v[j], (int)(fl - 16 * k)),
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
                 }
-            }
-        };
-        if constexpr (T::PIPE) {
-            uint4 v[U], vn[U];
-            if (lo < hi)
-                load_trip(lo, v);
-            for (u32 base = lo; base < hi; base += 64 * U) {
-                const u32 nb = base + 64 * U;
-                if (nb < hi)
-                    load_trip(nb, vn);
-                fold_trip(base, v);
-#pragma unroll
-                for (int j = 0; j < U; j++)
-                    v[j] = vn[j];
-            }
-        } else {
-            for (u32 base = lo; base < hi; base += 64 * U) {
-                uint4 v[U];
-                load_trip(base, v);
-                fold_trip(base, v);
             }
         }
         if (lane == 0)
@@ -992,101 +911,123 @@ __device__ __forceinline__ void desc_stream(uint8_t* __restrict__ frames, uint64
     }
     __syncthreads();
 
-    if constexpr (T::PROBE != 0) {
-        if (t == 0 && wtot[0] == 0x9E3779B9u)
-            out_code[f0] = 0xEE;              // keeps the probe's loads alive
-        if constexpr (T::PROBE == 2)
-            return;
-    }
     // phase 3: one lane per frame
-    {
-        const u32 QW = ((NCH + 4 * 64 - 1) / (4 * 64)) * 64;
-        const int tf = t < nf ? t : 0;
-        const uint4 h4[4] = {hdr[NH * tf], hdr[NH * tf + 1], hdr[NH * tf + 2],
-                             NH == 4 ? hdr[NH * tf + 3] : make_uint4(0, 0, 0, 0)};
-        Hdr h;
-        h.d3 = h4[0].w;
-        h.d4 = h4[1].x;
-        h.d5 = h4[1].y;
-        const int ihl = (int)((h.d3 >> 16) & 15u);
-        const int ts = 14 + 4 * ihl;
-        const int te = 14 + (int)bswap16(h.d4 & 0xFFFFu);
-        // NH = 3 (RX): chunk 3 is not stashed; words [48, te) come from the
-        // prefixes, and doff (byte ts + 12) must lie in chunk 2: ihl == 5
-        constexpr int HB = 16 * NH;                  // header bytes held per frame
-        const bool fast = t < nf && (NH == 4 ? ihl <= 8 : ihl == 5) &&
-                          (te <= HB || te == (int)len);
-        // wave-uniform: every fast frame of the wave has ihl == 5, so the word
-        // masks of the stashed chunks are constants (masks5, as the group
-        // kernels); and when every one also has te >= HB, no segment end lies
-        // in them
-        const bool all5 = __all(!fast || ihl == 5);
-        const bool end64 = __all(!fast || te >= HB);
-        // RX: fast frames' verdicts go straight out (coalesced, frame order)
-        uint8_t* oc = (!COMPUTE && out_code) ? out_code + f0 + t : codes + t;
-        if (t < nf && !fast) {
-            list[2][atomicAdd(&cnt[2], 1)] = (uint16_t)t;
-        } else if (fast) {
-            Acc a = {0u, 0u, 0u};
-            if (all5 && end64) {
-#pragma unroll
-                for (int c = 0; c < NH; c++)
-                    accum_fast5<COMPUTE, true>(h4[c], c, HB, masks5<COMPUTE>(c), a);
-            } else if (all5) {
-#pragma unroll
-                for (int c = 0; c < NH; c++)
-                    accum_fast5<COMPUTE, true>(h4[c], c, te < HB ? te : HB, masks5<COMPUTE>(c), a);
-            } else {
-#pragma unroll
-                for (int j = 0; j < NH; j++)
-                    accum_chunk<COMPUTE>(h4[j], 16 * j, ts, te < HB ? te : HB, a);
-            }
-            if (te > HB) {
-                auto wbase = [&](u32 c) {
-                    const u32 q = c / QW;
-                    u32 b = 0;
-#pragma unroll
-                    for (int k = 0; k < NW - 1; k++)
-                        b += (u32)k < q ? wtot[k] : 0u;
-                    return b;
-                };
-                const u32 p0 = pfirst[t] + wbase(start);
-                const u32 p1 = qend[t] + wbase(start + nch - 1);
-                a.tcp += (p1 - p0) - (hsum4(h4[0]) + hsum4(h4[1]) + hsum4(h4[2]) +
-                                      (NH == 4 ? hsum4(h4[3]) : 0u));
-            }
-            epilogue<1, 4, COMPUTE, S::WM, false>(
-                h, a, frames + o, len, (int64_t)(frames_bytes - o), true, 0, flags, oc,
-                COMPUTE ? csums + t : nullptr, true, h4, XFrame{},
-                COMPUTE ? reinterpret_cast<uint8_t*>(hdr + 4 * t) : nullptr);
-        }
+    const int tf = t < nf ? t : 0;
+    const uint4 h4[4] = {hdr[NH * tf], hdr[NH * tf + 1], hdr[NH * tf + 2],
+                         NH == 4 ? hdr[NH * tf + 3] : make_uint4(0, 0, 0, 0)};
+    Hdr h;
+    h.d3 = h4[0].w;
+    h.d4 = h4[1].x;
+    h.d5 = h4[1].y;
+    const int ihl = (int)((h.d3 >> 16) & 15u);
+    const int ts = 14 + 4 * ihl;
+    const int te = 14 + (int)bswap16(h.d4 & 0xFFFFu);
+    // NH = 3 (RX): doff (byte ts + 12) must lie in chunk 2: ihl == 5
+    const bool fast = t >= nf ||
+                      ((NH == 4 ? ihl <= 8 : ihl == 5) && (te <= HB || te == (int)len));
+    if (!__syncthreads_and(fast)) {
+        if (t == 0)
+            fb_push(fb, epoch, blk);
+        return;                            // block-uniform: nothing written yet
     }
-    __syncthreads();
-    const int ns = cnt[2];
-    if (ns)
-        desc_class<S::G2, S::U2, COMPUTE, true, false, S::WM, 1, S::NT>(
-            frames, frames_bytes, soff, slen, list[2], ns, flags, codes, csums, Ext{}, nullptr,
-            nullptr, COMPUTE ? hdr : nullptr);
-    if constexpr (COMPUTE) {
-        __syncthreads();
-        desc_tail<S, COMPUTE, false>(frames, frames_bytes, f0, n, soff, slen, codes, csums,
-                                     nullptr, nullptr, hdr, out_code, out_csum, flags, Ext{});
-    } else if (ns && out_code) {
-        __syncthreads();
-        for (int i = t; i < ns; i += kBlock) {
-            const int ft = list[2][i];
-            out_code[f0 + ft] = codes[ft];
+    // wave-uniform: every frame of the wave has ihl == 5, so the stash's word
+    // masks are constants (masks5, as the group kernels); and when every one
+    // also has te >= HB, no segment end lies in the stash
+    const bool all5 = NH == 3 || __all(t >= nf || ihl == 5);
+    const bool endh = __all(t >= nf || te >= HB);
+    if (t < nf) {
+        Acc a = {0u, 0u, 0u};
+        if (all5 && endh) {
+#pragma unroll
+            for (int c = 0; c < NH; c++)
+                accum_fast5<COMPUTE, true>(h4[c], c, HB, masks5<COMPUTE>(c), a);
+        } else if (all5) {
+#pragma unroll
+            for (int c = 0; c < NH; c++)
+                accum_fast5<COMPUTE, true>(h4[c], c, te < HB ? te : HB, masks5<COMPUTE>(c), a);
+        } else if constexpr (NH == 4) {
+#pragma unroll
+            for (int j = 0; j < NH; j++)
+                accum_chunk<COMPUTE>(h4[j], 16 * j, ts, te < HB ? te : HB, a);
         }
+        if (te > HB) {
+            // Q is wave-local: add the chunk's wave base at both ends
+            auto wbase = [&](u32 c) {
+                const u32 q = c / QW;
+                u32 b = 0;
+#pragma unroll
+                for (int k = 0; k < NW - 1; k++)
+                    b += (u32)k < q ? wtot[k] : 0u;
+                return b;
+            };
+            a.tcp += tail[t] + wbase(start + nch - 1) - wbase(start + NH);
+        }
+        epilogue<1, 4, COMPUTE, WM, false>(
+            h, a, frames + o, len, (int64_t)(frames_bytes - o), true, 0, flags,
+            COMPUTE ? codes + t : (out_code ? out_code + f0 + t : codes + t),
+            COMPUTE && out_csum ? out_csum + f0 + t : nullptr, true, h4, XFrame{},
+            COMPUTE ? reinterpret_cast<uint8_t*>(hdr + 4 * t) : nullptr);
+    }
+    if constexpr (COMPUTE) {
+        // the staged sectors leave together, in frame order, 16 B per lane:
+        // four lanes per sector, so two packed 64 B frames are one 128 B line
+        // of one store instruction.  A chunk goes out under exactly the
+        // epilogue's conditions: a status that fills, inside the frame (the
+        // region ends inside the buffer: phase 0).
+        __syncthreads();
+        if (!(flags & GCS_CF_NO_INPLACE)) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int q = r * kBlock + t, ft = q >> 2, c = q & 3;
+                if (ft >= nf)
+                    continue;
+                const u32 st = codes[ft], m = meta[ft];
+                const bool wip = st == GCS_TX_OK || st == GCS_TX_IP_ONLY || st == GCS_TX_BAD_TCPLEN;
+                if (wip && (u32)(16 * c) < (m & 0xFFFFu))
+                    stg16<WM>(frames + r0 + 16ull * ((m >> 16) + c), hdr[q]);
+            }
+        }
+        if (out_code && t < nf)
+            out_code[f0 + t] = codes[t];
     }
 }
 
-template <class S, class T, bool COMPUTE, bool XCD>
-__global__ void __launch_bounds__(kBlock, T::OCC)
-k_desc_stream(uint8_t* __restrict__ frames, uint64_t frames_bytes,
-              const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens, u32 n,
-              uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags)
+// The frames of the blocks k_desc_stream listed (fb), one 32-lane group per
+// frame (k_desc<32,3>'s shape, batches of 3 chunks per lane until the frame
+// ends), over a grid of at most kFbGrid workgroups: when nothing was listed
+// each reads the list's head and leaves (round 4: a workgroup per batch block
+// took 7 us per 4M-frame launch doing that; desc_mixed's class passes in a
+// loop spill 18-51 VGPRs).  Rare in mTCP traffic: misordered or sparse
+// descriptors, regions over RMAX (256 frames of ~1500 B), IP options, frames
+// padded past a segment that ends beyond byte 48/64.
+template <bool COMPUTE>
+__global__ void __launch_bounds__(kBlock)
+k_desc_fallback(uint8_t* __restrict__ frames, uint64_t frames_bytes,
+                const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens, u32 n,
+                uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags,
+                const uint32_t* __restrict__ fb, u32 epoch)
 {
-    desc_stream<S, T, COMPUTE, XCD>(frames, frames_bytes, off, lens, n, out_code, out_csum, flags);
+    constexpr int G = 32, U = 3, FPB = kBlock / G;
+    const unsigned long long v = __hip_atomic_load(
+        reinterpret_cast<const unsigned long long*>(fb), __ATOMIC_RELAXED,
+        __HIP_MEMORY_SCOPE_AGENT);
+    const u32 cnt = (uint32_t)(v >> 32) == epoch ? (uint32_t)v : 0u;
+    const uint64_t total = (uint64_t)cnt * kDescFrames;
+    const int sub = threadIdx.x & (G - 1), grp = threadIdx.x / G;
+    for (uint64_t w = (uint64_t)blockIdx.x * FPB + grp; w < total;
+         w += (uint64_t)gridDim.x * FPB) {     // group-uniform
+        const uint64_t i = (uint64_t)fb[kFbHead + w / kDescFrames] * kDescFrames +
+                           w % kDescFrames;
+        if (i >= n)
+            continue;
+        const uint64_t o = off[i];
+        const u32 len = lens[i];
+        const bool ok = (o & 15) == 0 && o <= frames_bytes && len <= frames_bytes - o;
+        uint8_t* f = frames + (ok ? o : 0);
+        do_frame<G, U, COMPUTE, true, true, kNT, WM_SECTOR_SC1>(
+            f, len, ok ? (int64_t)(frames_bytes - o) : 0, ok, sub, flags,
+            out_code ? out_code + i : nullptr, out_csum ? out_csum + i : nullptr);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -2330,55 +2271,63 @@ hipError_t launch_classify_fixed(uint8_t* frames, uint64_t stride, u32 frame_len
 
 // The shipped prefix-sum stream (k_desc_stream; tools/kbench.hip imix, DESIGN.md
 // §4): 8 chunks per lane per trip, block regions up to 12,288 chunks (192 KiB per
-// 256 frames; C3 blocks span ~91 KiB), 6 waves per SIMD (26-27 KB of LDS, 80
-// VGPRs).  4M IMIX frames against the list kernel on the same boxes: verify
-// 253-258 vs 284-289 us, fill (fresh check fields) 358-366 vs 428-431 us.  NT
-// loads for both (the stream fill with temporal loads: 374 vs 325 us).  The
-// fill's staged sectors leave with sc1 stores: 340 vs 372 us interleaved, 348
-// vs 364 blocked against nt (plain 345-349, sc0 sc1 344-347), where the list
-// kernel preferred nt (kbench_imix_stream_wm*.log).
-// RX stashes chunks 0..2 only (HDR3: ihl = 5 fast frames; LDS 27 -> 22 KB)
-// and runs 7 waves per SIMD (72 VGPRs): 240.7-245.7 vs 249-255 us interleaved,
-// 244.0 vs 244.6 blocked (kbench_imix_stream_h3*.log).
+// 256 frames; C3 blocks span ~91 KiB), NT loads.  TX stashes chunks 0..3 (the
+// sector written back, sc1 stores: 340 vs 372 us interleaved against nt,
+// kbench_imix_stream_wm*.log), RX chunks 0..2 (ihl = 5 fast frames; HDR3:
+// 240.7-245.7 vs 249-255 us interleaved, kbench_imix_stream_h3*.log).  With the
+// class passes in k_desc_fallback both run 8 waves per SIMD (round 4).
 template <bool COMPUTE>
-using StreamShip = typename std::conditional<COMPUTE, StreamShape<8, 12288, 6>,
-                                             StreamShape<8, 12288, 7, false, 0, true>>::type;
-template <bool COMPUTE>
-using DescStreamShip = DescShape<4, 1, 16, 3, 32, 3, WM_SECTOR_SC1, kBlock, true, 1, 1, COMPUTE,
-                                 true>;
-
+using StreamShip = StreamShape<8, 8192, 8, COMPUTE ? 4 : 3>;
 template <bool COMPUTE>
 static hipError_t launch_desc(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
                               const uint16_t* len, u32 n, uint8_t* code, uint32_t* csums,
-                              u32 flags, bool ext_on, const Ext& ext, hipStream_t s)
+                              u32 flags, bool ext_on, const Ext& ext, DescFb* fb, hipStream_t s)
 {
-    using S = DescShip<COMPUTE>;
-    const dim3 grid((n + S::F - 1) / S::F);
-    if (ext_on)
+    if (n == 0)
+        return hipSuccess;
+    const dim3 grid((n + kDescFrames - 1) / kDescFrames);
+    static_assert(kDescFrames == kBlock, "one descriptor per thread");
+    if (ext_on) {
+        using S = DescShip<COMPUTE>;
         hipLaunchKernelGGL((k_desc_mixed_x<S, COMPUTE, kXCD, kDescOcc>), grid, dim3(kBlock), 0, s,
                            frames, frames_bytes, off, len, n, code, csums, flags, ext);
-    else
-        hipLaunchKernelGGL((k_desc_stream<DescStreamShip<COMPUTE>, StreamShip<COMPUTE>, COMPUTE,
-                                          kXCD>),
-                           grid, dim3(kBlock), 0, s, frames, frames_bytes, off, len, n, code,
-                           csums, flags);
+        return hipGetLastError();
+    }
+    if (!fb || !fb->d || fb->cap_frames < n)
+        return hipErrorInvalidValue;
+    if (++fb->epoch == 0)                  // a zeroed list reads as epoch 0: never use it
+        fb->epoch = 1;
+    hipLaunchKernelGGL((k_desc_stream<StreamShip<COMPUTE>, COMPUTE, WM_SECTOR_SC1, kXCD>), grid,
+                       dim3(kBlock), 0, s, frames, frames_bytes, off, len, n, code, csums, flags,
+                       fb->d, fb->epoch);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return e;
+    // a verdict-less verify has nothing to fall back to (the stream kernel
+    // writes none either)
+    if (!COMPUTE && !code)
+        return hipSuccess;
+    const u32 fgrid = grid.x * (kDescFrames / 8) < kFbGrid ? grid.x * (kDescFrames / 8) : kFbGrid;
+    hipLaunchKernelGGL((k_desc_fallback<COMPUTE>), dim3(fgrid), dim3(kBlock), 0, s, frames,
+                       frames_bytes, off, len, n, code, csums, flags, (const uint32_t*)fb->d,
+                       fb->epoch);
     return hipGetLastError();
 }
 
 hipError_t launch_verify_desc(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
                               const uint16_t* len, u32 n, uint8_t* verdict, u32 flags,
-                              hipStream_t s)
+                              DescFb* fb, hipStream_t s)
 {
     return launch_desc<false>(frames, frames_bytes, off, len, n, verdict, nullptr, flags,
-                              (flags & GCS_VF_ICMP) != 0, Ext{}, s);
+                              (flags & GCS_VF_ICMP) != 0, Ext{}, fb, s);
 }
 
 hipError_t launch_compute_desc(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
                                const uint16_t* len, u32 n, uint8_t* status, uint32_t* csums,
-                               u32 flags, hipStream_t s)
+                               u32 flags, DescFb* fb, hipStream_t s)
 {
     return launch_desc<true>(frames, frames_bytes, off, len, n, status, csums, flags,
-                             (flags & GCS_CF_ICMP) != 0, Ext{}, s);
+                             (flags & GCS_CF_ICMP) != 0, Ext{}, fb, s);
 }
 
 // Descriptor batch spread thin: one frame per 32-lane group (8 frames per
@@ -2415,7 +2364,7 @@ hipError_t launch_classify_desc(uint8_t* frames, uint64_t frames_bytes, const ui
                                 const Ext& ext, hipStream_t s)
 {
     return launch_desc<false>(frames, frames_bytes, off, len, n, verdict, nullptr, flags, true,
-                              ext, s);
+                              ext, nullptr, s);
 }
 
 hipError_t launch_icmp_fn(const uint8_t* buf, uint64_t buf_bytes, const uint64_t* off,

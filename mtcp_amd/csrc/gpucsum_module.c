@@ -13,8 +13,11 @@
  * The checksum work itself is libmtcp_gpucsum's gcs_verify_ptrs /
  * gcs_compute_ptrs (one GPU batch per burst).  There is no CPU fallback: a
  * context that cannot reach its GPU exits at init_handle like the reference's
- * modules do (dpdk_module.c:243-247), and a failing batch is reported on
- * stderr and its frames are dropped.
+ * modules do (dpdk_module.c:243-247).  A failing call later is counted and
+ * reported on stderr, and its frames follow gpucsum_io_module.h's "GPU
+ * failures": RX frames come back NULL; TX frames of an in-place inner go out
+ * with the check fields mTCP left at 0 (counted: tx_unfilled_sent), shadow
+ * (TX_EAGER) frames are withheld; GPUCSUM_ON_GPU_FAIL=exit makes it fatal.
  *
  * Inner-module shapes (gpucsum_io_module.h): frames are filled in place for
  * modules whose TX buffers stay put until send_pkts (dpdk, onvm, psio), and
@@ -43,6 +46,11 @@ struct rx_if {
 	uint16_t *glen;     /* length the GPU folds (0 = skip)      */
 	uint8_t *verdict;
 	uint16_t *queue;    /* RSS on */
+	/* verify as you go (GPUCSUM_RX_GROUP): the burst is posted in groups of
+	 * rx_group frames; frames [0, ready) have their verdicts */
+	uint32_t ready;
+	uint32_t ngroups;
+	uint64_t *ticket;   /* per group (0: verified synchronously) */
 };
 
 struct tx_if {
@@ -60,6 +68,7 @@ struct gthr {
 	struct mtcp_thread_context *ctx;
 	gcs_ctx *gcs;
 	uint32_t tx_group;      /* async TX fill: post every tx_group completed frames (0: off) */
+	uint32_t rx_group;      /* async RX verify: frames per posted group (0: one sync batch) */
 	struct rx_if *rx[GPUCSUM_MAX_IFS];
 	struct tx_if *tx[GPUCSUM_MAX_IFS];
 	struct tx_if *last_tx;  /* the queue of the most recent get_wptr */
@@ -83,6 +92,7 @@ extern const int dpdk_module_ip_defrag __attribute__((weak));
 
 static io_module_func *g_inner;
 static uint32_t g_caps;
+static int g_fail_exit;      /* GPUCSUM_ON_GPU_FAIL=exit: a failed GPU call is fatal */
 static uint32_t g_seg_max = GPUCSUM_DEFAULT_SEG_MAX;
 static struct gthr *g_table[GPUCSUM_MAX_THREADS];
 static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER;
@@ -154,6 +164,20 @@ static void die(const char *what, int rc)
 	exit(EXIT_FAILURE);
 }
 
+/* A GPU call failed after init: count it, report it (the first few and then
+ * every 1024th, so a dead GPU does not flood stderr), or exit when
+ * GPUCSUM_ON_GPU_FAIL=exit. */
+static void gpu_failed(struct gthr *g, const char *what, uint32_t frames, int rc)
+{
+	g->st.gpu_failures++;
+	if (g_fail_exit)
+		die(what, rc);
+	if (g->st.gpu_failures <= 8 || (g->st.gpu_failures & 1023) == 0)
+		fprintf(stderr, "[gpucsum] %s of %u frames failed (failure %llu): %s %s\n", what,
+		        frames, (unsigned long long)g->st.gpu_failures, gcs_strerror(rc),
+		        gcs_last_hip_error());
+}
+
 /* ---- vtable ------------------------------------------------------------ */
 
 static void gpucsum_load_module(void)
@@ -171,6 +195,10 @@ static void gpucsum_load_module(void)
 	rc = gcs_device_count(&n);
 	if (rc || n <= 0)
 		die("gcs_device_count (no MI355X visible)", rc ? rc : GCS_ENODEV);
+	{
+		const char *f = getenv("GPUCSUM_ON_GPU_FAIL");
+		g_fail_exit = f && strcmp(f, "exit") == 0;
+	}
 	if (g_inner->load_module)
 		g_inner->load_module();
 }
@@ -224,6 +252,12 @@ static void gpucsum_init_handle(struct mtcp_thread_context *ctx)
 		 * the last group */
 		env = getenv("GPUCSUM_TX_GROUP");
 		g->tx_group = rc ? 0 : env ? (uint32_t)atoi(env) : 8;
+		/* verify as you go: recv_pkts posts the burst in groups of
+		 * GPUCSUM_RX_GROUP (default 16, 0 = off) frames and returns; get_rptr(i)
+		 * waits only for the group holding frame i, so mTCP processes the
+		 * first frames (core.c:792-795) while the GPU verifies the rest */
+		env = getenv("GPUCSUM_RX_GROUP");
+		g->rx_group = rc ? 0 : env ? (uint32_t)atoi(env) : 16;
 	}
 	env = getenv("GPUCSUM_RSS_QUEUES");
 	if (env && atoi(env) > 0) {
@@ -278,10 +312,9 @@ static void post_tx(struct gthr *g, struct tx_if *q)
 	rc = gcs_compute_ptrs_async(g->gcs, q->ptr + q->posted, q->len + q->posted,
 	                            q->done - q->posted, q->status + q->posted, NULL, &t);
 	if (rc) {
-		/* leave them to flush_tx's synchronous fill */
-		g->st.gpu_failures++;
-		fprintf(stderr, "[gpucsum] async TX fill of %u frames failed: %s %s\n",
-		        q->done - q->posted, gcs_strerror(rc), gcs_last_hip_error());
+		/* leave them to flush_tx's synchronous fill; no more async posts on
+		 * this context */
+		gpu_failed(g, "async TX fill post", q->done - q->posted, rc);
 		g->tx_group = 0;
 		return;
 	}
@@ -307,7 +340,7 @@ static void tx_complete(struct gthr *g, struct tx_if *q, uint32_t upto)
  * async fill, earlier groups are in flight already: post the tail, wait. */
 static void flush_tx(struct gthr *g, int ifidx, struct tx_if *q)
 {
-	uint32_t k;
+	uint32_t k, unfilled = 0;
 	int rc = 0;
 
 	if (!q || q->n == 0)
@@ -315,40 +348,55 @@ static void flush_tx(struct gthr *g, int ifidx, struct tx_if *q)
 	if (q->posted > 0 || (g->tx_group && q->n <= GPUCSUM_ASYNC_MAX)) {
 		q->done = q->n;
 		post_tx(g, q);
-		if (q->posted == q->n) {
+		if (q->ticket) {
+			/* a failed wait cancels every posted fill (gcs_wait) */
 			rc = gcs_wait(g->gcs, q->ticket);
-		} else {
-			/* the tail could not be posted: wait for what was, fill the rest */
-			rc = gcs_wait(g->gcs, q->ticket);
-			if (!rc)
-				rc = gcs_compute_ptrs(g->gcs, q->ptr + q->posted, q->len + q->posted,
-				                      q->n - q->posted, q->status + q->posted, NULL);
+			if (rc) {
+				unfilled += q->posted;
+				gpu_failed(g, "TX fill (async wait)", q->posted, rc);
+			}
+		}
+		if (q->posted < q->n) {
+			/* the tail could not be posted: fill it synchronously */
+			int rc2 = gcs_compute_ptrs(g->gcs, q->ptr + q->posted, q->len + q->posted,
+			                           q->n - q->posted, q->status + q->posted, NULL);
+			if (rc2) {
+				unfilled += q->n - q->posted;
+				gpu_failed(g, "TX fill", q->n - q->posted, rc2);
+				rc = rc2;
+			}
 		}
 	} else {
 		rc = gcs_compute_ptrs(g->gcs, q->ptr, q->len, q->n, q->status, NULL);
+		if (rc) {
+			unfilled = q->n;
+			gpu_failed(g, "TX fill", q->n, rc);
+		}
 	}
 	q->done = q->posted = 0;
 	q->ticket = 0;
-	if (rc) {
-		g->st.gpu_failures++;
-		fprintf(stderr, "[gpucsum] TX fill of %u frames failed: %s %s\n", q->n,
-		        gcs_strerror(rc), gcs_last_hip_error());
-	} else {
+	if (!rc) {
 		g->st.tx_frames += q->n;
 		g->st.tx_batches++;
 	}
 	if (q->shadow) {
-		for (k = 0; k < q->n; k++) {
-			uint8_t *p;
-			if (rc)
-				break;              /* unfilled frames never reach the wire */
-			p = g_inner->get_wptr(g->ctx, ifidx, q->len[k]);
-			if (!p) {
-				g->st.tx_inner_full += q->n - k;
-				break;
+		if (rc) {
+			/* unfilled frames never reach the wire: the whole flush is
+			 * withheld, so what goes out stays in mTCP's order */
+			g->st.tx_unfilled_dropped += q->n;
+		} else {
+			for (k = 0; k < q->n; k++) {
+				uint8_t *p = g_inner->get_wptr(g->ctx, ifidx, q->len[k]);
+				if (!p) {
+					g->st.tx_inner_full += q->n - k;
+					break;
+				}
+				memcpy(p, q->ptr[k], q->len[k]);
 			}
-			memcpy(p, q->ptr[k], q->len[k]);
 		}
+	} else {
+		/* in place: the inner sends them as they are (check fields 0) */
+		g->st.tx_unfilled_sent += unfilled;
 	}
 	q->n = 0;
 }
@@ -398,7 +446,7 @@ static int32_t gpucsum_send_pkts(struct mtcp_thread_context *ctx, int nif)
 static int rx_reserve(struct rx_if *r, uint32_t n)
 {
 	uint32_t cap = r->cap ? r->cap : 64;
-	void *a, *b, *c, *d, *e;
+	void *a, *b, *c, *d, *e, *f;
 
 	if (n <= r->cap)
 		return 0;
@@ -414,20 +462,86 @@ static int rx_reserve(struct rx_if *r, uint32_t n)
 	if (d) r->verdict = d;
 	e = realloc(r->queue, cap * sizeof(*r->queue));
 	if (e) r->queue = e;
-	if (!a || !b || !c || !d || !e)
+	f = realloc(r->ticket, cap * sizeof(*r->ticket));   /* >= groups of any size */
+	if (f) r->ticket = f;
+	if (!a || !b || !c || !d || !e || !f)
 		return -1;
 	r->cap = cap;
 	return 0;
+}
+
+/* Frames [lo, hi) have their GPU verdicts: apply the decorator's own
+ * dispositions (inner drops, chains left to the inner's checks) and the RSS
+ * bookkeeping. */
+static void rx_settle(struct gthr *g, struct rx_if *r, int32_t lo, int32_t hi, int rss_ok)
+{
+	int32_t i;
+
+	for (i = lo; i < hi; i++) {
+		if (!r->ptr[i])
+			r->verdict[i] = GCS_V_DROP_TRUNC;   /* the inner module's own drop */
+		else if (r->glen[i] != r->len[i])
+			r->verdict[i] = V_INNER;            /* chain: the inner's checks */
+	}
+	if (g->rss && rss_ok)
+		for (i = lo; i < hi; i++)
+			if (r->verdict[i] == GCS_V_ACCEPT && r->queue[i] != (uint16_t)g->own_queue)
+				g->st.rx_foreign++;
+}
+
+/* The verify of frames [lo, hi) failed: every one comes back NULL. */
+static void rx_unverified(struct gthr *g, struct rx_if *r, int32_t lo, int32_t hi, int rc)
+{
+	int32_t i;
+
+	gpu_failed(g, "RX verify", (uint32_t)(hi - lo), rc);
+	for (i = lo; i < hi; i++) {
+		if (r->ptr[i] && r->glen[i] == r->len[i])
+			g->st.rx_unverified++;
+		r->verdict[i] = GCS_V_DROP_TRUNC;
+	}
+	rx_settle(g, r, lo, hi, 0);
+}
+
+/* Verify as you go: wait until frame `index` has its verdict -- the group
+ * holding it, and with it every group posted before (gcs_wait completes in
+ * posting order). */
+static void rx_wait(struct gthr *g, struct rx_if *r, int32_t index)
+{
+	const uint32_t G = g->rx_group;
+	uint32_t grp = (uint32_t)index / G, k;
+	int32_t hi;
+	int rc = 0;
+
+	if (grp >= r->ngroups)
+		grp = r->ngroups - 1;
+	for (k = grp + 1; k-- > r->ready / G;)
+		if (r->ticket[k]) {                 /* the newest posted group up to grp */
+			rc = gcs_wait(g->gcs, r->ticket[k]);
+			break;
+		}
+	hi = (int32_t)((grp + 1) * G) < r->n ? (int32_t)((grp + 1) * G) : r->n;
+	if (rc)
+		rx_unverified(g, r, (int32_t)r->ready, r->n, rc);   /* the rest of the burst */
+	else
+		rx_settle(g, r, (int32_t)r->ready, hi, 1);
+	r->ready = rc ? (uint32_t)r->n : (uint32_t)hi;
 }
 
 static int32_t gpucsum_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
 {
 	struct gthr *g = lookup(ctx);
 	struct rx_if *r;
-	int32_t n = g_inner->recv_pkts(ctx, ifidx), i;
+	int32_t n, i;
 	const int chained = (g_caps & GPUCSUM_INNER_RX_CHAINED) != 0;
 	int rc;
 
+	if (g && ifidx >= 0 && ifidx < GPUCSUM_MAX_IFS && g->rx[ifidx] &&
+	    g->rx[ifidx]->ready < (uint32_t)g->rx[ifidx]->n && g->rx[ifidx]->n > 0)
+		/* a loop that left frames of the last burst unread: its groups
+		 * complete before the inner reuses their buffers */
+		rx_wait(g, g->rx[ifidx], g->rx[ifidx]->n - 1);
+	n = g_inner->recv_pkts(ctx, ifidx);
 	if (!g || ifidx < 0 || ifidx >= GPUCSUM_MAX_IFS)
 		return n;
 	if (!g->rx[ifidx])
@@ -436,6 +550,8 @@ static int32_t gpucsum_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
 	if (!r)
 		die("calloc", GCS_ENOMEM);
 	r->n = 0;
+	r->ready = 0;
+	r->ngroups = 0;
 	if (n <= 0)
 		return n;
 	if (rx_reserve(r, (uint32_t)n))
@@ -450,6 +566,31 @@ static int32_t gpucsum_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
 			r->len[i] = 0;
 		r->glen[i] = (chained && r->len[i] > g_seg_max) ? 0 : r->len[i];
 	}
+	g->st.rx_frames += (uint64_t)n;
+	r->n = n;
+	if (g->rx_group && !g->rss) {
+		/* verify as you go: post the groups, return; get_rptr waits */
+		const uint32_t G = g->rx_group;
+		for (i = 0; i < n; i += (int32_t)G) {
+			const uint32_t m = (uint32_t)(n - i) < G ? (uint32_t)(n - i) : G;
+			uint64_t t = 0;
+			rc = gcs_verify_ptrs_async(g->gcs, r->ptr + i, r->glen + i, m, r->verdict + i,
+			                           GCS_VF_ZERO_BAD_TCP_CHECK, &t);
+			if (rc) {
+				/* the groups posted so far complete; the rest is unverified */
+				if (i > 0)
+					rx_wait(g, r, i - 1);
+				if (r->ready < (uint32_t)n)
+					rx_unverified(g, r, (int32_t)r->ready, n, rc);
+				r->ready = (uint32_t)n;
+				break;
+			}
+			r->ticket[r->ngroups++] = t;
+			g->st.rx_posts++;
+		}
+		g->st.rx_batches++;
+		return n;
+	}
 	if (g->rss)
 		rc = gcs_classify_ptrs(g->gcs, r->ptr, r->glen, (uint32_t)n, r->verdict, NULL,
 		                       r->queue, GCS_VF_ZERO_BAD_TCP_CHECK);
@@ -457,25 +598,13 @@ static int32_t gpucsum_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
 		rc = gcs_verify_ptrs(g->gcs, r->ptr, r->glen, (uint32_t)n, r->verdict,
 		                     GCS_VF_ZERO_BAD_TCP_CHECK);
 	if (rc) {
-		g->st.gpu_failures++;
-		fprintf(stderr, "[gpucsum] RX verify of %d frames failed: %s %s\n", n,
-		        gcs_strerror(rc), gcs_last_hip_error());
-		memset(r->verdict, GCS_V_DROP_TRUNC, (size_t)n);
+		/* unverified: every frame of the burst comes back NULL */
+		rx_unverified(g, r, 0, n, rc);
 	} else {
 		g->st.rx_batches++;
+		rx_settle(g, r, 0, n, 1);
 	}
-	for (i = 0; i < n; i++) {
-		if (!r->ptr[i])
-			r->verdict[i] = GCS_V_DROP_TRUNC;   /* the inner module's own drop */
-		else if (r->glen[i] != r->len[i])
-			r->verdict[i] = V_INNER;            /* chain: the inner's checks */
-	}
-	if (g->rss && !rc)
-		for (i = 0; i < n; i++)
-			if (r->verdict[i] == GCS_V_ACCEPT && r->queue[i] != (uint16_t)g->own_queue)
-				g->st.rx_foreign++;
-	g->st.rx_frames += (uint64_t)n;
-	r->n = n;
+	r->ready = (uint32_t)n;
 	return n;
 }
 
@@ -489,6 +618,8 @@ static uint8_t *gpucsum_get_rptr(struct mtcp_thread_context *ctx, int ifidx, int
 
 	if (!r || index < 0 || index >= r->n)
 		return g_inner->get_rptr(ctx, ifidx, index, len);
+	if ((uint32_t)index >= r->ready)
+		rx_wait(g, r, index);                   /* verify as you go */
 	if (g_caps & GPUCSUM_INNER_RX_ONCE) {
 		/* the burst pass's call was the inner's one call for this index */
 		if (GCS_V_IS_ERROR(r->verdict[index])) {
@@ -530,6 +661,10 @@ static void gpucsum_destroy_handle(struct mtcp_thread_context *ctx)
 	struct gthr *g = lookup(ctx);
 	int i;
 
+	if (g)
+		for (i = 0; i < GPUCSUM_MAX_IFS; i++)
+			if (g->rx[i] && g->rx[i]->n > 0 && g->rx[i]->ready < (uint32_t)g->rx[i]->n)
+				rx_wait(g, g->rx[i], g->rx[i]->n - 1);   /* nothing in flight */
 	if (g_inner->destroy_handle)
 		g_inner->destroy_handle(ctx);
 	if (!g)
@@ -550,6 +685,7 @@ static void gpucsum_destroy_handle(struct mtcp_thread_context *ctx)
 			free(g->rx[i]->glen);
 			free(g->rx[i]->verdict);
 			free(g->rx[i]->queue);
+			free(g->rx[i]->ticket);
 			free(g->rx[i]);
 		}
 		if (g->tx[i]) {
@@ -624,7 +760,11 @@ int gpucsum_rx_verdict(struct mtcp_thread_context *ctx, int ifidx, int index)
 	struct gthr *g = lookup(ctx);
 	struct rx_if *r = (g && ifidx >= 0 && ifidx < GPUCSUM_MAX_IFS) ? g->rx[ifidx] : NULL;
 
-	if (!r || index < 0 || index >= r->n || r->verdict[index] == V_INNER)
+	if (!r || index < 0 || index >= r->n)
+		return -1;
+	if ((uint32_t)index >= r->ready)
+		rx_wait(g, r, index);
+	if (r->verdict[index] == V_INNER)
 		return -1;
 	return r->verdict[index];
 }

@@ -115,28 +115,68 @@ static int process_one(int ifidx, uint32_t ts, unsigned char *pkt, int len)
 	return ret < 0 ? REFS_ERROR : ret ? REFS_TRUE : REFS_FALSE;
 }
 
+static double refs_now_us(void);
+
+/* refs_rx_loop, timed per burst when blocked_us is not NULL: blocked_us[b] =
+ * the time burst b's recv_pkts and get_rptr calls kept the mTCP thread inside
+ * the I/O module (core.c:789-793; through the decorator, the GPU verify it
+ * waits for), burst_us[b] = recv_pkts to the end of the burst's last
+ * ProcessPacket (core.c:789-801, without the send round). */
+int refs_rx_loop_timed(struct io_module_func *iom, struct mtcp_thread_context *ctx, int ifidx,
+                       uint8_t *disp, uint32_t max, uint64_t *rx_errors, double *blocked_us,
+                       double *burst_us, uint32_t max_bursts);
+
 /* core.c:785-801 plus the send_pkts of core.c:846-848 after each round (ICMP
  * echo replies and ARP answers go out through get_wptr).  Returns frames seen;
  * disp[k] per frame in arrival order; *rx_errors as nstat.rx_errors counts them. */
 int refs_rx_loop(struct io_module_func *iom, struct mtcp_thread_context *ctx, int ifidx,
                  uint8_t *disp, uint32_t max, uint64_t *rx_errors)
 {
-	uint32_t k = 0;
+	return refs_rx_loop_timed(iom, ctx, ifidx, disp, max, rx_errors, NULL, NULL, 0);
+}
+
+int refs_rx_loop_timed(struct io_module_func *iom, struct mtcp_thread_context *ctx, int ifidx,
+                       uint8_t *disp, uint32_t max, uint64_t *rx_errors, double *blocked_us,
+                       double *burst_us, uint32_t max_bursts)
+{
+	uint32_t k = 0, b = 0;
 	int32_t n, i;
+	const int timed = blocked_us != NULL;
+	double t0 = 0, t1 = 0, in_mod = 0;
 
 	refs_bind(iom, ctx, 1000);
 	*rx_errors = 0;
-	while ((n = iom->recv_pkts(ctx, ifidx)) > 0) {
+	for (;;) {
+		if (timed)
+			t0 = refs_now_us();
+		n = iom->recv_pkts(ctx, ifidx);
+		if (timed)
+			in_mod = refs_now_us() - t0;
+		if (n <= 0)
+			break;
 		for (i = 0; i < n; i++) {
 			uint16_t len = 0;
-			unsigned char *p = iom->get_rptr(ctx, ifidx, i, &len);
-			int d = p ? process_one(ifidx, refs_mgr.cur_ts, p, len) : REFS_NULL;
+			unsigned char *p;
+			int d;
+			if (timed) {
+				t1 = refs_now_us();
+				p = iom->get_rptr(ctx, ifidx, i, &len);
+				in_mod += refs_now_us() - t1;
+			} else {
+				p = iom->get_rptr(ctx, ifidx, i, &len);
+			}
+			d = p ? process_one(ifidx, refs_mgr.cur_ts, p, len) : REFS_NULL;
 			if (d == REFS_NULL || d == REFS_ERROR)
 				(*rx_errors)++;
 			if (k < max)
 				disp[k] = (uint8_t)d;
 			k++;
 		}
+		if (timed && b < max_bursts) {
+			blocked_us[b] = in_mod;
+			burst_us[b] = refs_now_us() - t0;
+		}
+		b++;
 		iom->send_pkts(ctx, ifidx);
 		refs_mgr.cur_ts++;
 	}

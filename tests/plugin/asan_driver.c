@@ -377,6 +377,81 @@ static void part_async(int registered)
 	free(src); free(ref); free(st); free(vd); free(ptrs); free(cs); free(off); free(len);
 }
 
+/* Part 7: the decorator's GPU-failure paths (gpucsum_io_module.h "GPU
+ * failures"), forced with the test-only GCS_FAULT_INJECT switch: an RX burst
+ * whose verify fails comes back NULL; in-place TX frames whose fill, or whose
+ * async wait, fails go out as mTCP left them, counted; a failed async post
+ * falls back to the synchronous fill. */
+static void part_faults(void)
+{
+	const uint32_t n = 700;
+	uint64_t *off, bytes;
+	uint16_t *len;
+	uint8_t *buf = imix(n, 0xFA17, &off, &len, &bytes), *rx = malloc(bytes + 64);
+	uint8_t *d = malloc(n), *f = malloc(2048);
+	struct mini_stats s;
+	struct gpucsum_stats g0, g1;
+	struct mtcp_thread_context *ctx = (struct mtcp_thread_context *)(uintptr_t)0x2000;
+	uint32_t i, filled = 0;
+	int rc;
+
+	memcpy(rx, buf, bytes + 64);
+	for (i = 0; i < n; i++) {
+		uint32_t c2;
+		ref_tx_fill(rx + off[i], len[i], &c2);
+	}
+	setenv("GCS_FAULT_INJECT", "none", 1);           /* armed when the context is made */
+	setenv("GPUCSUM_TX_GROUP", "8", 1);
+	rc = gpucsum_set_inner(&synth_module_func);
+	CHECK(rc == 0, "gpucsum_set_inner %d", rc);
+	mini_start(&gpucsum_module_func, ctx);
+	gpucsum_get_stats(ctx, &g0);
+
+	setenv("GCS_FAULT_INJECT", "verify_ptrs", 1);
+	synth_reset(64);
+	synth_set_rx(rx, off, len, n);
+	rc = mini_rx_loop(&gpucsum_module_func, ctx, 0, &s, d, n);
+	gpucsum_get_stats(ctx, &g1);
+	CHECK(rc == (int)n && s.accepted == 0 && s.rx_errors == n &&
+	      g1.rx_unverified - g0.rx_unverified == n,
+	      "RX verify failure: %d frames, %llu accepted, %llu unverified", rc,
+	      (unsigned long long)s.accepted, (unsigned long long)(g1.rx_unverified - g0.rx_unverified));
+
+	setenv("GCS_FAULT_INJECT", "wait", 1);             /* async waits fail: fills cancelled */
+	synth_reset(64);
+	mini_tx(&gpucsum_module_func, ctx, 0, buf, off, len, n, 64);
+	gpucsum_get_stats(ctx, &g0);
+	CHECK(synth_tx_sent() == n && g0.tx_unfilled_sent == n, "TX wait failure: %u sent, %llu unfilled",
+	      synth_tx_sent(), (unsigned long long)g0.tx_unfilled_sent);
+	for (i = 0; i < n; i++) {
+		synth_tx_frame(i, f);
+		filled += f[24] != 0 || f[25] != 0;            /* no check written */
+	}
+	CHECK(filled == 0, "%u frames with an IP check after cancelled fills", filled);
+
+	setenv("GCS_FAULT_INJECT", "compute_async", 1);    /* async post fails: sync fill */
+	synth_reset(64);
+	mini_tx(&gpucsum_module_func, ctx, 0, buf, off, len, n, 64);
+	gpucsum_get_stats(ctx, &g1);
+	filled = 0;
+	for (i = 0; i < n; i++) {
+		uint32_t c2;
+		memcpy(rx, buf + off[i], len[i]);
+		if (ref_tx_fill(rx, len[i], &c2) < 0)
+			continue;
+		synth_tx_frame(i, f);
+		filled += memcmp(rx, f, len[i]) != 0;
+	}
+	CHECK(synth_tx_sent() == n && filled == 0 && g1.tx_unfilled_sent == g0.tx_unfilled_sent,
+	      "TX after a failed post: %u sent, %u differ from the oracle", synth_tx_sent(), filled);
+	mini_stop(&gpucsum_module_func, ctx);
+	unsetenv("GCS_FAULT_INJECT");
+	unsetenv("GPUCSUM_TX_GROUP");
+	printf("part 7 GPU-failure paths: RX burst NULL, TX unfilled counted %llu, failures %llu\n",
+	       (unsigned long long)g1.tx_unfilled_sent, (unsigned long long)g1.gpu_failures);
+	free(buf); free(rx); free(d); free(f); free(off); free(len);
+}
+
 int main(void)
 {
 	uint64_t mism = 0, frames = 0;
@@ -399,6 +474,7 @@ int main(void)
 	part_errors();
 	part_async(0);
 	part_async(1);
+	part_faults();
 	if (g_fail) {
 		printf("HOST DRIVER FAILED\n");
 		return 1;

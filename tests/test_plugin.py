@@ -35,7 +35,9 @@ class GStats(C.Structure):
     _fields_ = [(k, C.c_uint64) for k in
                 ("rx_frames", "rx_errors", "rx_batches", "tx_frames", "tx_batches",
                  "gpu_failures", "rx_foreign")] + [("device", C.c_int)] + \
-                [(k, C.c_uint64) for k in ("rx_inner", "rx_rptr_changed", "tx_inner_full", "tx_posts")]
+                [(k, C.c_uint64) for k in ("rx_inner", "rx_rptr_changed", "tx_inner_full", "tx_posts",
+                                           "tx_unfilled_sent", "tx_unfilled_dropped",
+                                           "rx_unverified", "rx_posts")]
 
 
 @pytest.fixture(scope="module")

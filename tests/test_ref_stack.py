@@ -259,6 +259,53 @@ def test_decorator_under_reference_rx(H, P, R, D, burst):  # noqa: F811
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("group", ["0", "1", "8", "64", "100"])
+@pytest.mark.parametrize("stage", ["host", "device"])
+def test_verify_as_you_go_under_reference_rx(H, P, R, monkeypatch, group, stage):  # noqa: F811
+    """Verify as you go (GPUCSUM_RX_GROUP): recv_pkts posts the burst in groups
+    and returns; mTCP's get_rptr(i) waits for frame i's group only, while
+    ProcessPacket runs on the earlier frames and icmp.c's echo replies are
+    filled through the same request ring.  Every group size (0: one
+    synchronous batch; 100 > the burst: one group) and staging gives the
+    reference's own dispositions, rx_errors and wire frames."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("plugin GPU tests need a GPU (no CPU fallback exists)")
+    monkeypatch.setenv("GPUCSUM_RX_GROUP", group)
+    monkeypatch.setenv("GCS_ASYNC_STAGE", stage)
+    buf, off, lens = rx_set(seed=29)
+    sw_ctx = C.create_string_buffer(64)
+    d_sw, e_sw, w_sw = run_rx(H, R, vtab(H, "synth_module_func"), C.addressof(sw_ctx),
+                              buf.copy(), off, lens, 64)
+    assert P.gpucsum_set_inner(vtab(H, "synth_module_func")) == 0
+    cbuf = C.create_string_buffer(64)
+    ctx = C.addressof(cbuf)
+    iom = vtab(P, "gpucsum_module_func")
+    assert H.mini_start(iom, ctx) == 0
+    try:
+        d_hw, e_hw, w_hw = run_rx(H, R, iom, ctx, buf.copy(), off, lens, 64)
+        st = GStats()
+        P.gpucsum_get_stats(ctx, C.byref(st))
+    finally:
+        H.mini_stop(iom, ctx)
+    v = Oracle().verify_batch(buf.copy(), off, lens)
+    inb = ~np.isin(v, [8, 9])
+    errs = lambda d: np.isin(d, [REFS_ERROR, REFS_NULL])  # noqa: E731
+    np.testing.assert_array_equal(errs(d_sw)[inb], errs(d_hw)[inb])
+    np.testing.assert_array_equal(d_sw[inb & ~errs(d_sw)], d_hw[inb & ~errs(d_hw)])
+    assert e_sw - errs(d_sw)[~inb].sum() == e_hw - errs(d_hw)[~inb].sum()
+    assert len(w_sw) == len(w_hw) > 0
+    for a, b in zip(w_sw, w_hw):
+        np.testing.assert_array_equal(a, b)
+    assert st.gpu_failures == 0
+    bursts = (len(off) + 63) // 64
+    if group == "0":
+        assert st.rx_posts == 0
+    else:
+        assert st.rx_posts >= bursts
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("burst", [64, 1, 1000])
 def test_decorator_under_reference_tx(H, P, R, D, burst):  # noqa: F811
     iom, ctx, _ = D

@@ -95,23 +95,39 @@ __global__ void __launch_bounds__(256) k_read1(const uint8_t* __restrict__ p, ui
     if (acc == 0x9E3779B9u) out[0] = acc;
 }
 
-// 512 MiB of writes between timed launches (KB_SCRUB=1): twice the 256 MiB
-// Infinity Cache, so a timed kernel starts with nothing of its batch cached.
+// 1 GiB written, then read, between timed launches (KB_SCRUB=1): four times
+// the 256 MiB Infinity Cache, so a timed kernel starts with nothing of its
+// batch cached -- and, since the read pass evicts the write pass's dirty
+// lines (round 3's scrub only wrote: the timed kernel then paid for writing
+// back up to 256 MB of scrub lines, verify 241 -> 281 us), with no dirty line
+// of the scrub either.  The same protocol as bench.py's _scrub.
 __global__ void k_scrub(uint4* p, uint64_t n16, uint32_t seed)
 {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16;
          i += (uint64_t)gridDim.x * blockDim.x)
         p[i] = make_uint4((uint32_t)i, seed, (uint32_t)(i >> 32), ~seed);
 }
+__global__ void k_scrub_read(const uint4* p, uint64_t n16, uint32_t* sink)
+{
+    uint32_t acc = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 v = p[i];
+        acc ^= v.x ^ v.w;
+    }
+    if (acc == 0x9E3779B9u && sink) sink[0] = acc;
+}
 
 static uint4* g_scrub = nullptr;
-static const uint64_t kScrubBytes = 512ull << 20;
+static const uint64_t kScrubBytes = 1024ull << 20;
 
 static void scrub(hipStream_t s)
 {
     static uint32_t seed = 1;
     if (!g_scrub) return;
     hipLaunchKernelGGL(k_scrub, dim3(4096), dim3(256), 0, s, g_scrub, kScrubBytes / 16, seed++);
+    hipLaunchKernelGGL(k_scrub_read, dim3(4096), dim3(256), 0, s, g_scrub, kScrubBytes / 16,
+                       (uint32_t*)nullptr);
 }
 
 struct Variant {
@@ -155,6 +171,22 @@ __global__ void k_hdr_desc(uint8_t* buf, const uint64_t* off, const uint16_t* le
 }
 
 void run_variants(std::vector<Variant>& vs, hipStream_t s, int rounds);
+
+// The descriptor launches' fallback list (gcs_internal.h DescFb), one for the
+// whole tool: every variant runs on one stream at a time.
+static DescFb* kb_fb(u32 n)
+{
+    static DescFb fb;
+    if (fb.cap_frames < n) {
+        if (fb.d)
+            CK(hipFree(fb.d));
+        CK(hipMalloc(&fb.d, desc_fb_words(n) * 4));
+        CK(hipMemset(fb.d, 0, desc_fb_words(n) * 4));
+        fb.cap_frames = n;
+        fb.epoch = 0;
+    }
+    return &fb;
+}
 
 // IMIX read ceiling in the descriptor kernel's own block partition: block b
 // streams the packed region of descriptors [256b, 256b+256), [off[256b],
@@ -1199,6 +1231,328 @@ k_desc_ring_x(uint8_t* __restrict__ frames, uint64_t frames_bytes,
                                         flags, ext);
 }
 // ---------------------------------------------------------------------------
+// ROUND 3's SHIPPED prefix-sum stream (k_desc_stream before round 4: the class
+// passes of non-streamable blocks and slow frames inside the same kernel, 6 / 7
+// waves per SIMD; PIPE / PROBE were its A/B knobs), kept here as the baseline
+// the round-4 split (stream kernel + k_desc_fallback) is measured against on
+// the same box.
+template <int U_, int RMAX_, int OCC_, bool PIPE_ = false, int PROBE_ = 0, bool HDR3_ = false>
+struct StreamShapeR03 {
+    static constexpr bool HDR3 = HDR3_;   // RX: stash chunks 0..2 only (ihl = 5 fast frames)
+    static constexpr int U = U_;          // chunks per lane per trip (64 * U per wave)
+    static constexpr int RMAX = RMAX_;    // region chunks a streaming block may span
+    static constexpr int OCC = OCC_;
+    static constexpr bool PIPE = PIPE_;   // issue trip k+1's loads before folding trip k
+    static constexpr int PROBE = PROBE_;  // A/B (kbench): 1 = phase 2 loads only, 2 = no phase 3
+    static_assert(RMAX % 64 == 0 && RMAX <= 65536, "start chunks fit 16 bits");
+};
+
+template <class S, class T, bool COMPUTE, bool XCD>
+__device__ __forceinline__ void desc_stream_r03(uint8_t* __restrict__ frames, uint64_t frames_bytes,
+                                            const uint64_t* __restrict__ off,
+                                            const uint16_t* __restrict__ lens, u32 n,
+                                            uint8_t* __restrict__ out_code,
+                                            uint32_t* __restrict__ out_csum, u32 flags)
+{
+    static_assert(S::F == kBlock && S::R == 1, "one descriptor per thread");
+    static_assert(!COMPUTE || S::STAGE, "TX stages sector 0 in hdr");
+    constexpr int F = kBlock, NW = kBlock / 64, RW = T::RMAX / 64, U = T::U;
+    constexpr int NH = (!COMPUTE && T::HDR3) ? 3 : 4;   // header chunks stashed per frame
+    __shared__ uint64_t soff[F];
+    __shared__ uint16_t slen[F];
+    __shared__ uint16_t list[3][F];
+    __shared__ int cnt[3];
+    __shared__ int wcnt[3][NW];
+    __shared__ uint8_t codes[F];
+    __shared__ uint32_t csums[COMPUTE ? F : 1];
+    __shared__ uint4 hdr[NH * F];      // chunks 0..NH-1 per frame; TX: the staged sector 0
+    __shared__ uint64_t bm[RW];        // bit c: a frame starts at region chunk c
+    __shared__ uint16_t rbase[RW];     // frames starting before chunk 64 * w
+    __shared__ u32 meta[F];            // start chunk << 16 | len
+    __shared__ u32 pfirst[F];          // wave-local prefix at the first chunk
+    __shared__ u32 qend[F];            // wave-local Q(len)
+    __shared__ u32 wtot[NW];
+    __shared__ u32 nchunks_s;
+
+    const uint32_t blk = XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint64_t f0 = (uint64_t)blk * F;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int nf = (int)((n - f0) < (uint64_t)F ? (n - f0) : (uint64_t)F);
+    if (t < 3)
+        cnt[t] = 0;
+
+    // phase 0: validate, classify (for the list passes), test streamability
+    int cls = -1;
+    uint64_t o = 0;
+    u32 len = 0;
+    if (t < nf) {
+        o = off[f0 + t];
+        len = lens[f0 + t];
+        const bool ok = (o & 15) == 0 && o <= frames_bytes && len <= frames_bytes - o;
+        if (!ok) {
+            codes[t] = COMPUTE ? GCS_TX_BAD_DESC : GCS_V_BAD_DESC;
+            if (COMPUTE)
+                csums[t] = 0;
+        } else {
+            soff[t] = o;
+            slen[t] = (uint16_t)len;
+            cls = len <= (u32)S::T0 ? 0 : (len <= (u32)S::T1 ? 1 : 2);
+        }
+    }
+    const u32 nch = (len + 15) >> 4;
+    // streamability, and each frame's place in the region (chunks from frame
+    // 0's start): its first chunk and the next frame's (the last frame: NCH)
+    const uint64_t r0 = off[f0];
+    u32 start = 0, snext = 0;
+    bool sok = t >= nf || (cls >= 0 && len > 0);
+    if (sok && t < nf) {
+        if (o < r0 || ((o - r0) >> 4) + nch > (uint64_t)T::RMAX) {
+            sok = false;
+        } else {
+            start = (u32)((o - r0) >> 4);
+            if (t + 1 < nf) {
+                const uint64_t on = off[f0 + t + 1], e = o + 16ull * nch;
+                sok = on >= e && on - e <= 64;
+                snext = (u32)((on - r0) >> 4);
+            } else {
+                sok = o + 16ull * nch <= frames_bytes;
+                snext = start + nch;
+                nchunks_s = snext;
+            }
+        }
+    }
+    for (int r = t; r < RW; r += kBlock)
+        bm[r] = 0;
+    // the three ordered class lists (desc_mixed's phase 0, R = 1)
+    {
+        const uint64_t below = (1ull << lane) - 1;
+        int rank = 0;
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            const uint64_t m = __ballot(cls == c);
+            if (lane == 0)
+                wcnt[c][w] = __popcll(m);
+            if (cls == c)
+                rank = __popcll(m & below);
+        }
+        const bool stream = __syncthreads_and(sok);
+        if (!stream) {
+            if (cls >= 0) {
+                int base = 0;
+                for (int k = 0; k < w; k++)
+                    base += wcnt[cls][k];
+                list[cls][base + rank] = (uint16_t)t;
+            }
+            if (t < 3) {
+                int tot = 0;
+                for (int k = 0; k < NW; k++)
+                    tot += wcnt[t][k];
+                cnt[t] = tot;
+            }
+            __syncthreads();
+            const int n0 = cnt[0], n1 = cnt[1], n2 = cnt[2];
+            uint4* stg = COMPUTE ? hdr : nullptr;
+            if (n0) desc_class<S::G0, S::U0, COMPUTE, false, false, S::WM, S::K0, S::NT>(frames, frames_bytes, soff, slen, list[0], n0, flags, codes, csums, Ext{}, nullptr, nullptr, stg);
+            if (n1) desc_class<S::G1, S::U1, COMPUTE, false, false, S::WM, S::K1, S::NT>(frames, frames_bytes, soff, slen, list[1], n1, flags, codes, csums, Ext{}, nullptr, nullptr, stg);
+            if (n2) desc_class<S::G2, S::U2, COMPUTE, true, false, S::WM, 1, S::NT>(frames, frames_bytes, soff, slen, list[2], n2, flags, codes, csums, Ext{}, nullptr, nullptr, stg);
+            __syncthreads();
+            desc_tail<S, COMPUTE, false>(frames, frames_bytes, f0, n, soff, slen, codes, csums,
+                                         nullptr, nullptr, hdr, out_code, out_csum, flags, Ext{});
+            return;
+        }
+    }
+
+    // phase 1: the region's first-chunk bitmap, per-frame metadata, and per
+    // 64-chunk row the number of frames starting before it (frame t owns the
+    // rows r with start_t < 64 r <= start_t+1)
+    const u32 NCH = nchunks_s, NR = (NCH + 63) >> 6;
+    if (t < nf) {
+        meta[t] = start << 16 | len;
+#pragma unroll
+        for (int k = 0; k < NH; k++)
+            if ((u32)k >= nch)
+                hdr[NH * t + k] = make_uint4(0, 0, 0, 0);
+        atomicOr((unsigned long long*)&bm[start >> 6], 1ull << (start & 63));
+        const u32 rhi = t + 1 < nf ? snext >> 6 : NR - 1;
+        for (u32 r = (start >> 6) + 1; r <= rhi; r++)
+            rbase[r] = (uint16_t)(t + 1);
+    }
+    if (t == 0)
+        rbase[0] = 0;
+    __syncthreads();
+
+    // phase 2: wave w streams chunks [w*QW, (w+1)*QW) of the region
+    {
+        const u32 QW = ((NCH + 4 * 64 - 1) / (4 * 64)) * 64;
+        const u32 lo = w * QW, hi = (lo + QW < NCH) ? lo + QW : NCH;
+        const uint8_t* reg = frames + r0;
+        u32 run = 0;
+        auto load_trip = [&](u32 base, uint4 (&v)[U]) {
+#pragma unroll
+            for (int j = 0; j < U; j++) {
+                const u32 c = base + 64 * j + lane;
+                v[j] = c < hi ? ldg16<S::NT>(reg + 16ull * c) : make_uint4(0, 0, 0, 0);
+            }
+        };
+        auto fold_trip = [&](u32 base, const uint4 (&v)[U]) {
+            if constexpr (T::PROBE == 1) {
+                u32 x = 0;
+#pragma unroll
+                for (int j = 0; j < U; j++)
+                    x ^= v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
+                run += x;
+                return;
+            }
+#pragma unroll
+            for (int j = 0; j < U; j++) {
+                const u32 row = (base >> 6) + j;
+                if (64 * row >= hi)           // wave-uniform
+                    break;
+                const u32 c = 64 * row + lane;
+                const u32 s = hsum4(v[j]);
+                const u32 incl = wave_incl_scan(s);
+                const u32 excl = run + incl - s;
+                run += (u32)__builtin_amdgcn_readlane((int)incl, 63);
+                const uint64_t bits = bm[row];
+                const u32 below = __builtin_amdgcn_mbcnt_hi((u32)(bits >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((u32)bits, 0u));
+                const int f = (int)rbase[row] + (int)below + (int)((bits >> lane) & 1u) - 1;
+                if (c < hi) {
+                    const u32 m = meta[f], fl = m & 0xFFFFu;
+                    const u32 k = c - (m >> 16), fn = (fl + 15) >> 4;
+                    if (k < (u32)NH && k < fn)
+                        hdr[NH * f + k] = v[j];
+                    if (k == 0)
+                        pfirst[f] = excl;
+                    if (k + 1 == fn)
+                        qend[f] = excl + chunk_prefix_sum(v[j], (int)(fl - 16 * k));
+                }
+            }
+        };
+        if constexpr (T::PIPE) {
+            uint4 v[U], vn[U];
+            if (lo < hi)
+                load_trip(lo, v);
+            for (u32 base = lo; base < hi; base += 64 * U) {
+                const u32 nb = base + 64 * U;
+                if (nb < hi)
+                    load_trip(nb, vn);
+                fold_trip(base, v);
+#pragma unroll
+                for (int j = 0; j < U; j++)
+                    v[j] = vn[j];
+            }
+        } else {
+            for (u32 base = lo; base < hi; base += 64 * U) {
+                uint4 v[U];
+                load_trip(base, v);
+                fold_trip(base, v);
+            }
+        }
+        if (lane == 0)
+            wtot[w] = run;
+    }
+    __syncthreads();
+
+    if constexpr (T::PROBE != 0) {
+        if (t == 0 && wtot[0] == 0x9E3779B9u)
+            out_code[f0] = 0xEE;              // keeps the probe's loads alive
+        if constexpr (T::PROBE == 2)
+            return;
+    }
+    // phase 3: one lane per frame
+    {
+        const u32 QW = ((NCH + 4 * 64 - 1) / (4 * 64)) * 64;
+        const int tf = t < nf ? t : 0;
+        const uint4 h4[4] = {hdr[NH * tf], hdr[NH * tf + 1], hdr[NH * tf + 2],
+                             NH == 4 ? hdr[NH * tf + 3] : make_uint4(0, 0, 0, 0)};
+        Hdr h;
+        h.d3 = h4[0].w;
+        h.d4 = h4[1].x;
+        h.d5 = h4[1].y;
+        const int ihl = (int)((h.d3 >> 16) & 15u);
+        const int ts = 14 + 4 * ihl;
+        const int te = 14 + (int)bswap16(h.d4 & 0xFFFFu);
+        // NH = 3 (RX): chunk 3 is not stashed; words [48, te) come from the
+        // prefixes, and doff (byte ts + 12) must lie in chunk 2: ihl == 5
+        constexpr int HB = 16 * NH;                  // header bytes held per frame
+        const bool fast = t < nf && (NH == 4 ? ihl <= 8 : ihl == 5) &&
+                          (te <= HB || te == (int)len);
+        // wave-uniform: every fast frame of the wave has ihl == 5, so the word
+        // masks of the stashed chunks are constants (masks5, as the group
+        // kernels); and when every one also has te >= HB, no segment end lies
+        // in them
+        const bool all5 = __all(!fast || ihl == 5);
+        const bool end64 = __all(!fast || te >= HB);
+        // RX: fast frames' verdicts go straight out (coalesced, frame order)
+        uint8_t* oc = (!COMPUTE && out_code) ? out_code + f0 + t : codes + t;
+        if (t < nf && !fast) {
+            list[2][atomicAdd(&cnt[2], 1)] = (uint16_t)t;
+        } else if (fast) {
+            Acc a = {0u, 0u, 0u};
+            if (all5 && end64) {
+#pragma unroll
+                for (int c = 0; c < NH; c++)
+                    accum_fast5<COMPUTE, true>(h4[c], c, HB, masks5<COMPUTE>(c), a);
+            } else if (all5) {
+#pragma unroll
+                for (int c = 0; c < NH; c++)
+                    accum_fast5<COMPUTE, true>(h4[c], c, te < HB ? te : HB, masks5<COMPUTE>(c), a);
+            } else {
+#pragma unroll
+                for (int j = 0; j < NH; j++)
+                    accum_chunk<COMPUTE>(h4[j], 16 * j, ts, te < HB ? te : HB, a);
+            }
+            if (te > HB) {
+                auto wbase = [&](u32 c) {
+                    const u32 q = c / QW;
+                    u32 b = 0;
+#pragma unroll
+                    for (int k = 0; k < NW - 1; k++)
+                        b += (u32)k < q ? wtot[k] : 0u;
+                    return b;
+                };
+                const u32 p0 = pfirst[t] + wbase(start);
+                const u32 p1 = qend[t] + wbase(start + nch - 1);
+                a.tcp += (p1 - p0) - (hsum4(h4[0]) + hsum4(h4[1]) + hsum4(h4[2]) +
+                                      (NH == 4 ? hsum4(h4[3]) : 0u));
+            }
+            epilogue<1, 4, COMPUTE, S::WM, false>(
+                h, a, frames + o, len, (int64_t)(frames_bytes - o), true, 0, flags, oc,
+                COMPUTE ? csums + t : nullptr, true, h4, XFrame{},
+                COMPUTE ? reinterpret_cast<uint8_t*>(hdr + 4 * t) : nullptr);
+        }
+    }
+    __syncthreads();
+    const int ns = cnt[2];
+    if (ns)
+        desc_class<S::G2, S::U2, COMPUTE, true, false, S::WM, 1, S::NT>(
+            frames, frames_bytes, soff, slen, list[2], ns, flags, codes, csums, Ext{}, nullptr,
+            nullptr, COMPUTE ? hdr : nullptr);
+    if constexpr (COMPUTE) {
+        __syncthreads();
+        desc_tail<S, COMPUTE, false>(frames, frames_bytes, f0, n, soff, slen, codes, csums,
+                                     nullptr, nullptr, hdr, out_code, out_csum, flags, Ext{});
+    } else if (ns && out_code) {
+        __syncthreads();
+        for (int i = t; i < ns; i += kBlock) {
+            const int ft = list[2][i];
+            out_code[f0 + ft] = codes[ft];
+        }
+    }
+}
+
+template <class S, class T, bool COMPUTE, bool XCD>
+__global__ void __launch_bounds__(kBlock, T::OCC)
+k_desc_stream_r03(uint8_t* __restrict__ frames, uint64_t frames_bytes,
+              const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens, u32 n,
+              uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags)
+{
+    desc_stream_r03<S, T, COMPUTE, XCD>(frames, frames_bytes, off, lens, n, out_code, out_csum, flags);
+}
+
+
+// ---------------------------------------------------------------------------
 // round 3: k_desc_stream with one wave per block (64 frames), measured against the
 // shipped 256-thread stream on the same boxes: verify 244-249 vs 248-256 us (box
 // noise decides), fill 373 vs 359-361 us; U8 spills at 6 waves (423 us).  Not shipped.
@@ -1479,7 +1833,7 @@ int imix_main(uint64_t n, int rounds)
     hipLaunchKernelGGL(k_init, dim3(4096), dim3(256), 0, s, tx, total / 64, (uint64_t)64, 64u);
     hipLaunchKernelGGL(k_hdr_desc, dim3((n + 255) / 256), dim3(256), 0, s, tx, doff, dlen, n);
     CK(hipMemcpyAsync(rx, tx, total, hipMemcpyDeviceToDevice, s));
-    CK(launch_compute_desc(rx, total, doff, dlen, (u32)n, nullptr, nullptr, 0, s));
+    CK(launch_compute_desc(rx, total, doff, dlen, (u32)n, nullptr, nullptr, 0, kb_fb(1u << 24), s));
     CK(hipStreamSynchronize(s));
     int dev = 0, cus = 0;
     CK(hipGetDevice(&dev));
@@ -1488,302 +1842,72 @@ int imix_main(uint64_t n, int rounds)
                 total / 1e9, (double)bytes / n);
     const double vb = bytes + n * (1.0 + 10.0), cb = bytes + n * (4.0 + 10.0);
     std::vector<Variant> vs;
-    vs.push_back({"verify  k_desc<16,2> (one group size)", vb, [&](hipStream_t st) {
-        hipLaunchKernelGGL((k_desc<16, 2, false, true, WM_SECTOR_SC1>), dim3((n + 15) / 16),
-                           dim3(256), 0, st, rx, total, doff, dlen, (u32)n, v1, nullptr, 0u);
-    }});
-    vs.push_back({"compute k_desc<16,2> (one group size)", cb, [&](hipStream_t st) {
-        hipLaunchKernelGGL((k_desc<16, 2, true, true, WM_SECTOR_SC1>), dim3((n + 15) / 16),
-                           dim3(256), 0, st, tx, total, doff, dlen, (u32)n, nullptr, nullptr, 0u);
-    }});
-#define MIXED(C_, OCC_, TAG, ...)                                                          \
-    vs.push_back({std::string(C_ ? "compute" : "verify ") + " mixed occ " + TAG,            \
-                  C_ ? cb : vb, [&](hipStream_t st) {                                      \
-        using S_ = DescShape<__VA_ARGS__>;                                                  \
-        hipLaunchKernelGGL((k_desc_mixed<S_, C_, true, OCC_>),                              \
-                           dim3((n + S_::F - 1) / S_::F), dim3(256), 0, st, C_ ? tx : rx, total, \
-                           doff, dlen, (u32)n, C_ ? nullptr : v1, nullptr,                  \
-                           std::string(TAG).find("no write") != std::string::npos           \
-                               ? (u32)GCS_CF_NO_INPLACE : 0u);                              \
-    }});
-    // round 2b: staged sector write-back (shipped: STAGE nt)
-    MIXED(true, 6, "6 epilogue sectors sc1 (round 1)", 4, 1, 16, 3, 32, 3)
-    MIXED(true, 6, "6 STAGE nt (shipped)", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true)
-    MIXED(true, 6, "6 no write-back", 4, 1, 16, 3, 32, 3)
-    // temporal frame loads: a 128 B line split between frames of two classes
-    // (64 B packing) may stay in L2 for the second pass
-    MIXED(false, 6, "6 verify NT loads (shipped)", 4, 1, 16, 3, 32, 3)
-    MIXED(false, 6, "6 verify temporal loads", 4, 1, 16, 3, 32, 3, kWM, 256, true, 1, 1, false, false)
-    // descriptors per block: the three class passes walk a smaller region
-    MIXED(false, 6, "6 verify F=512", 4, 1, 16, 3, 32, 3, kWM, 512, true, 1, 1, false, true)
-    MIXED(true, 6, "6 STAGE nt, temporal loads F=512", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 512, true, 1, 1, true, false)
-    MIXED(true, 5, "5 STAGE nt, temporal loads F=512", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 512, true, 1, 1, true, false)
-    MIXED(false, 6, "6 verify F=128", 4, 1, 16, 3, 32, 3, kWM, 128, true, 1, 1, false, true)
-    MIXED(false, 6, "6 verify F=64", 4, 1, 16, 3, 32, 3, kWM, 64, true, 1, 1, false, true)
-    MIXED(true, 6, "6 STAGE nt, temporal loads F=128", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 128, true, 1, 1, true, false)
-    MIXED(true, 6, "6 STAGE nt, temporal loads F=64", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 64, true, 1, 1, true, false)
-    MIXED(true, 6, "6 STAGE nt, temporal loads", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true, false)
-    // fresh IMIX TX batches: check fields zeroed (untimed) before every launch
-    vs.push_back({"compute desc (launch_compute_desc) FRESH checks", cb, [&](hipStream_t st) {
-        CK(launch_compute_desc(tx, total, doff, dlen, (u32)n, nullptr, nullptr, 0u, st));
-    }});
-    vs.back().prep = [&](hipStream_t st) {
-        hipLaunchKernelGGL(k_zero_checks_desc, dim3((n + 255) / 256), dim3(256), 0, st, tx, doff, dlen, n);
+    // round 4: the stream kernel without the class passes (k_desc_fallback
+    // takes the blocks it hands on), against round 3's kernel on this box
+    DescFb& fb = *kb_fb((u32)n);
+    auto zero_prep = [&](hipStream_t st) {
+        hipLaunchKernelGGL(k_zero_checks_desc, dim3((n + 255) / 256), dim3(256), 0, st, tx, doff,
+                           dlen, n);
     };
-    vs.push_back({"compute mixed no write-back FRESH checks", cb, [&](hipStream_t st) {
-        CK(launch_compute_desc(tx, total, doff, dlen, (u32)n, nullptr, nullptr, (u32)GCS_CF_NO_INPLACE, st));
+    vs.push_back({"verify  desc (launch_verify_desc, shipped)", vb, [&](hipStream_t st) {
+        CK(launch_verify_desc(rx, total, doff, dlen, (u32)n, v1, 0u, &fb, st));
     }});
-    vs.back().prep = vs[vs.size() - 2].prep;
-    // round 2e: re-read each staged sector (line into L2) right before its store
-    MIXED(true, 6, "6 STAGE nt, temporal loads, RELOAD temporal", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true, false, 1)
-    MIXED(true, 6, "6 STAGE nt, temporal loads, RELOAD nt", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true, false, 2)
-    MIXED(true, 6, "6 STAGE nt, nt loads, RELOAD temporal", 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true, true, 1)
-    MIXED(true, 6, "6 STAGE sc1, temporal loads, RELOAD temporal", 4, 1, 16, 3, 32, 3, WM_SECTOR_SC1, 256, true, 1, 1, true, false, 1)
-    // round 2c: the block's packed region streamed through an LDS ring
-#define RINGP(C_, OCC_, TAG, W_, NIF_, LNT_, PR_, ...)                                     \
-    vs.push_back({std::string(C_ ? "compute" : "verify ") + " ring " + TAG,                 \
+    vs.push_back({"compute desc (launch_compute_desc, shipped) FRESH", cb, [&](hipStream_t st) {
+        CK(launch_compute_desc(tx, total, doff, dlen, (u32)n, nullptr, nullptr, 0u, &fb, st));
+    }});
+    vs.back().prep = zero_prep;
+    vs.push_back({"compute desc (launch_compute_desc, shipped) refill", cb, [&](hipStream_t st) {
+        CK(launch_compute_desc(tx, total, doff, dlen, (u32)n, nullptr, nullptr, 0u, &fb, st));
+    }});
+    vs.push_back({"compute desc no write-back (GCS_CF_NO_INPLACE)", cb, [&](hipStream_t st) {
+        CK(launch_compute_desc(tx, total, doff, dlen, (u32)n, nullptr, nullptr,
+                               (u32)GCS_CF_NO_INPLACE, &fb, st));
+    }});
+    vs.push_back({"fallback kernel alone (nothing listed)", 0.0, [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_desc_fallback<false>), dim3(kFbGrid), dim3(256), 0, st, rx, total,
+                           doff, dlen, (u32)n, v1, nullptr, 0u, (const uint32_t*)fb.d,
+                           0xFFFFFFFFu);
+    }});
+#define STREAM4(C_, TAG, U_, RMAX_, OCC_, WM_)                                              \
+    vs.push_back({std::string(C_ ? "compute" : "verify ") + " stream4 " + TAG,              \
                   C_ ? cb : vb, [&](hipStream_t st) {                                      \
-        using S_ = DescShape<__VA_ARGS__>;                                                  \
-        using R_ = RingShape<W_, NIF_, LNT_, 4, PR_>;                                       \
-        hipLaunchKernelGGL((k_desc_ring<S_, R_, C_, true, OCC_>), dim3((n + 255) / 256),    \
+        using T_ = StreamShape<U_, RMAX_, OCC_, C_ ? 4 : 3>;                               \
+        if (++fb.epoch == 0) fb.epoch = 1;                                                  \
+        hipLaunchKernelGGL((k_desc_stream<T_, C_, WM_, true>), dim3((n + 255) / 256),      \
                            dim3(256), 0, st, C_ ? tx : rx, total, doff, dlen, (u32)n,       \
-                           C_ ? nullptr : v1, nullptr, 0u);                                 \
-    }});
-#define RING(C_, OCC_, TAG, W_, NIF_, LNT_, ...) RINGP(C_, OCC_, TAG, W_, NIF_, LNT_, 0, __VA_ARGS__)
-    if (getenv("KB_RING")) {
-    RING(false, 4, "W8K NIF2 occ4", 8192, 2, true, 4, 1, 16, 3, 32, 3)
-    RINGP(false, 4, "W8K NIF2 occ4 PROBE no fold", 8192, 2, true, 1, 4, 1, 16, 3, 32, 3)
-    RINGP(false, 4, "W8K NIF2 occ4 PROBE no DMA", 8192, 2, true, 2, 4, 1, 16, 3, 32, 3)
-    RINGP(false, 4, "W16K NIF2 occ4 PROBE no fold", 16384, 2, true, 1, 4, 1, 16, 3, 32, 3)
-    RING(true, 2, "W8K NIF2 occ2 temporal", 8192, 2, false, 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true, false)
-    RINGP(true, 2, "W8K NIF2 occ2 PROBE no DMA", 8192, 2, false, 2, 4, 1, 16, 3, 32, 3, WM_SECTOR_NT, 256, true, 1, 1, true, false)
-    }
-    // round 2d: one frame per lane out of an LDS copy of the block's region
-#define LANE(C_, TAG, F_, CAP_, LNT_)                                                      \
-    vs.push_back({std::string(C_ ? "compute" : "verify ") + " lane " + TAG,                 \
+                           C_ ? nullptr : v1, nullptr, 0u, fb.d, fb.epoch);                 \
+        hipLaunchKernelGGL((k_desc_fallback<C_>), dim3(kFbGrid), dim3(256), 0, st,          \
+                           C_ ? tx : rx, total, doff, dlen, (u32)n, C_ ? nullptr : v1,      \
+                           nullptr, 0u, (const uint32_t*)fb.d, fb.epoch);                   \
+    }});                                                                                    \
+    if (C_)                                                                                 \
+        vs.back().prep = zero_prep;
+    STREAM4(false, "U4 R8K occ8", 4, 8192, 8, WM_SECTOR_SC1)
+    STREAM4(true, "U4 R8K occ8 sc1 FRESH", 4, 8192, 8, WM_SECTOR_SC1)
+    STREAM4(true, "U8 R8K occ8 nt FRESH", 8, 8192, 8, WM_SECTOR_NT)
+    STREAM4(true, "U8 R8K occ8 plain FRESH", 8, 8192, 8, WM_SECTOR)
+    STREAM4(true, "U8 R12K occ7 sc1 FRESH", 8, 12288, 7, WM_SECTOR_SC1)
+#define STREAM3(C_, TAG, OCC_, HDR3_)                                                       \
+    vs.push_back({std::string(C_ ? "compute" : "verify ") + " stream r03 " + TAG,           \
                   C_ ? cb : vb, [&](hipStream_t st) {                                      \
-        using L_ = LaneShape<F_, CAP_, LNT_, WM_SECTOR_NT>;                                 \
-        hipLaunchKernelGGL((k_desc_lane<L_, C_, true>), dim3((n + F_ - 1) / F_), dim3(64),  \
-                           0, st, C_ ? tx : rx, total, doff, dlen, (u32)n,                  \
-                           C_ ? nullptr : v1, nullptr, 0u);                                 \
-    }});
-    if (getenv("KB_LANE")) {
-    LANE(false, "F64 CAP32K nt", 64, 32768, true)
-    LANE(false, "F32 CAP16K nt", 32, 16384, true)
-    LANE(false, "F64 CAP32K temporal", 64, 32768, false)
-    LANE(true, "F64 CAP32K temporal", 64, 32768, false)
-    LANE(true, "F64 CAP32K nt", 64, 32768, true)
-    LANE(true, "F32 CAP16K temporal", 32, 16384, false)
-    }
-    // round 3: the list passes' loads alone (DescShape PROBE = 1): access pattern vs fold
-    MIXED(false, 6, "6 PROBE loads only", 4, 1, 16, 3, 32, 3, kWM, 256, true, 1, 1, false, true, 0, 1)
-    MIXED(false, 6, "6 PROBE loads only, temporal", 4, 1, 16, 3, 32, 3, kWM, 256, true, 1, 1, false, false, 0, 1)
-    MIXED(false, 6, "6 PROBE loads only K3/K2", 4, 1, 16, 3, 32, 3, kWM, 256, true, 3, 2, false, true, 0, 1)
-    MIXED(false, 8, "8 PROBE loads only", 4, 1, 16, 3, 32, 3, kWM, 256, true, 1, 1, false, true, 0, 1)
-    MIXED(false, 6, "6 PROBE loads only F=512", 4, 1, 16, 3, 32, 3, kWM, 512, true, 1, 1, false, true, 0, 1)
-    vs.push_back({"verify  mixed PROBE loads only, 6 blocks/CU (LDS pad)", vb, [&](hipStream_t st) {
-        using S_ = DescShape<4, 1, 16, 3, 32, 3, kWM, 256, true, 1, 1, false, true, 0, 1>;
-        hipLaunchKernelGGL((k_desc_mixed<S_, false, true, 6>), dim3((n + 255) / 256), dim3(256),
-                           22 * 1024, st, rx, total, doff, dlen, (u32)n, v1, nullptr, 0u);
-    }});
-    vs.push_back({"verify  mixed shipped, 6 blocks/CU (LDS pad)", vb, [&](hipStream_t st) {
-        using S_ = DescShip<false>;
-        hipLaunchKernelGGL((k_desc_mixed<S_, false, true, 6>), dim3((n + 255) / 256), dim3(256),
-                           22 * 1024, st, rx, total, doff, dlen, (u32)n, v1, nullptr, 0u);
-    }});
-    // round 3: the shared-line (EDGE) list variant -- lines shared by neighbouring
-    // frames of different classes read once into LDS -- measured 350-356 us verify,
-    // 451-531 us fill (its loads alone 247 vs 251 us); removed from the kernels
-    // round 3: class-split blocks (k_desc_part): one class of one tile per block
-#define PART(C_, OCC_, TAG, NT_, WM_, ...)                                                 \
-    vs.push_back({std::string(C_ ? "compute" : "verify ") + " part " + TAG,                 \
-                  C_ ? cb : vb, [&](hipStream_t st) {                                      \
-        using P_ = PartShape<__VA_ARGS__>;                                                  \
-        hipLaunchKernelGGL((k_desc_part<P_, C_, false, WM_, NT_, OCC_>), part_grid<P_>((u32)n), \
-                           dim3(256), 0, st, C_ ? tx : rx, total, doff, dlen, (u32)n,       \
-                           C_ ? nullptr : v1, nullptr, 0u, Ext{});                          \
-    }});
-    if (getenv("KB_PART")) {   // measured r03: 339-435 us verify (per-block fixed costs)
-    PART(false, 6, "768/256k2/96k2/128 occ6", true, kWM, 768, 256, 2, 96, 2, 128)
-    PART(false, 6, "768/256k2/128k2/192 occ6", true, kWM, 768, 256, 2, 128, 2, 192)
-    PART(true, 6, "768/256k2/96k2/128 occ6 sector nt", false, WM_SECTOR_NT, 768, 256, 2, 96, 2, 128)
-    }
-    // round 3: a block's whole region through LDS (k_desc_region)
-#define REGION(C_, TAG, WM_, ...)                                                          \
-    vs.push_back({std::string(C_ ? "compute" : "verify ") + " region " + TAG,               \
-                  C_ ? cb : vb, [&](hipStream_t st) {                                      \
-        using R_ = RegionShape<__VA_ARGS__>;                                                \
-        hipLaunchKernelGGL((k_desc_region<R_, C_, false, WM_>), dim3((n + R_::F - 1) / R_::F), \
-                           dim3(256), 0, st, C_ ? tx : rx, total, doff, dlen, (u32)n,       \
-                           C_ ? nullptr : v1, nullptr, 0u, Ext{});                          \
-    }});
-    if (getenv("KB_REGION")) {   // measured r03: 501-783 us verify, 546-742 us fill (the fold
-                                 // from LDS: 4-way bank conflicts, group-divergent loops)
-    REGION(false, "F64 CAP32K G4 nt", kWM, 64, 32768, 4, true)
-    REGION(false, "F48 CAP24K G4 nt", kWM, 48, 24576, 4, true)
-    REGION(true, "F64 CAP32K G4 nt, sector nt", WM_SECTOR_NT, 64, 32768, 4, true)
-    }
-    // round 3b: global class partition + homogeneous passes (KB_GPART)
-    uint64_t* gent = nullptr;
-    uint32_t *gidx = nullptr, *gcnt = nullptr;
-    uint32_t hcnt[4] = {0, 0, 0, 0};
-    if (getenv("KB_GPART")) {
-        CK(hipMalloc(&gent, 8 * 4 * n));
-        CK(hipMalloc(&gidx, 4 * 4 * n));
-        CK(hipMalloc(&gcnt, 16));
-        CK(hipMemsetAsync(gcnt, 0, 16, s));
-        hipLaunchKernelGGL(k_class_part, dim3((n + 255) / 256), dim3(256), 0, s, doff, dlen, (u32)n,
-                           576u, 1536u, gent, gidx, gcnt, (u32)n);
-        CK(hipMemcpyAsync(hcnt, gcnt, 16, hipMemcpyDeviceToHost, s));
-        CK(hipStreamSynchronize(s));
-        std::printf("classes: %u %u %u %u\n", hcnt[0], hcnt[1], hcnt[2], hcnt[3]);
-        auto passes = [&, n](hipStream_t st, bool C, int v2) {
-            uint8_t* fr = C ? tx : rx;
-            uint8_t* oc = C ? nullptr : v1;
-            const u32 n0 = hcnt[0], n1 = hcnt[1], n2 = hcnt[2];
-            if (n0)
-                hipLaunchKernelGGL((C ? k_list_small<true> : k_list_small<false>), dim3((n0 + 255) / 256),
-                                   dim3(256), 0, st, fr, total, gent, gidx, n0, oc, nullptr, 0u);
-            if (n1) {
-                if (v2 == 0)
-                    hipLaunchKernelGGL((C ? k_list<16, 3, true, WM_SECTOR_SC1> : k_list<16, 3, false, WM_SECTOR_SC1>),
-                                       dim3((n1 + 15) / 16), dim3(256), 0, st, fr, total, gent + n,
-                                       gidx + n, n1, oc, nullptr, 0u);
-                else
-                    hipLaunchKernelGGL((C ? k_list<8, 5, true, WM_SECTOR_SC1> : k_list<8, 5, false, WM_SECTOR_SC1>),
-                                       dim3((n1 + 31) / 32), dim3(256), 0, st, fr, total, gent + n,
-                                       gidx + n, n1, oc, nullptr, 0u);
-            }
-            if (n2)
-                hipLaunchKernelGGL((C ? k_list<32, 3, true, WM_SECTOR_SC1> : k_list<32, 3, false, WM_SECTOR_SC1>),
-                                   dim3((n2 + 7) / 8), dim3(256), 0, st, fr, total, gent + 2 * n,
-                                   gidx + 2 * n, n2, oc, nullptr, 0u);
-        };
-        auto part = [&, n](hipStream_t st) {
-            CK(hipMemsetAsync(gcnt, 0, 16, st));
-            hipLaunchKernelGGL(k_class_part, dim3((n + 255) / 256), dim3(256), 0, st, doff, dlen,
-                               (u32)n, 576u, 1536u, gent, gidx, gcnt, (u32)n);
-        };
-        vs.push_back({"verify  gpart passes only 64|16x3|32x3", vb, [=](hipStream_t st) { passes(st, false, 0); }});
-        vs.push_back({"verify  gpart passes only 64|8x5|32x3", vb, [=](hipStream_t st) { passes(st, false, 1); }});
-        vs.push_back({"verify  gpart partition + passes 64|16x3|32x3", vb, [=](hipStream_t st) { part(st); passes(st, false, 0); }});
-        vs.push_back({"verify  gpart partition alone", vb, [=](hipStream_t st) { part(st); }});
-        vs.push_back({"compute gpart passes only 64|16x3|32x3", cb, [=](hipStream_t st) { passes(st, true, 0); }});
-        vs.push_back({"compute gpart partition + passes FRESH", cb, [=](hipStream_t st) { part(st); passes(st, true, 0); }});
-        vs.back().prep = [&](hipStream_t st) {
-            hipLaunchKernelGGL(k_zero_checks_desc, dim3((n + 255) / 256), dim3(256), 0, st, tx, doff, dlen, n);
-        };
-    }
-    // round 3c: the region as a prefix-sum stream (k_desc_stream)
-#define STREAMV(C_, TAG, U_, RMAX_, OCC_, NT_, PIPE_, PROBE_)                               \
-    vs.push_back({std::string(C_ ? "compute" : "verify ") + " stream " + TAG,               \
-                  C_ ? cb : vb, [&](hipStream_t st) {                                      \
-        using S_ = DescShape<4, 1, 16, 3, 32, 3, C_ ? WM_SECTOR_NT : kWM, 256, true, 1, 1,  \
-                             C_, NT_>;                                                     \
-        using T_ = StreamShape<U_, RMAX_, OCC_, PIPE_, PROBE_>;                            \
-        hipLaunchKernelGGL((k_desc_stream<S_, T_, C_, true>), dim3((n + 255) / 256),       \
+        using S_ = DescShape<4, 1, 16, 3, 32, 3, WM_SECTOR_SC1, 256, true, 1, 1, C_, true>; \
+        using T_ = StreamShapeR03<8, 12288, OCC_, false, 0, HDR3_>;                        \
+        hipLaunchKernelGGL((k_desc_stream_r03<S_, T_, C_, true>), dim3((n + 255) / 256),   \
                            dim3(256), 0, st, C_ ? tx : rx, total, doff, dlen, (u32)n,       \
                            C_ ? nullptr : v1, nullptr, 0u);                                 \
     }});                                                                                    \
     if (C_)                                                                                 \
-        vs.back().prep = [&](hipStream_t st) {                                              \
-            hipLaunchKernelGGL(k_zero_checks_desc, dim3((n + 255) / 256), dim3(256), 0, st, \
-                               tx, doff, dlen, n);                                          \
-        };
-    // measured r03 (first version, general masks in phase 3): U8/U4 occ5 nt 281/282 us,
-    // temporal 283, occ4 276, PIPE (next trip's loads before the fold) 282/292, phases
-    // 0-2 alone 251 (list kernel 278-286); fill nt FRESH 325-366 (temporal 374; list
-    // kernel 385-431 on the same boxes)
-    // second version (fast5 phase 3, one barrier less), occ 6: verify 253 / 255 (U8 / U4),
-    // U4 phases 0-2 alone 238, read ceiling 230; fill FRESH 359-361 (list kernel 428);
-    // third (direct RX verdicts, constant te): 258 / 259, phases 0-2 247 (ceiling 239)
-    STREAMV(false, "U8 occ6 R12K nt (shipped)", 8, 12288, 6, true, false, 0)
-#define STREAMH3(TAG, OCC_)                                                                 \
-    vs.push_back({"verify  stream HDR3 " TAG, vb, [&](hipStream_t st) {                     \
-        using S_ = DescShape<4, 1, 16, 3, 32, 3, kWM, 256, true, 1, 1, false, true>;        \
-        using T_ = StreamShape<8, 12288, OCC_, false, 0, true>;                            \
-        hipLaunchKernelGGL((k_desc_stream<S_, T_, false, true>), dim3((n + 255) / 256),    \
-                           dim3(256), 0, st, rx, total, doff, dlen, (u32)n, v1, nullptr, 0u); \
-    }});
-    STREAMH3("occ6", 6) STREAMH3("occ7", 7) STREAMH3("occ8", 8)
-    STREAMV(true, "U8 occ6 R12K nt FRESH (shipped)", 8, 12288, 6, true, false, 0)
-    // the fill's staged write-back policy (shipped: nt)
-#define STREAMWM(TAG, WM_)                                                                  \
-    vs.push_back({"compute stream WM " TAG " FRESH", cb, [&](hipStream_t st) {               \
-        using S_ = DescShape<4, 1, 16, 3, 32, 3, WM_, 256, true, 1, 1, true, true>;          \
-        hipLaunchKernelGGL((k_desc_stream<S_, StreamShape<8, 12288, 6>, true, true>),      \
-                           dim3((n + 255) / 256), dim3(256), 0, st, tx, total, doff, dlen,  \
-                           (u32)n, nullptr, nullptr, 0u);                                   \
-    }});                                                                                    \
-    vs.back().prep = [&](hipStream_t st) {                                                  \
-        hipLaunchKernelGGL(k_zero_checks_desc, dim3((n + 255) / 256), dim3(256), 0, st, tx,  \
-                           doff, dlen, n);                                                  \
-    };
-    STREAMWM("sc1", WM_SECTOR_SC1) STREAMWM("plain", WM_SECTOR) STREAMWM("sc0sc1", WM_SECTOR_SC01)
-#define STREAMWMT(TAG, WM_)                                                                 \
-    vs.push_back({"compute stream WM " TAG " temporal loads FRESH", cb, [&](hipStream_t st) { \
-        using S_ = DescShape<4, 1, 16, 3, 32, 3, WM_, 256, true, 1, 1, true, false>;         \
-        hipLaunchKernelGGL((k_desc_stream<S_, StreamShape<8, 12288, 6>, true, true>),      \
-                           dim3((n + 255) / 256), dim3(256), 0, st, tx, total, doff, dlen,  \
-                           (u32)n, nullptr, nullptr, 0u);                                   \
-    }});                                                                                    \
-    vs.back().prep = [&](hipStream_t st) {                                                  \
-        hipLaunchKernelGGL(k_zero_checks_desc, dim3((n + 255) / 256), dim3(256), 0, st, tx,  \
-                           doff, dlen, n);                                                  \
-    };
-    STREAMWMT("sc1", WM_SECTOR_SC1) STREAMWMT("sc0sc1", WM_SECTOR_SC01)
-    // one wave per block, 64 frames (k_desc_wstream)
-#define WSTREAMV(C_, TAG, U_, RMAX_, OCC_)                                                  \
-    vs.push_back({std::string(C_ ? "compute" : "verify ") + " wstream " + TAG,              \
-                  C_ ? cb : vb, [&](hipStream_t st) {                                      \
-        using S_ = DescShape<4, 1, 16, 3, 32, 3, C_ ? WM_SECTOR_NT : kWM, 64, true, 1, 1,   \
-                             C_, true>;                                                    \
-        using T_ = WStreamShape<U_, RMAX_, OCC_>;                                          \
-        hipLaunchKernelGGL((k_desc_wstream<S_, T_, C_, true>), dim3((n + 63) / 64),        \
-                           dim3(64), 0, st, C_ ? tx : rx, total, doff, dlen, (u32)n,        \
-                           C_ ? nullptr : v1, nullptr, 0u);                                 \
-    }});                                                                                    \
-    if (C_)                                                                                 \
-        vs.back().prep = [&](hipStream_t st) {                                              \
-            hipLaunchKernelGGL(k_zero_checks_desc, dim3((n + 255) / 256), dim3(256), 0, st, \
-                               tx, doff, dlen, n);                                          \
-        };
-    // measured: U8 occ6 (23 VGPRs spilled) 423, U4 occ6 (10 spilled) 249, U4 "occ8"
-    // (the compiler's 96 VGPRs, 5 waves) 244 vs the 256-thread stream 256 on one box
-    // (read ceiling 219); fill U4 occ6 374 vs 361.  Second box: U4 occ4 / occ5 / U2 /
-    // U8 occ4 249 / 256 / 272 / 258 vs the shipped stream 248; fills 373-374 vs 359
-    WSTREAMV(false, "U4 occ5 R6K", 4, 6144, 5)
-    WSTREAMV(false, "U2 occ5 R6K", 2, 6144, 5)
-    WSTREAMV(false, "U8 occ4 R6K", 8, 6144, 4)
-    WSTREAMV(false, "U4 occ4 R6K", 4, 6144, 4)
-    WSTREAMV(true, "U4 occ5 R6K FRESH", 4, 6144, 5)
-    WSTREAMV(true, "U2 occ5 R6K FRESH", 2, 6144, 5)
-    WSTREAMV(true, "U4 occ4 R6K FRESH", 4, 6144, 4)
-    vs.push_back({"verify  desc (launch_verify_desc)", vb, [&](hipStream_t st) {
-        CK(launch_verify_desc(rx, total, doff, dlen, (u32)n, v1, 0u, st));
-    }});
-    vs.push_back({"compute desc (launch_compute_desc)", cb, [&](hipStream_t st) {
-        CK(launch_compute_desc(tx, total, doff, dlen, (u32)n, nullptr, nullptr, 0u, st));
-    }});
+        vs.back().prep = zero_prep;
+    STREAM3(false, "HDR3 occ7 (shipped r03)", 7, true)
+    STREAM3(true, "occ6 FRESH (shipped r03)", 6, false)
 #define RREG(U_)                                                                          \
     vs.push_back({"read-ceiling block regions one-shot U=" #U_, (double)total, [&](hipStream_t st) { \
         hipLaunchKernelGGL((k_read_regions<U_>), dim3((n + 255) / 256), dim3(256), 0, st, rx,  \
                            doff, dlen, (u32)n, sink);                                           \
     }});
-    RREG(2) RREG(4) RREG(8)
-#define FCEIL(U_, LNT_)                                                                   \
-    vs.push_back({"fill-ceiling region stream + sector nt U=" #U_ " LNT=" #LNT_, cb,           \
-                  [&](hipStream_t st) {                                                    \
-        hipLaunchKernelGGL((k_fill_ceiling<U_, LNT_>), dim3((n + 255) / 256), dim3(256), 0,   \
-                           st, tx, doff, dlen, (u32)n, sink);                              \
-    }});
-    FCEIL(4, false) FCEIL(4, true)
-    vs.push_back({"fill-ceiling ... LNT=true RNT, data changed", cb, [&](hipStream_t st) {
+    RREG(8)
+    vs.push_back({"fill-ceiling region stream + sector nt, data changed", cb, [&](hipStream_t st) {
         hipLaunchKernelGGL((k_fill_ceiling<4, true, true, true>), dim3((n + 255) / 256), dim3(256), 0,
-                           st, tx, doff, dlen, (u32)n, sink);
-    }});
-    vs.push_back({"fill-ceiling region stream + sector nt U=4 LNT=true RNT", cb, [&](hipStream_t st) {
-        hipLaunchKernelGGL((k_fill_ceiling<4, true, true>), dim3((n + 255) / 256), dim3(256), 0,
                            st, tx, doff, dlen, (u32)n, sink);
     }});
     vs.push_back({"read-ceiling uint4 NT (whole packed buffer)", (double)total,
@@ -1812,7 +1936,7 @@ int imix_main(uint64_t n, int rounds)
         CK(hipMemcpy(rxc, hb.data(), total, hipMemcpyHostToDevice));
         uint8_t* keep = rx;
         rx = rxc;
-        CK(launch_verify_desc(rx, total, doff, dlen, (u32)n, v1, 0u, s));
+        CK(launch_verify_desc(rx, total, doff, dlen, (u32)n, v1, 0u, kb_fb(1u << 24), s));
         std::vector<uint8_t> ref(n), got(n);
         CK(hipMemcpy(ref.data(), v1, n, hipMemcpyDeviceToHost));
         size_t drops = 0;
@@ -1832,7 +1956,7 @@ int imix_main(uint64_t n, int rounds)
     // all, and the filled buffer is byte-identical to launch_compute_desc's
     std::vector<uint8_t> fref(total), fgot(total);
     hipLaunchKernelGGL(k_hdr_desc, dim3((n + 255) / 256), dim3(256), 0, s, tx, doff, dlen, n);
-    CK(launch_compute_desc(tx, total, doff, dlen, (u32)n, nullptr, nullptr, 0u, s));
+    CK(launch_compute_desc(tx, total, doff, dlen, (u32)n, nullptr, nullptr, 0u, kb_fb(1u << 24), s));
     CK(hipMemcpy(fref.data(), tx, total, hipMemcpyDeviceToHost));
     for (auto& v : vs) {
         if (v.name.rfind("compute", 0) != 0 || v.name.find("no write") != std::string::npos)
@@ -1840,7 +1964,7 @@ int imix_main(uint64_t n, int rounds)
         hipLaunchKernelGGL(k_hdr_desc, dim3((n + 255) / 256), dim3(256), 0, s, tx, doff, dlen, n);
         v.run(s);
         CK(hipMemcpy(fgot.data(), tx, total, hipMemcpyDeviceToHost));
-        CK(launch_verify_desc(tx, total, doff, dlen, (u32)n, v1, 0u, s));
+        CK(launch_verify_desc(tx, total, doff, dlen, (u32)n, v1, 0u, kb_fb(1u << 24), s));
         CK(hipMemcpy(h.data(), v1, n, hipMemcpyDeviceToHost));
         bad = 0;
         for (auto b : h) bad += b != 0;
@@ -2295,13 +2419,13 @@ int copy_main(uint64_t n, int rounds)
     }});
     vs.push_back({"hipMemcpy2DAsync payloads + fill", bytes, [&](hipStream_t st_) {
         CK(hipMemcpy2DAsync(tx + hl, stride, src, plen, plen, n, hipMemcpyDeviceToDevice, st_));
-        CK(launch_compute_desc(tx, n * stride, off, lens, (u32)n, st, nullptr, 0u, st_));
+        CK(launch_compute_desc(tx, n * stride, off, lens, (u32)n, st, nullptr, 0u, kb_fb(1u << 24), st_));
     }});
     vs.push_back({"  hipMemcpy2DAsync payloads alone", (double)n * plen * 2, [&](hipStream_t st_) {
         CK(hipMemcpy2DAsync(tx + hl, stride, src, plen, plen, n, hipMemcpyDeviceToDevice, st_));
     }});
     vs.push_back({"  fill alone (launch_compute_desc)", cbytes, [&](hipStream_t st_) {
-        CK(launch_compute_desc(tx, n * stride, off, lens, (u32)n, st, nullptr, 0u, st_));
+        CK(launch_compute_desc(tx, n * stride, off, lens, (u32)n, st, nullptr, 0u, kb_fb(1u << 24), st_));
     }});
 #define DFILL(F_)                                                                            \
     vs.push_back({"  fill alone, desc_mixed F=" #F_, cbytes, [&](hipStream_t st_) {          \
@@ -2320,7 +2444,7 @@ int copy_main(uint64_t n, int rounds)
     }});
     run_variants(vs, s, rounds);
     std::vector<uint8_t> h(n);
-    CK(launch_verify_desc(tx, n * stride, off, lens, (u32)n, st, 0u, s));
+    CK(launch_verify_desc(tx, n * stride, off, lens, (u32)n, st, 0u, kb_fb(1u << 24), s));
     CK(hipMemcpy(h.data(), st, n, hipMemcpyDeviceToHost));
     size_t bad = 0;
     for (auto b : h) bad += b != 0;
@@ -2372,8 +2496,8 @@ int lro_main(uint64_t n, int rounds)
     hipLaunchKernelGGL(k_stream_hdr, dim3((n + 255) / 256), dim3(256), 0, s, in, n, stride, L);
     hipLaunchKernelGGL(k_seq_off, dim3((n + 255) / 256), dim3(256), 0, s, off, soff, lens, n,
                        stride, L, 0u);
-    CK(launch_compute_desc(in, n * stride, off, lens, (u32)n, nullptr, nullptr, 0u, s));
-    CK(launch_verify_desc(in, n * stride, off, lens, (u32)n, vd, 0u, s));
+    CK(launch_compute_desc(in, n * stride, off, lens, (u32)n, nullptr, nullptr, 0u, kb_fb(1u << 24), s));
+    CK(launch_verify_desc(in, n * stride, off, lens, (u32)n, vd, 0u, kb_fb(1u << 24), s));
     CK(hipStreamSynchronize(s));
     std::printf("LRO: n %llu x %u B segments, 16 flows in runs of 8, windows of 64\n",
                 (unsigned long long)n, L);
@@ -2474,7 +2598,7 @@ int lro_main(uint64_t n, int rounds)
                            n * stride, off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd);
     }});
     vs.push_back({"verify (launch_verify_desc) for scale", (double)n * (L + 1), [&](hipStream_t st) {
-        CK(launch_verify_desc(in, n * stride, off, lens, (u32)n, vd, 0u, st));
+        CK(launch_verify_desc(in, n * stride, off, lens, (u32)n, vd, 0u, kb_fb(1u << 24), st));
     }});
     vs.push_back({"D2D copy of the batch for scale", 2.0 * n * stride, [&](hipStream_t st) {
         CK(hipMemcpyAsync(out, in, n * stride, hipMemcpyDeviceToDevice, st));
@@ -2513,7 +2637,7 @@ int lro_main(uint64_t n, int rounds)
     CK(hipMalloc(&dml, 2 * ml.size()));
     CK(hipMemcpy(dmo, mo.data(), 8 * mo.size(), hipMemcpyHostToDevice));
     CK(hipMemcpy(dml, ml.data(), 2 * ml.size(), hipMemcpyHostToDevice));
-    CK(launch_verify_desc(out, n * stride, dmo, dml, (u32)mo.size(), vd, 0u, s));
+    CK(launch_verify_desc(out, n * stride, dmo, dml, (u32)mo.size(), vd, 0u, kb_fb(1u << 24), s));
     std::vector<uint8_t> hv(mo.size());
     CK(hipMemcpy(hv.data(), vd, mo.size(), hipMemcpyDeviceToHost));
     size_t bad = 0;
