@@ -77,8 +77,8 @@
  * Burst server: each thread's context serves its bursts through the
  * process's resident grid for its GPU, polling the context's request ring in
  * pinned memory (gcs_ctx_set_burst_server), unless the environment sets
- * GPUCSUM_BURST_SERVER=0 (then: one kernel launch per burst).  Up to 16
- * threads per GPU share the grid; a 17th launches per burst.
+ * GPUCSUM_BURST_SERVER=0 (then: one kernel launch per burst).  Up to 32
+ * threads per GPU share the grid; a 33rd launches per burst.
  * GPU failures (no CPU fallback: a context that cannot reach its GPU exits at
  * init_handle as dpdk_module.c:243-247 does).  A failed call after init is
  * counted in gpu_failures and reported on stderr, and its frames are:

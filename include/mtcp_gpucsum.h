@@ -142,13 +142,15 @@ int gcs_sync(gcs_ctx *ctx);                               /* wait for ctx stream
  * kernel reads pinned staging over PCIe: an mTCP burst) are served by a
  * resident grid that polls a request ring in pinned memory, instead of one
  * kernel launch and one event wait per batch.  ONE grid per process and
- * device serves the rings of up to 16 contexts (one per mTCP thread; 8
- * blocks each), on a highest-priority stream of its own; a 17th context gets
+ * device serves the rings of up to 32 contexts (one per mTCP thread; 8
+ * blocks each), on a highest-priority stream of its own; a 33rd context gets
  * GCS_ERANGE and runs without it.  The grid leaves after GCS_SERVER_LIFE_US
  * (default 10000) in total, or when a ring's blocks have had no work for
  * GCS_SERVER_IDLE_US (default 10000); a later batch starts it again.  A ring
  * goes cold after GCS_SERVER_HOT_US (default 20; 0 = never) without a
- * request: then one block, not eight, polls it over PCIe.  Default: off, or
+ * request -- or, when 3 x the gap between its last two requests is within
+ * GCS_SERVER_HOT_MAX_US (default 200), after that long, so a thread bursting
+ * every few tens of us keeps it hot: then one block, not eight, polls it.  Default: off, or
  * the environment variable GCS_BURST_SERVER=1 at gcs_ctx_create. */
 int gcs_ctx_set_burst_server(gcs_ctx *ctx, int on);
 

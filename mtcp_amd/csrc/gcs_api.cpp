@@ -390,6 +390,12 @@ class ServerHub {
         e = std::getenv("GCS_SERVER_HOT_US");
         const double hot_us = e ? std::atof(e) : 20.0;
         hot_ticks_ = hot_us > 0 ? (uint64_t)(hot_us * ticks_per_us_) : ~0ull;
+        // ... and stays hot longer, up to this, while its requests come in
+        // short gaps (3 x the gap: a thread bursting every 50 us stays hot)
+        e = std::getenv("GCS_SERVER_HOT_MAX_US");
+        const double hot_max_us = e ? std::atof(e) : 200.0;
+        hot_max_ticks_ = hot_us > 0 ? (uint64_t)(std::max(hot_us, hot_max_us) * ticks_per_us_)
+                                    : ~0ull;
         // extra ~2 us naps between the polls of a block with no hot ring
         e = std::getenv("GCS_SERVER_COLD_NAPS");
         cold_naps_ = e ? (uint32_t)std::atoi(e) : 0;
@@ -413,18 +419,22 @@ class ServerHub {
         if (mask_ == 0)
             return GCS_OK;
         int groups = 0;
-        uint64_t ids = 0;
         for (int k = 0; k < gcs::kHubRings; k++) {
             if (!((mask_ >> k) & 1u))
                 continue;
             for (auto& st : mb_->ring[k].state)
                 __atomic_store_n(&st.v, 0u, __ATOMIC_RELAXED);
-            ids |= (uint64_t)k << (4 * groups++);
+            ring_of_[groups++] = (uint32_t)k;
         }
         __atomic_store_n(&mb_->cmd.v, 0u, __ATOMIC_RELEASE);
         HIP_TRY(hipMemsetAsync(dpub_->exit, 0, sizeof dpub_->exit, stream_));
-        HIP_TRY(gcs::launch_burst_server(dmb_, dpub_, groups, ids, idle_ticks_, life_ticks_,
-                                         hot_ticks_, kMaxPolls, cold_naps_, prof_, stream_));
+        // ring_of_ is only rewritten under mu_ after the previous grid left and
+        // this copy completed (stop_locked synchronises the stream)
+        HIP_TRY(hipMemcpyAsync(dpub_->ring_of, ring_of_, groups * sizeof(uint32_t),
+                               hipMemcpyHostToDevice, stream_));
+        HIP_TRY(gcs::launch_burst_server(dmb_, dpub_, groups, idle_ticks_, life_ticks_,
+                                         hot_ticks_, hot_max_ticks_, kMaxPolls, cold_naps_, prof_,
+                                         stream_));
         launched_.store(true, std::memory_order_release);
         return GCS_OK;
     }
@@ -437,7 +447,8 @@ class ServerHub {
     hipStream_t stream_ = nullptr;
     uint32_t mask_ = 0;                   // rings in use
     std::atomic<bool> launched_{false};
-    uint64_t idle_ticks_ = 0, life_ticks_ = 0, hot_ticks_ = 0;
+    uint64_t idle_ticks_ = 0, life_ticks_ = 0, hot_ticks_ = 0, hot_max_ticks_ = 0;
+    uint32_t ring_of_[gcs::kHubRings] = {};
     uint32_t cold_naps_ = 0;
     bool prof_ = false;
     double ticks_per_us_ = 100.0;

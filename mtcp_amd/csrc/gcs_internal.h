@@ -55,7 +55,7 @@ constexpr int kServerFPB = 8;            // frames per block and pass (32 lanes 
 constexpr int kServerSlots = 8;
 constexpr int kSlotFrames = 512;         // frames per request
 constexpr int kServerMaxFrames = 4096;   // a larger synchronous batch: several requests
-constexpr int kHubRings = 16;            // contexts one grid serves (4-bit ring ids)
+constexpr int kHubRings = 32;            // contexts one grid serves (mTCP threads per GPU)
 struct alignas(16) ServerReqA {
     uint32_t seq;                       // request number (written last)
     uint32_t cmd;                       // unused (0)
@@ -115,6 +115,7 @@ struct HubPub {
     uint64_t ent[kHubRings][kServerSlots];
     PubFlag exit[kHubRings];
     uint32_t prog[kHubRings][kServerBlocks];
+    uint32_t ring_of[kHubRings];         // host, before each launch: group g serves ring_of[g]
 };
 
 // The request number after q: q + 1, skipping numbers whose 16-bit record tag
@@ -132,10 +133,13 @@ __host__ __device__ inline int server_block(uint32_t q, uint32_t i)
     return (int)((q + i / kServerFPB) % kServerBlocks);
 }
 
-// groups rings, ring_ids: 4 bits per group (group g serves ring
-// (ring_ids >> 4g) & 15); the grid is groups * kServerBlocks blocks.
-hipError_t launch_burst_server(HubMailbox* mb, HubPub* pub, int groups, uint64_t ring_ids,
-                               uint64_t idle_ticks, uint64_t life_ticks, uint64_t hot_ticks,
+// groups rings (group g serves ring pub->ring_of[g]); the grid is groups *
+// kServerBlocks blocks.  A block stays hot for hot_ticks after a request, or
+// for 3 x the gap between its last two requests when that is <= hot_max_ticks
+// (a thread bursting every 50 us keeps its ring hot; one bursting every 200 us
+// does not).
+hipError_t launch_burst_server(HubMailbox* mb, HubPub* pub, int groups, uint64_t idle_ticks,
+                               uint64_t life_ticks, uint64_t hot_ticks, uint64_t hot_max_ticks,
                                uint32_t max_polls, uint32_t cold_naps, bool prof, hipStream_t s);
 
 hipError_t launch_verify_fixed(uint8_t* frames, uint64_t stride, uint32_t frame_len, uint32_t n,

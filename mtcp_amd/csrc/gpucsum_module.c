@@ -243,7 +243,7 @@ static void gpucsum_init_handle(struct mtcp_thread_context *ctx)
 		rc = gcs_ctx_set_burst_server(g->gcs, 1);
 		if (rc && rc != GCS_ERANGE)
 			die("gcs_ctx_set_burst_server", rc);
-		/* GCS_ERANGE: 16 threads of this process already share the
+		/* GCS_ERANGE: 32 threads of this process already share the
 		 * device's grid; this one launches per burst */
 		/* fill as you go: a TX frame is complete once mTCP asks for the next
 		 * one or for its checksum (tcp_out.c:239-333); every

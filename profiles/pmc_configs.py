@@ -13,8 +13,9 @@ which bench.py then looks up for its roofline.traffic.
 Labels: <op>_<layout>_<frame_len|imix>_<frames per launch>, e.g.
 compute_fixed_1500_4194304 is the TX fill of a C4 shard.
 
---scrub writes 512 MiB (twice the Infinity Cache) between launches, outside
-the HIP events, so each launch starts with nothing of its batch cached.
+--scrub writes, then reads, 1 GiB (four times the Infinity Cache) between
+launches, outside the HIP events, so each launch starts with nothing of its
+batch cached and no dirty line of the scrub (bench.py's _scrub).
 Timings (HIP events on the launch stream) are printed as one JSON line.
 """
 from __future__ import annotations
@@ -50,7 +51,7 @@ def main():
     ctx = gpucsum.Context(0)
     manifest: list[str] = []
     timings: dict[str, dict] = {}
-    scrub_buf = torch.empty(512 << 20, dtype=torch.uint8, device="cuda") if a.scrub else None
+    scrub_buf = torch.empty(256 << 20, dtype=torch.int32, device="cuda") if a.scrub else None
 
     def setup(fn, *args, **kw):
         manifest.append("setup")
@@ -65,6 +66,7 @@ def main():
         for _ in range(a.reps):
             if scrub_buf is not None:
                 scrub_buf.fill_(len(ms) & 0xFF)
+                scrub_buf.sum()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             manifest.append(label)

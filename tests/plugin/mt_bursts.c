@@ -70,6 +70,8 @@ static void *run(void *arg)
 	j->rc = gcs_ctx_create(&ctx, 0, 4096, 8u << 20);
 	if (!j->rc && j->server)
 		j->rc = gcs_ctx_set_burst_server(ctx, 1);
+	if (j->rc == GCS_ERANGE)   /* the device's grid serves kHubRings contexts: launch per call */
+		j->rc = 0;
 	for (it = 0; it < j->iters && !j->rc; it++) {
 		double t0, t1;
 		for (i = 0; i < BURST; i++) {

@@ -2501,86 +2501,29 @@ int lro_main(uint64_t n, int rounds)
     CK(hipStreamSynchronize(s));
     std::printf("LRO: n %llu x %u B segments, 16 flows in runs of 8, windows of 64\n",
                 (unsigned long long)n, L);
+    int dev = 0, cus = 0;
+    CK(hipGetDevice(&dev));
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     const double bytes = 2.0 * n * L;                   // read each frame, write it merged
     std::vector<Variant> vs;
     vs.push_back({"gro (launch_gro, window 64, max 16384)", bytes, [&](hipStream_t st) {
         CK(launch_gro(in, n * stride, off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol,
                       hd, st));
     }});
-#define GROU(U_)                                                                             \
-    vs.push_back({"k_gro<" #U_ "> (window 64, max 16384)", bytes, [&](hipStream_t st) {          \
-        hipLaunchKernelGGL((k_gro<U_>), dim3((n + 63) / 64), dim3(256), 0, st, in, n * stride,   \
-                           off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd);    \
+    // round 4: the persistent pipelined kernel (k_gro_pipe: wave 0 plans the
+    // next window while waves 1-3 stream this one) against round 3's shipped
+    // one-window-per-block FLAT kernel on the same box
+    const u32 nwin = (u32)((n + 63) / 64);
+#define GROPIPE(U_, OCC_, BPC_)                                                              \
+    vs.push_back({"k_gro_pipe<" #U_ "," #OCC_ "> " #BPC_ " blocks/CU", bytes, [&](hipStream_t st) { \
+        const u32 g = nwin < (u32)(BPC_ * cus) ? nwin : (u32)(BPC_ * cus);                 \
+        hipLaunchKernelGGL((k_gro_pipe<U_, OCC_, WM_SECTOR_NT>), dim3(g), dim3(256), 0, st,  \
+                           in, n * stride, off, lens, vd, (u32)n, 64u, 16384u, out,         \
+                           n * stride, oo, ol, hd);                                         \
     }});
-    if (getenv("KB_GRO_W256")) { GROU(2) GROU(4) }
-#define GROW(U_, W_)                                                                         \
-    vs.push_back({"k_gro<" #U_ "," #W_ "> (window 64, max 16384)", bytes, [&](hipStream_t st) {  \
-        hipLaunchKernelGGL((k_gro<U_, W_>), dim3((n + 63) / 64), dim3(256), 0, st, in, n * stride, \
-                           off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd);  \
-    }});
-    GROW(2, 64)
-#define GROO(U_, W_, O_)                                                                     \
-    vs.push_back({"k_gro<" #U_ "," #W_ "," #O_ "> (window 64, max 16384)", bytes, [&](hipStream_t st) { \
-        hipLaunchKernelGGL((k_gro<U_, W_, O_>), dim3((n + 63) / 64), dim3(256), 0, st, in, n * stride, \
-                           off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd);  \
-    }});
-    GROO(2, 64, 6)          // the run-per-wave form shipped until round 3c
-    // round 3: more bytes in flight per wave (U) against waves per SIMD (OCC)
-    if (getenv("KB_GRO_SHAPES")) {   // measured r03: none faster (kbench_lro_shapes.log)
-    GROO(3, 64, 5) GROO(3, 64, 6) GROO(4, 64, 4) GROO(4, 64, 5) GROO(2, 64, 8) GROO(4, 64, 6)
-    }
-    // round 3b: two batches in flight per wave (k_gro PIPE: batch b + 1's loads
-    // issued before batch b is assembled, folded and stored) measured 929-1766 us
-    // against 766 us (spills: 32-176 B per lane; profiles/r03/kbench_lro_pipe.log);
-    // removed from the kernel
-    // round 3c: phase D as one stream over the window's output (k_gro FLAT)
-#define GROF(U_, O_)                                                                         \
-    vs.push_back({"k_gro<" #U_ ",64," #O_ ",FLAT> (window 64, max 16384)", bytes, [&](hipStream_t st) { \
-        hipLaunchKernelGGL((k_gro<U_, 64, O_, true>), dim3((n + 63) / 64), dim3(256), 0, st, in, \
-                           n * stride, off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd); \
-    }});
-    // measured r03: <2,6> 715, <4,6> 711, <4,5> 713, <8,4> (41 VGPRs spilled) 970 vs shipped 761
-    // <4,6> 712, <2,8> 687 (shipped), <2,7> 692, <3,7> 686, <3,6> 708 (run-per-wave 761,
-    // D2D 637); <1,10> / <2,10> (the compiler gives 7 waves) 722 / 714, <1,8> 693
-    GROF(2, 8) GROF(3, 7)
-#define GROFWM(TAG, WM_)                                                                     \
-    vs.push_back({"k_gro<2,64,8,FLAT> stores " TAG, bytes, [&](hipStream_t st) {            \
-        hipLaunchKernelGGL((k_gro<2, 64, 8, true, 0, WM_>), dim3((n + 63) / 64), dim3(256), 0, st, \
-                           in, n * stride, off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, \
-                           oo, ol, hd);                                                     \
-    }});
-    GROFWM("sc1", WM_SECTOR_SC1) GROFWM("nt", WM_SECTOR_NT) GROFWM("sc0sc1", WM_SECTOR_SC01)
-    vs.push_back({"k_gro<2,64,8,FLAT> ACX (word compares, scanned chains)", bytes, [&](hipStream_t st) {
-        hipLaunchKernelGGL((k_gro<2, 64, 8, true, 0, WM_SECTOR, true>), dim3((n + 63) / 64),
-                           dim3(256), 0, st, in, n * stride, off, lens, vd, (u32)n, 64u, 16384u,
-                           out, n * stride, oo, ol, hd);
-    }});
-#define GROACX(TAG, WM_)                                                                     \
-    vs.push_back({"k_gro<2,64,8,FLAT> ACX stores " TAG, bytes, [&](hipStream_t st) {        \
-        hipLaunchKernelGGL((k_gro<2, 64, 8, true, 0, WM_, true>), dim3((n + 63) / 64),         \
-                           dim3(256), 0, st, in, n * stride, off, lens, vd, (u32)n, 64u, 16384u, \
-                           out, n * stride, oo, ol, hd);                                    \
-    }});
-    GROACX("nt", WM_SECTOR_NT) GROACX("sc0sc1", WM_SECTOR_SC01)
-#define GROPF(PF_)                                                                           \
-    vs.push_back({"k_gro<2,64,8,FLAT> ACX nt PF" #PF_, bytes, [&](hipStream_t st) {          \
-        hipLaunchKernelGGL((k_gro<2, 64, 8, true, 0, WM_SECTOR_NT, true, PF_>), dim3((n + 63) / 64), \
-                           dim3(256), 0, st, in, n * stride, off, lens, vd, (u32)n, 64u, 16384u, \
-                           out, n * stride, oo, ol, hd);                                    \
-    }});
-    GROPF(4) GROPF(8)
-    vs.push_back({"k_gro<2,64,8,FLAT> ACX sc0sc1 PF8", bytes, [&](hipStream_t st) {
-        hipLaunchKernelGGL((k_gro<2, 64, 8, true, 0, WM_SECTOR_SC01, true, 8>), dim3((n + 63) / 64),
-                           dim3(256), 0, st, in, n * stride, off, lens, vd, (u32)n, 64u, 16384u,
-                           out, n * stride, oo, ol, hd);
-    }});
-    vs.push_back({"k_gro<3,64,7,FLAT> ACX nt PF8", bytes, [&](hipStream_t st) {
-        hipLaunchKernelGGL((k_gro<3, 64, 7, true, 0, WM_SECTOR_NT, true, 8>), dim3((n + 63) / 64),
-                           dim3(256), 0, st, in, n * stride, off, lens, vd, (u32)n, 64u, 16384u,
-                           out, n * stride, oo, ol, hd);
-    }});
-    vs.push_back({"k_gro<2,64,8,FLAT> ACX nt PF16", bytes, [&](hipStream_t st) {
-        hipLaunchKernelGGL((k_gro<2, 64, 8, true, 0, WM_SECTOR_NT, true, 16>), dim3((n + 63) / 64),
+    GROPIPE(2, 5, 5) GROPIPE(3, 5, 5) GROPIPE(4, 5, 5) GROPIPE(3, 5, 4) GROPIPE(3, 5, 10)
+    vs.push_back({"k_gro<2,64,8,FLAT> ACX nt PF8 (shipped r03)", bytes, [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_gro<2, 64, 8, true, 0, WM_SECTOR_NT, true, 8>), dim3((n + 63) / 64),
                            dim3(256), 0, st, in, n * stride, off, lens, vd, (u32)n, 64u, 16384u,
                            out, n * stride, oo, ol, hd);
     }});
@@ -2588,14 +2531,6 @@ int lro_main(uint64_t n, int rounds)
         hipLaunchKernelGGL((k_gro<2, 64, 8, true, 1, WM_SECTOR, true>), dim3((n + 63) / 64),
                            dim3(256), 0, st, in, n * stride, off, lens, vd, (u32)n, 64u, 16384u,
                            out, n * stride, oo, ol, hd);
-    }});
-    vs.push_back({"k_gro<2,64,8,FLAT> without the row table", bytes, [&](hipStream_t st) {
-        hipLaunchKernelGGL((k_gro<2, 64, 8, true, 2>), dim3((n + 63) / 64), dim3(256), 0, st, in,
-                           n * stride, off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd);
-    }});
-    vs.push_back({"probe: FLAT <2,64,8> phases A-C + D1 only", bytes, [&](hipStream_t st) {
-        hipLaunchKernelGGL((k_gro<2, 64, 8, true, 1>), dim3((n + 63) / 64), dim3(256), 0, st, in,
-                           n * stride, off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd);
     }});
     vs.push_back({"verify (launch_verify_desc) for scale", (double)n * (L + 1), [&](hipStream_t st) {
         CK(launch_verify_desc(in, n * stride, off, lens, (u32)n, vd, 0u, kb_fb(1u << 24), st));

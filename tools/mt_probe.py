@@ -18,7 +18,7 @@ out = {"workload": "threads each with its own context on GPU 0, 64-frame IMIX bu
                    "(fill + verify), every frame checked against the oracle; mean us per call "
                    "inside the gcs calls",
        "GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES", "default (4)")}
-for threads in (1, 4, 8, 12):
+for threads in (1, 4, 8, 12, 16, 24):
     for server in (1, 0):
         mis, fr, us = C.c_uint64(), C.c_uint64(), C.c_double()
         rc = M.mt_bursts(threads, 300, server, C.byref(mis), C.byref(fr), C.byref(us))
