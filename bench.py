@@ -734,6 +734,21 @@ def plugin_threads():
         return {"error": repr(e)[:200]}
 
 
+def plugin_rx_async():
+    """How long the RX path keeps the mTCP thread inside the plugin per 64 x
+    1500 B burst, verifying the burst as one batch or as you go
+    (GPUCSUM_RX_GROUP), under the reference's own RX code (ProcessPacket per
+    frame); the software path alongside (tools/rx_async_probe.py, child
+    process)."""
+    import subprocess
+    try:
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "rx_async_probe.py")],
+                           capture_output=True, text=True, timeout=240)
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    except Exception as e:   # a side measurement: report, never fail the bench line
+        return {"error": repr(e)[:200]}
+
+
 def server_poll_cost():
     """What idle burst-server rings cost the PCIe link (tools/poll_cost.py,
     child process): the pinned verify's rate while 0, 8 and 12 other
@@ -882,6 +897,7 @@ def main():
             line["plugin_bursts"] = plugin_bursts(gpucsum)
             line["plugin_threads"] = plugin_threads()
             line["plugin_tx_async"] = plugin_tx_async()
+            line["plugin_rx_async"] = plugin_rx_async()
             line["server_poll_cost"] = server_poll_cost()
     ctx.close()
     if rank == 0:

@@ -1427,8 +1427,8 @@ __device__ bool gro_cont32(const uint8_t* p, const uint8_t* c, int pp, int pc)
 // one wave per run -- see the comment at phase D2.
 enum { SEG_HDR = 0, SEG_PAY = 1, SEG_WHOLE = 2 };
 
-template <int U, int W = kGroW, int OCC = 1, bool FLAT = false, int PROBE = 0,
-          int FWM = WM_SECTOR, bool ACX = false, int PF = 0>
+template <int U, int W = kGroW, int OCC = 1, bool FLAT = false, int FWM = WM_SECTOR,
+          bool ACX = false, int PF = 0>
 __global__ void __launch_bounds__(kBlock, OCC)
 k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restrict__ off,
       const uint16_t* __restrict__ lens, const uint8_t* __restrict__ verdict, u32 n, u32 window,
@@ -1714,8 +1714,6 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
             }
         }
         __syncthreads();
-        if constexpr (PROBE == 1)           // A/B (kbench): phases A-C and D1 only
-            return;
         // D2: the window's output chunks as one stream, wave w a quarter of
         // them, 64 * U per trip.  A chunk finds its segment by binary search
         // (7 steps over <= 128 starts in LDS) and is one unaligned load, or
@@ -1740,8 +1738,7 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
                 const u32 c = base + 64 * j + lane, p = 16 * c;
                 // from the row's first segment: a row (1 KiB) spans few segments
                 const u32 rw = (c < hi ? c : hi - 1) >> 6;
-                int sgi = rw < (u32)NROW && PROBE != 2 ? sg_row[rw] : 0;   // past the table: search
-                                                           // (PROBE 2, A/B: always search)
+                int sgi = rw < (u32)NROW ? sg_row[rw] : 0;   // past the table: search
 #pragma unroll
                 for (int k = 0; k < 3; k++)
                     if (sgi + 1 < nseg && sg_st[sgi + 1] <= p)

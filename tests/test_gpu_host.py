@@ -323,6 +323,84 @@ def test_async_fill_many_outstanding(torch_dev, monkeypatch, stage):
     np.testing.assert_array_equal(buf, ref)
 
 
+@pytest.mark.parametrize("stage,registered", [("host", False), ("device", False),
+                                               ("host", True)])
+def test_async_verify_interleaved_with_fills(torch_dev, monkeypatch, stage, registered):
+    """gcs_verify_ptrs_async (the plugin's RX verify as you go) interleaved
+    with gcs_compute_ptrs_async on one context's request ring: 60 posts of
+    1..64 frames, alternating at random between verifies of corrupted frames
+    and fills of TX frames, past the 8 request slots, waits on older tickets
+    in between.  Every verdict -- and the tcp_in.c:1237 side effect on bad TCP
+    frames, written by the host at completion -- every status and every filled
+    frame equals the oracle.  Frames staged in pinned or device memory, or
+    read in place from a registered region."""
+    import ctypes as C
+    monkeypatch.setenv("GCS_ASYNC_STAGE", stage)
+    L = gpucsum.lib()
+    L.gcs_verify_ptrs_async.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                        C.c_void_p, C.c_uint32, C.POINTER(C.c_uint64)]
+    L.gcs_compute_ptrs_async.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                         C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64)]
+    L.gcs_wait.argtypes = [C.c_void_p, C.c_uint64]
+    O = Oracle()
+    n = 1800
+    rx, roff, rlens = synth.packed_frames(synth.imix_lengths(n, seed=81), seed=82)
+    O.compute_batch(rx, roff, rlens)
+    bad = synth.corrupt(rx, roff, rlens, frac_log2=3, seed=83)
+    tx, toff, tlens = synth.packed_frames(synth.imix_lengths(n, seed=84), seed=85)
+    mem = np.zeros(rx.nbytes + tx.nbytes + 16384, np.uint8)
+    base = (-mem.ctypes.data) % 4096
+    rxm = mem[base:base + rx.nbytes]
+    txo = base + rx.nbytes + ((-(base + rx.nbytes)) % 64)
+    txm = mem[txo:txo + tx.nbytes]
+    rxm[:] = rx
+    txm[:] = tx
+    rref, tref = rx.copy(), tx.copy()
+    rv = O.verify_batch(rref, roff, rlens, flags=1)      # GCS_VF_ZERO_BAD_TCP_CHECK
+    rst, rcs = O.compute_batch(tref, toff, tlens)
+    rp = (C.c_void_p * n)(*[rxm.ctypes.data + int(o) for o in roff])
+    tp = (C.c_void_p * n)(*[txm.ctypes.data + int(o) for o in toff])
+    vd = np.full(n, 0xEE, np.uint8)
+    st = np.full(n, 0xEE, np.uint8)
+    cs = np.zeros(n, np.uint32)
+    rng = np.random.default_rng(86)
+    if registered:
+        gpucsum.check(L.gcs_host_register(mem.ctypes.data + base, (mem.nbytes - base) & ~4095))
+    try:
+        with gpucsum.Context(0, max_frames=4096, max_bytes=8 << 20) as c:
+            c.set_burst_server(True)
+            i = j = 0
+            tickets = []
+            while i < n or j < n:
+                t = C.c_uint64()
+                if j >= n or (i < n and rng.random() < 0.5):
+                    m = min(int(rng.integers(1, 65)), n - i)
+                    gpucsum.check(L.gcs_verify_ptrs_async(
+                        c.h, C.cast(C.byref(rp, 8 * i), C.c_void_p), rlens.ctypes.data + 2 * i, m,
+                        vd.ctypes.data + i, 1, C.byref(t)))
+                    i += m
+                else:
+                    m = min(int(rng.integers(1, 65)), n - j)
+                    gpucsum.check(L.gcs_compute_ptrs_async(
+                        c.h, C.cast(C.byref(tp, 8 * j), C.c_void_p), tlens.ctypes.data + 2 * j, m,
+                        st.ctypes.data + j, cs.ctypes.data + 4 * j, C.byref(t)))
+                    j += m
+                assert t.value != 0
+                tickets.append(t.value)
+                if len(tickets) % 13 == 0:
+                    gpucsum.check(L.gcs_wait(c.h, tickets[-9]))
+            gpucsum.check(L.gcs_wait(c.h, tickets[-1]))
+    finally:
+        if registered:
+            gpucsum.check(L.gcs_host_unregister(mem.ctypes.data + base))
+    np.testing.assert_array_equal(vd, rv)
+    assert (vd[bad] != 0).all()
+    np.testing.assert_array_equal(rxm, rref)              # the side effect, exactly
+    np.testing.assert_array_equal(st, rst)
+    np.testing.assert_array_equal(cs, rcs)
+    np.testing.assert_array_equal(txm, tref)
+
+
 def test_async_fill_without_server_is_synchronous(torch_dev):
     import ctypes as C
     L = gpucsum.lib()

@@ -2523,15 +2523,12 @@ int lro_main(uint64_t n, int rounds)
     }});
     GROPIPE(2, 5, 5) GROPIPE(3, 5, 5) GROPIPE(4, 5, 5) GROPIPE(3, 5, 4) GROPIPE(3, 5, 10)
     vs.push_back({"k_gro<2,64,8,FLAT> ACX nt PF8 (shipped r03)", bytes, [&](hipStream_t st) {
-        hipLaunchKernelGGL((k_gro<2, 64, 8, true, 0, WM_SECTOR_NT, true, 8>), dim3((n + 63) / 64),
+        hipLaunchKernelGGL((k_gro<2, 64, 8, true, WM_SECTOR_NT, true, 8>), dim3((n + 63) / 64),
                            dim3(256), 0, st, in, n * stride, off, lens, vd, (u32)n, 64u, 16384u,
                            out, n * stride, oo, ol, hd);
     }});
-    vs.push_back({"probe: FLAT <2,64,8> ACX phases A-C + D1 only", bytes, [&](hipStream_t st) {
-        hipLaunchKernelGGL((k_gro<2, 64, 8, true, 1, WM_SECTOR, true>), dim3((n + 63) / 64),
-                           dim3(256), 0, st, in, n * stride, off, lens, vd, (u32)n, 64u, 16384u,
-                           out, n * stride, oo, ol, hd);
-    }});
+    // (round 3's k_gro PROBE = 1, phases A-C + D1 alone: 69-91 us for this batch,
+    // profiles/r03/kbench_lro_*.log; the knob left the product kernel in round 4)
     vs.push_back({"verify (launch_verify_desc) for scale", (double)n * (L + 1), [&](hipStream_t st) {
         CK(launch_verify_desc(in, n * stride, off, lens, (u32)n, vd, 0u, kb_fb(1u << 24), st));
     }});
