@@ -20,7 +20,6 @@
 #include <new>
 #include <system_error>
 #include <thread>
-#include <unordered_map>
 #include <vector>
 
 #include "gcs_internal.h"
@@ -691,9 +690,6 @@ struct gcs_ctx {
     // unarmed context never reads the environment on the burst path
     bool faults = false;
     AsyncReq areq[gcs::kServerSlots];
-    // descriptor launches' fallback lists (gcs_internal.h DescFb), one per
-    // stream: launches on one stream run in order, so they may share one
-    std::unordered_map<hipStream_t, gcs::DescFb> fbs;
 
     // Copy work for `count` frames / `bytes` bytes: inline when small, else
     // spread over the gather pool.
@@ -735,29 +731,6 @@ struct DeviceGuard {
 hipStream_t pick_stream(gcs_ctx* ctx, void* stream)
 {
     return stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
-}
-
-// The fallback list for a descriptor launch of n frames on stream s: one per
-// stream of the context, grown (after the stream's earlier launches are done
-// with the old one) when n outgrows it.
-int desc_fb(gcs_ctx* ctx, hipStream_t s, uint32_t n, gcs::DescFb** out)
-{
-    gcs::DescFb& fb = ctx->fbs[s];
-    if (!fb.d || fb.cap_frames < n) {
-        const uint32_t cap = std::max<uint32_t>(n, 1u << 16);
-        if (fb.d) {
-            HIP_TRY(hipStreamSynchronize(s));
-            HIP_TRY(hipFree(fb.d));
-            fb.d = nullptr;
-        }
-        const size_t bytes = gcs::desc_fb_words(cap) * sizeof(uint32_t);
-        HIP_TRY(hipMalloc((void**)&fb.d, bytes));
-        HIP_TRY(hipMemset(fb.d, 0, bytes));
-        fb.cap_frames = cap;
-        fb.epoch = 0;
-    }
-    *out = &fb;
-    return GCS_OK;
 }
 
 void free_slot(Slot& s)
@@ -1152,11 +1125,8 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
             HIP_TRY(gcs::launch_compute_desc_spread(frames_d, used, off_d, len_d, cnt, code_d,
                                                     csum_d, GCS_CF_NO_INPLACE, s.stream));
         } else if (compute) {
-            gcs::DescFb* fb = nullptr;
-            int rc = desc_fb(ctx, s.stream, cnt, &fb);
-            if (rc) return rc;
             HIP_TRY(gcs::launch_compute_desc(frames_d, used, off_d, len_d, cnt, code_d, csum_d,
-                                             GCS_CF_NO_INPLACE, fb, s.stream));
+                                             GCS_CF_NO_INPLACE, s.stream));
             if (!direct)
                 HIP_TRY(hipMemcpyAsync(s.h_csum, s.d_csum, cnt * sizeof(uint32_t),
                                        hipMemcpyDeviceToHost, s.stream));
@@ -1175,11 +1145,8 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
                                                    flags & GCS_VF_ICMP, s.stream));
         } else {
             // the tcp_in.c:1237 side effect is applied on the host copy below
-            gcs::DescFb* fb = nullptr;
-            int rc = desc_fb(ctx, s.stream, cnt, &fb);
-            if (rc) return rc;
             HIP_TRY(gcs::launch_verify_desc(frames_d, used, off_d, len_d, cnt, code_d,
-                                            flags & GCS_VF_ICMP, fb, s.stream));
+                                            flags & GCS_VF_ICMP, s.stream));
         }
         if (!direct)
             HIP_TRY(hipMemcpyAsync(s.h_code, s.d_code, cnt, hipMemcpyDeviceToHost, s.stream));
@@ -1302,14 +1269,6 @@ try {
                 (void)hipStreamSynchronize(s.stream);
             free_slot(s);
         }
-        for (auto& kv : ctx->fbs) {
-            // a caller's stream may be gone already: wait for the device instead
-            if (kv.second.d) {
-                (void)hipDeviceSynchronize();
-                (void)hipFree(kv.second.d);
-            }
-        }
-        ctx->fbs.clear();
         if (ctx->stream) {
             (void)hipStreamSynchronize(ctx->stream);
             (void)hipStreamDestroy(ctx->stream);
@@ -1456,11 +1415,7 @@ try {
         return GCS_OK;
     DeviceGuard g(ctx->device);
     const hipStream_t st = pick_stream(ctx, stream);
-    gcs::DescFb* fb = nullptr;
-    int rc = desc_fb(ctx, st, n, &fb);
-    if (rc) return rc;
-    HIP_TRY(gcs::launch_verify_desc(d_frames, frames_bytes, d_off, d_len, n, d_verdict, flags, fb,
-                                    st));
+    HIP_TRY(gcs::launch_verify_desc(d_frames, frames_bytes, d_off, d_len, n, d_verdict, flags, st));
     return GCS_OK;
 } GCS_CATCH
 
@@ -1474,11 +1429,8 @@ try {
         return GCS_OK;
     DeviceGuard g(ctx->device);
     const hipStream_t st = pick_stream(ctx, stream);
-    gcs::DescFb* fb = nullptr;
-    int rc = desc_fb(ctx, st, n, &fb);
-    if (rc) return rc;
     HIP_TRY(gcs::launch_compute_desc(d_frames, frames_bytes, d_off, d_len, n, d_status, d_csums,
-                                     flags, fb, st));
+                                     flags, st));
     return GCS_OK;
 } GCS_CATCH
 

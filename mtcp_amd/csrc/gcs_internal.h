@@ -146,30 +146,13 @@ hipError_t launch_verify_fixed(uint8_t* frames, uint64_t stride, uint32_t frame_
                                uint8_t* verdict, uint32_t flags, hipStream_t s);
 hipError_t launch_compute_fixed(uint8_t* frames, uint64_t stride, uint32_t frame_len, uint32_t n,
                                 uint8_t* status, uint32_t* csums, uint32_t flags, hipStream_t s);
-// Descriptor batches (k_desc_stream + k_desc_fallback) need a fallback list
-// in device memory for the blocks the stream kernel hands on: desc_fb_words(n)
-// u32, zeroed once when allocated.  Its head (u64 at word 0) is epoch << 32 |
-// blocks listed; each launch pair takes the next epoch, so a list is never
-// cleared: a head of an older epoch reads as empty.  Launches that share one
-// list must not overlap (one list per stream).
-constexpr uint32_t kFbHead = 2;          // u32 words of the head
 constexpr uint32_t kDescFrames = 256;    // frames per k_desc_stream block
-constexpr uint32_t kFbGrid = 2048;       // k_desc_fallback's largest grid (8 per CU)
-inline uint64_t desc_fb_words(uint32_t n)
-{
-    return kFbHead + (n + kDescFrames - 1) / kDescFrames;
-}
-struct DescFb {
-    uint32_t* d = nullptr;               // device list, desc_fb_words(cap_frames) words
-    uint32_t cap_frames = 0;             // the largest n it holds
-    uint32_t epoch = 0;                  // the last launch's (host copy)
-};
 hipError_t launch_verify_desc(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
                               const uint16_t* len, uint32_t n, uint8_t* verdict, uint32_t flags,
-                              DescFb* fb, hipStream_t s);
+                              hipStream_t s);
 hipError_t launch_compute_desc(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
                                const uint16_t* len, uint32_t n, uint8_t* status, uint32_t* csums,
-                               uint32_t flags, DescFb* fb, hipStream_t s);
+                               uint32_t flags, hipStream_t s);
 hipError_t launch_verify_desc_spread(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
                                      const uint16_t* len, uint32_t n, uint8_t* verdict,
                                      uint32_t flags, hipStream_t s);

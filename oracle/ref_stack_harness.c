@@ -124,7 +124,7 @@ static double refs_now_us(void);
  * ProcessPacket (core.c:789-801, without the send round). */
 int refs_rx_loop_timed(struct io_module_func *iom, struct mtcp_thread_context *ctx, int ifidx,
                        uint8_t *disp, uint32_t max, uint64_t *rx_errors, double *blocked_us,
-                       double *burst_us, uint32_t max_bursts);
+                       double *burst_us, double *recv_us, uint32_t max_bursts);
 
 /* core.c:785-801 plus the send_pkts of core.c:846-848 after each round (ICMP
  * echo replies and ARP answers go out through get_wptr).  Returns frames seen;
@@ -132,12 +132,12 @@ int refs_rx_loop_timed(struct io_module_func *iom, struct mtcp_thread_context *c
 int refs_rx_loop(struct io_module_func *iom, struct mtcp_thread_context *ctx, int ifidx,
                  uint8_t *disp, uint32_t max, uint64_t *rx_errors)
 {
-	return refs_rx_loop_timed(iom, ctx, ifidx, disp, max, rx_errors, NULL, NULL, 0);
+	return refs_rx_loop_timed(iom, ctx, ifidx, disp, max, rx_errors, NULL, NULL, NULL, 0);
 }
 
 int refs_rx_loop_timed(struct io_module_func *iom, struct mtcp_thread_context *ctx, int ifidx,
                        uint8_t *disp, uint32_t max, uint64_t *rx_errors, double *blocked_us,
-                       double *burst_us, uint32_t max_bursts)
+                       double *burst_us, double *recv_us, uint32_t max_bursts)
 {
 	uint32_t k = 0, b = 0;
 	int32_t n, i;
@@ -150,8 +150,11 @@ int refs_rx_loop_timed(struct io_module_func *iom, struct mtcp_thread_context *c
 		if (timed)
 			t0 = refs_now_us();
 		n = iom->recv_pkts(ctx, ifidx);
-		if (timed)
+		if (timed) {
 			in_mod = refs_now_us() - t0;
+			if (recv_us && b < max_bursts)
+				recv_us[b] = in_mod;
+		}
 		if (n <= 0)
 			break;
 		for (i = 0; i < n; i++) {

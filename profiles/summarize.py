@@ -23,11 +23,9 @@ are KB; on gfx950 FETCH_SIZE counts half the bytes of a wide coalesced
 streaming read (MI355X_MICROARCH.md, HBM / rocprofv3 section); WRITE_SIZE is
 exact for 16 B-per-lane streaming stores.
 
-Pairing: every launcher of libmtcp_gpucsum launches one kernel -- plus, for a
-descriptor batch (round 4), k_desc_fallback right behind k_desc_stream; its
-counters and duration are added to the stream kernel's dispatch (one launch
-of the batch) -- and pmc_configs.py launches on one stream, so the k-th gcs::
-launch (by Dispatch_Id) is the k-th manifest label.  A count mismatch is an
+Pairing: every launcher of libmtcp_gpucsum launches one kernel, and
+pmc_configs.py launches on one stream, so the k-th gcs:: launch (by
+Dispatch_Id) is the k-th manifest label.  A count mismatch is an
 error.
 """
 import csv
@@ -75,22 +73,6 @@ def per_dispatch_duration(d):
             for r in gcs_rows(f, "Dispatch_Id")]
 
 
-COMPANIONS = ("k_desc_fallback",)   # second kernel of one launcher call
-
-
-def fold_companions(s):
-    """A companion kernel's value added to the dispatch before it."""
-    if s is None:
-        return None
-    out = []
-    for name, val in s:
-        if out and any(c in name for c in COMPANIONS):
-            out[-1] = (out[-1][0], out[-1][1] + val)
-        else:
-            out.append((name, val))
-    return out
-
-
 def main():
     src, rnd = sys.argv[1], sys.argv[2]
     dst = os.path.join(ROOT, "profiles", rnd)
@@ -105,7 +87,6 @@ def main():
     series = {"FETCH_SIZE": per_dispatch_counter(os.path.join(src, "fetch"), "FETCH_SIZE"),
               "WRITE_SIZE": per_dispatch_counter(os.path.join(src, "write"), "WRITE_SIZE"),
               "duration_ns": per_dispatch_duration(os.path.join(src, "trace"))}
-    series = {k: fold_companions(v) for k, v in series.items()}
     acc = defaultdict(lambda: defaultdict(list))
     names = {}
     for what, s in series.items():

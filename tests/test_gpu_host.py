@@ -460,25 +460,29 @@ def test_hub_serves_many_contexts_at_once(torch_dev, monkeypatch, life_us):
     assert not errors, errors[:2]
 
 
+HUB_RINGS = 32   # gcs_internal.h kHubRings: contexts one device's grid serves
+
+
 def test_hub_ring_limit(torch_dev):
-    """A 17th context of the process gets GCS_ERANGE from
+    """A 33rd context of the process gets GCS_ERANGE from
     gcs_ctx_set_burst_server and still serves its bursts (launch per batch);
-    a ring freed by a leaving context is taken again."""
+    every one of the 32 rings serves its own; a ring freed by a leaving
+    context is taken again."""
     L = gpucsum.lib()
     O = Oracle()
-    ctxs = [gpucsum.Context(0, max_frames=256, max_bytes=1 << 20) for _ in range(17)]
+    ctxs = [gpucsum.Context(0, max_frames=256, max_bytes=1 << 20) for _ in range(HUB_RINGS + 1)]
     try:
-        for c in ctxs[:16]:
+        for c in ctxs[:HUB_RINGS]:
             c.set_burst_server(True)
-        assert L.gcs_ctx_set_burst_server(ctxs[16].h, 1) == gpucsum.K["GCS_ERANGE"]
+        assert L.gcs_ctx_set_burst_server(ctxs[HUB_RINGS].h, 1) == gpucsum.K["GCS_ERANGE"]
         for j, c in enumerate(ctxs):
             buf, off, lens = bursts(1, 64, 1300 + j)[0]
             v = c.verify_host(buf.copy(), off, lens)
             np.testing.assert_array_equal(v, O.verify_batch(buf.copy(), off, lens))
         ctxs[3].set_burst_server(False)
-        gpucsum.check(L.gcs_ctx_set_burst_server(ctxs[16].h, 1))
+        gpucsum.check(L.gcs_ctx_set_burst_server(ctxs[HUB_RINGS].h, 1))
         buf, off, lens = bursts(1, 64, 1400)[0]
-        v = ctxs[16].verify_host(buf.copy(), off, lens)
+        v = ctxs[HUB_RINGS].verify_host(buf.copy(), off, lens)
         np.testing.assert_array_equal(v, O.verify_batch(buf.copy(), off, lens))
     finally:
         for c in ctxs:

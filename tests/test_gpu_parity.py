@@ -370,6 +370,45 @@ def test_desc_no_inplace_and_null_outputs(torch_dev, ctx, O):
     np.testing.assert_array_equal(host(d), ref)
 
 
+def test_desc_all_blocks_fall_back(torch_dev, ctx, O):
+    """A descriptor batch in which no block streams (256 x 1500 B frames span
+    more than the stream's region cap): every block runs its frames one wave
+    per frame, bit-exact against the oracle, and not serialised -- the first
+    round-4 form listed such blocks behind one atomic head for a second kernel
+    and took 22 ms per 1M frames (here: 256K frames in well under 3 ms)."""
+    t = torch_dev
+    n, L = 1 << 18, 1500
+    src, stride = synth.fixed_frames(n, L, seed=0xFB)
+    off = np.arange(n, dtype=np.uint64) * stride
+    lens = np.full(n, L, dtype=np.uint16)
+    doff, dlen = dev(t, off.view(np.int64)), dev(t, lens.view(np.int16))
+    ref = src.copy()
+    rst, rcs = O.compute_batch(ref, off, lens)
+    d = dev(t, src)
+    st = t.zeros(n, dtype=t.uint8, device="cuda")
+    cs = t.zeros(n, dtype=t.int32, device="cuda")
+    ctx.compute(d, doff, dlen, n, st, cs)
+    ctx.sync()
+    np.testing.assert_array_equal(host(st), rst)
+    np.testing.assert_array_equal(host(cs).view(np.uint32), rcs)
+    np.testing.assert_array_equal(host(d), ref)
+    bad = synth.corrupt(ref, off, lens, frac_log2=5, seed=0xFC)
+    d = dev(t, ref)
+    v = t.full((n,), 0xEE, dtype=t.uint8, device="cuda")
+    ms = []
+    for _ in range(3):
+        e0, e1 = t.cuda.Event(enable_timing=True), t.cuda.Event(enable_timing=True)
+        e0.record()
+        ctx.verify(d, doff, dlen, n, v, stream=t.cuda.current_stream().cuda_stream)
+        e1.record()
+        t.cuda.synchronize()
+        ms.append(e0.elapsed_time(e1))
+    rv = O.verify_batch(ref.copy(), off, lens)
+    np.testing.assert_array_equal(host(v), rv)
+    assert (rv[bad] != 0).all() and int((rv != 0).sum()) == len(bad)
+    assert min(ms) < 3.0, ms
+
+
 def test_desc_stream_region_at_buffer_end(torch_dev, ctx, O):
     """A streaming block whose region ends exactly at frames_bytes (16 B-
     aligned: streamed; not aligned: the block falls back to guarded loads)."""

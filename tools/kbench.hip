@@ -5,6 +5,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../include tools/kbench.hip -o tools/kbench
 //   tools/kbench [frame_len=1500] [n=1048576] [rounds=15]
 #include "../mtcp_amd/csrc/gcs_kernels.hip"
+#include "gro_pipe.hip"
 
 #include <algorithm>
 #include <cstdio>
@@ -171,22 +172,6 @@ __global__ void k_hdr_desc(uint8_t* buf, const uint64_t* off, const uint16_t* le
 }
 
 void run_variants(std::vector<Variant>& vs, hipStream_t s, int rounds);
-
-// The descriptor launches' fallback list (gcs_internal.h DescFb), one for the
-// whole tool: every variant runs on one stream at a time.
-static DescFb* kb_fb(u32 n)
-{
-    static DescFb fb;
-    if (fb.cap_frames < n) {
-        if (fb.d)
-            CK(hipFree(fb.d));
-        CK(hipMalloc(&fb.d, desc_fb_words(n) * 4));
-        CK(hipMemset(fb.d, 0, desc_fb_words(n) * 4));
-        fb.cap_frames = n;
-        fb.epoch = 0;
-    }
-    return &fb;
-}
 
 // IMIX read ceiling in the descriptor kernel's own block partition: block b
 // streams the packed region of descriptors [256b, 256b+256), [off[256b],
@@ -1234,7 +1219,7 @@ k_desc_ring_x(uint8_t* __restrict__ frames, uint64_t frames_bytes,
 // ROUND 3's SHIPPED prefix-sum stream (k_desc_stream before round 4: the class
 // passes of non-streamable blocks and slow frames inside the same kernel, 6 / 7
 // waves per SIMD; PIPE / PROBE were its A/B knobs), kept here as the baseline
-// the round-4 split (stream kernel + k_desc_fallback) is measured against on
+// the round-4 stream kernel (class passes out of the kernel) is measured against on
 // the same box.
 template <int U_, int RMAX_, int OCC_, bool PIPE_ = false, int PROBE_ = 0, bool HDR3_ = false>
 struct StreamShapeR03 {
@@ -1833,7 +1818,7 @@ int imix_main(uint64_t n, int rounds)
     hipLaunchKernelGGL(k_init, dim3(4096), dim3(256), 0, s, tx, total / 64, (uint64_t)64, 64u);
     hipLaunchKernelGGL(k_hdr_desc, dim3((n + 255) / 256), dim3(256), 0, s, tx, doff, dlen, n);
     CK(hipMemcpyAsync(rx, tx, total, hipMemcpyDeviceToDevice, s));
-    CK(launch_compute_desc(rx, total, doff, dlen, (u32)n, nullptr, nullptr, 0, kb_fb(1u << 24), s));
+    CK(launch_compute_desc(rx, total, doff, dlen, (u32)n, nullptr, nullptr, 0, s));
     CK(hipStreamSynchronize(s));
     int dev = 0, cus = 0;
     CK(hipGetDevice(&dev));
@@ -1842,43 +1827,33 @@ int imix_main(uint64_t n, int rounds)
                 total / 1e9, (double)bytes / n);
     const double vb = bytes + n * (1.0 + 10.0), cb = bytes + n * (4.0 + 10.0);
     std::vector<Variant> vs;
-    // round 4: the stream kernel without the class passes (k_desc_fallback
-    // takes the blocks it hands on), against round 3's kernel on this box
-    DescFb& fb = *kb_fb((u32)n);
+    // round 4: the stream kernel without the class passes (a block it cannot
+    // stream runs desc_fallback_block), against round 3's kernel on this box
     auto zero_prep = [&](hipStream_t st) {
         hipLaunchKernelGGL(k_zero_checks_desc, dim3((n + 255) / 256), dim3(256), 0, st, tx, doff,
                            dlen, n);
     };
     vs.push_back({"verify  desc (launch_verify_desc, shipped)", vb, [&](hipStream_t st) {
-        CK(launch_verify_desc(rx, total, doff, dlen, (u32)n, v1, 0u, &fb, st));
+        CK(launch_verify_desc(rx, total, doff, dlen, (u32)n, v1, 0u, st));
     }});
     vs.push_back({"compute desc (launch_compute_desc, shipped) FRESH", cb, [&](hipStream_t st) {
-        CK(launch_compute_desc(tx, total, doff, dlen, (u32)n, nullptr, nullptr, 0u, &fb, st));
+        CK(launch_compute_desc(tx, total, doff, dlen, (u32)n, nullptr, nullptr, 0u, st));
     }});
     vs.back().prep = zero_prep;
     vs.push_back({"compute desc (launch_compute_desc, shipped) refill", cb, [&](hipStream_t st) {
-        CK(launch_compute_desc(tx, total, doff, dlen, (u32)n, nullptr, nullptr, 0u, &fb, st));
+        CK(launch_compute_desc(tx, total, doff, dlen, (u32)n, nullptr, nullptr, 0u, st));
     }});
     vs.push_back({"compute desc no write-back (GCS_CF_NO_INPLACE)", cb, [&](hipStream_t st) {
         CK(launch_compute_desc(tx, total, doff, dlen, (u32)n, nullptr, nullptr,
-                               (u32)GCS_CF_NO_INPLACE, &fb, st));
-    }});
-    vs.push_back({"fallback kernel alone (nothing listed)", 0.0, [&](hipStream_t st) {
-        hipLaunchKernelGGL((k_desc_fallback<false>), dim3(kFbGrid), dim3(256), 0, st, rx, total,
-                           doff, dlen, (u32)n, v1, nullptr, 0u, (const uint32_t*)fb.d,
-                           0xFFFFFFFFu);
+                               (u32)GCS_CF_NO_INPLACE, st));
     }});
 #define STREAM4(C_, TAG, U_, RMAX_, OCC_, WM_)                                              \
     vs.push_back({std::string(C_ ? "compute" : "verify ") + " stream4 " + TAG,              \
                   C_ ? cb : vb, [&](hipStream_t st) {                                      \
         using T_ = StreamShape<U_, RMAX_, OCC_, C_ ? 4 : 3>;                               \
-        if (++fb.epoch == 0) fb.epoch = 1;                                                  \
         hipLaunchKernelGGL((k_desc_stream<T_, C_, WM_, true>), dim3((n + 255) / 256),      \
                            dim3(256), 0, st, C_ ? tx : rx, total, doff, dlen, (u32)n,       \
-                           C_ ? nullptr : v1, nullptr, 0u, fb.d, fb.epoch);                 \
-        hipLaunchKernelGGL((k_desc_fallback<C_>), dim3(kFbGrid), dim3(256), 0, st,          \
-                           C_ ? tx : rx, total, doff, dlen, (u32)n, C_ ? nullptr : v1,      \
-                           nullptr, 0u, (const uint32_t*)fb.d, fb.epoch);                   \
+                           C_ ? nullptr : v1, nullptr, 0u);                                 \
     }});                                                                                    \
     if (C_)                                                                                 \
         vs.back().prep = zero_prep;
@@ -1936,7 +1911,7 @@ int imix_main(uint64_t n, int rounds)
         CK(hipMemcpy(rxc, hb.data(), total, hipMemcpyHostToDevice));
         uint8_t* keep = rx;
         rx = rxc;
-        CK(launch_verify_desc(rx, total, doff, dlen, (u32)n, v1, 0u, kb_fb(1u << 24), s));
+        CK(launch_verify_desc(rx, total, doff, dlen, (u32)n, v1, 0u, s));
         std::vector<uint8_t> ref(n), got(n);
         CK(hipMemcpy(ref.data(), v1, n, hipMemcpyDeviceToHost));
         size_t drops = 0;
@@ -1956,7 +1931,7 @@ int imix_main(uint64_t n, int rounds)
     // all, and the filled buffer is byte-identical to launch_compute_desc's
     std::vector<uint8_t> fref(total), fgot(total);
     hipLaunchKernelGGL(k_hdr_desc, dim3((n + 255) / 256), dim3(256), 0, s, tx, doff, dlen, n);
-    CK(launch_compute_desc(tx, total, doff, dlen, (u32)n, nullptr, nullptr, 0u, kb_fb(1u << 24), s));
+    CK(launch_compute_desc(tx, total, doff, dlen, (u32)n, nullptr, nullptr, 0u, s));
     CK(hipMemcpy(fref.data(), tx, total, hipMemcpyDeviceToHost));
     for (auto& v : vs) {
         if (v.name.rfind("compute", 0) != 0 || v.name.find("no write") != std::string::npos)
@@ -1964,7 +1939,7 @@ int imix_main(uint64_t n, int rounds)
         hipLaunchKernelGGL(k_hdr_desc, dim3((n + 255) / 256), dim3(256), 0, s, tx, doff, dlen, n);
         v.run(s);
         CK(hipMemcpy(fgot.data(), tx, total, hipMemcpyDeviceToHost));
-        CK(launch_verify_desc(tx, total, doff, dlen, (u32)n, v1, 0u, kb_fb(1u << 24), s));
+        CK(launch_verify_desc(tx, total, doff, dlen, (u32)n, v1, 0u, s));
         CK(hipMemcpy(h.data(), v1, n, hipMemcpyDeviceToHost));
         bad = 0;
         for (auto b : h) bad += b != 0;
@@ -2419,13 +2394,13 @@ int copy_main(uint64_t n, int rounds)
     }});
     vs.push_back({"hipMemcpy2DAsync payloads + fill", bytes, [&](hipStream_t st_) {
         CK(hipMemcpy2DAsync(tx + hl, stride, src, plen, plen, n, hipMemcpyDeviceToDevice, st_));
-        CK(launch_compute_desc(tx, n * stride, off, lens, (u32)n, st, nullptr, 0u, kb_fb(1u << 24), st_));
+        CK(launch_compute_desc(tx, n * stride, off, lens, (u32)n, st, nullptr, 0u, st_));
     }});
     vs.push_back({"  hipMemcpy2DAsync payloads alone", (double)n * plen * 2, [&](hipStream_t st_) {
         CK(hipMemcpy2DAsync(tx + hl, stride, src, plen, plen, n, hipMemcpyDeviceToDevice, st_));
     }});
     vs.push_back({"  fill alone (launch_compute_desc)", cbytes, [&](hipStream_t st_) {
-        CK(launch_compute_desc(tx, n * stride, off, lens, (u32)n, st, nullptr, 0u, kb_fb(1u << 24), st_));
+        CK(launch_compute_desc(tx, n * stride, off, lens, (u32)n, st, nullptr, 0u, st_));
     }});
 #define DFILL(F_)                                                                            \
     vs.push_back({"  fill alone, desc_mixed F=" #F_, cbytes, [&](hipStream_t st_) {          \
@@ -2444,7 +2419,7 @@ int copy_main(uint64_t n, int rounds)
     }});
     run_variants(vs, s, rounds);
     std::vector<uint8_t> h(n);
-    CK(launch_verify_desc(tx, n * stride, off, lens, (u32)n, st, 0u, kb_fb(1u << 24), s));
+    CK(launch_verify_desc(tx, n * stride, off, lens, (u32)n, st, 0u, s));
     CK(hipMemcpy(h.data(), st, n, hipMemcpyDeviceToHost));
     size_t bad = 0;
     for (auto b : h) bad += b != 0;
@@ -2496,8 +2471,8 @@ int lro_main(uint64_t n, int rounds)
     hipLaunchKernelGGL(k_stream_hdr, dim3((n + 255) / 256), dim3(256), 0, s, in, n, stride, L);
     hipLaunchKernelGGL(k_seq_off, dim3((n + 255) / 256), dim3(256), 0, s, off, soff, lens, n,
                        stride, L, 0u);
-    CK(launch_compute_desc(in, n * stride, off, lens, (u32)n, nullptr, nullptr, 0u, kb_fb(1u << 24), s));
-    CK(launch_verify_desc(in, n * stride, off, lens, (u32)n, vd, 0u, kb_fb(1u << 24), s));
+    CK(launch_compute_desc(in, n * stride, off, lens, (u32)n, nullptr, nullptr, 0u, s));
+    CK(launch_verify_desc(in, n * stride, off, lens, (u32)n, vd, 0u, s));
     CK(hipStreamSynchronize(s));
     std::printf("LRO: n %llu x %u B segments, 16 flows in runs of 8, windows of 64\n",
                 (unsigned long long)n, L);
@@ -2530,7 +2505,7 @@ int lro_main(uint64_t n, int rounds)
     // (round 3's k_gro PROBE = 1, phases A-C + D1 alone: 69-91 us for this batch,
     // profiles/r03/kbench_lro_*.log; the knob left the product kernel in round 4)
     vs.push_back({"verify (launch_verify_desc) for scale", (double)n * (L + 1), [&](hipStream_t st) {
-        CK(launch_verify_desc(in, n * stride, off, lens, (u32)n, vd, 0u, kb_fb(1u << 24), st));
+        CK(launch_verify_desc(in, n * stride, off, lens, (u32)n, vd, 0u, st));
     }});
     vs.push_back({"D2D copy of the batch for scale", 2.0 * n * stride, [&](hipStream_t st) {
         CK(hipMemcpyAsync(out, in, n * stride, hipMemcpyDeviceToDevice, st));
@@ -2569,7 +2544,7 @@ int lro_main(uint64_t n, int rounds)
     CK(hipMalloc(&dml, 2 * ml.size()));
     CK(hipMemcpy(dmo, mo.data(), 8 * mo.size(), hipMemcpyHostToDevice));
     CK(hipMemcpy(dml, ml.data(), 2 * ml.size(), hipMemcpyHostToDevice));
-    CK(launch_verify_desc(out, n * stride, dmo, dml, (u32)mo.size(), vd, 0u, kb_fb(1u << 24), s));
+    CK(launch_verify_desc(out, n * stride, dmo, dml, (u32)mo.size(), vd, 0u, s));
     std::vector<uint8_t> hv(mo.size());
     CK(hipMemcpy(hv.data(), vd, mo.size(), hipMemcpyDeviceToHost));
     size_t bad = 0;

@@ -32,9 +32,11 @@ H.synth_set_rx.argtypes = [vp, vp, vp, u32]
 H.mini_start.argtypes = [vp, vp]
 H.mini_stop.argtypes = [vp, vp]
 R.refs_config.argtypes = [u32]
-R.refs_rx_loop_timed.argtypes = [vp, vp, C.c_int, vp, u32, C.POINTER(C.c_uint64), vp, vp, u32]
+R.refs_rx_loop_timed.argtypes = [vp, vp, C.c_int, vp, u32, C.POINTER(C.c_uint64), vp, vp, vp, u32]
 P.gpucsum_set_inner.argtypes = [vp]
 R.refs_config(0x0100000A)
+T = C.CDLL(os.path.join(ROOT, "tools", "libburst_timer.so"))
+T.bt_run.argtypes = [vp, vp, vp, vp, u32, vp, vp, u32, vp]
 
 
 def vtab(lib, name):
@@ -62,17 +64,44 @@ def run(iom, ctx, registered):
         gpucsum.check(P.gcs_host_register(vp(frames.ctypes.data), frames.nbytes), "register")
     blocked = np.zeros(BURSTS, np.float64)
     burst = np.zeros(BURSTS, np.float64)
+    recv = np.zeros(BURSTS, np.float64)
     disp = np.zeros(n, np.uint8)
     errs = C.c_uint64()
     try:
         assert R.refs_rx_loop_timed(iom, ctx, 0, disp.ctypes.data, n, C.byref(errs),
-                                    blocked.ctypes.data, burst.ctypes.data, BURSTS) == n
+                                    blocked.ctypes.data, burst.ctypes.data, recv.ctypes.data,
+                                    BURSTS) == n
     finally:
         if registered:
             gpucsum.check(P.gcs_host_unregister(vp(frames.ctypes.data)), "unregister")
-    b, w = blocked[20:], burst[20:]                    # past the first bursts' warm-up
+    b, w, rv = blocked[20:], burst[20:], recv[20:]     # past the first bursts' warm-up
     return {"blocked_us_median": float(np.median(b)), "blocked_us_p90": float(np.percentile(b, 90)),
+            "recv_pkts_us_median": float(np.median(rv)),
             "burst_us_median": float(np.median(w)), "rx_errors": int(errs.value)}
+
+
+def direct(registered, same):
+    """gcs_verify_ptrs on each burst's 64 frames, no decorator and no RX loop
+    (same: burst 0's frames every time, as bench plugin_bursts)."""
+    frames[:] = src
+    ctx = gpucsum.Context(0)
+    verdict = np.zeros(BURST, np.uint8)
+    ln = np.full(BURST, L, np.uint16)
+    t = np.zeros(BURSTS, np.float64)
+    fn = C.cast(P.gcs_verify_ptrs, vp)
+    if registered:
+        gpucsum.check(P.gcs_host_register(vp(frames.ctypes.data), frames.nbytes), "register")
+    try:
+        for k in range(BURSTS):
+            j = 0 if same else k
+            ptrs = (vp * BURST)(*[frames.ctypes.data + int(off[j * BURST + i]) for i in range(BURST)])
+            gpucsum.check(T.bt_run(fn, ctx.h, ptrs, ln.ctypes.data, BURST, verdict.ctypes.data,
+                                   None, 1, t[k:].ctypes.data), "verify")
+    finally:
+        if registered:
+            gpucsum.check(P.gcs_host_unregister(vp(frames.ctypes.data)), "unregister")
+        ctx.close()
+    return {"verify_us_median": float(np.median(t[20:])), "verify_us_p90": float(np.percentile(t[20:], 90))}
 
 
 out = {"workload": f"{BURSTS} bursts of {BURST} x {L}B TCP frames ({len(bad)} corrupted) through "
@@ -101,4 +130,8 @@ for registered, group, stage in MODES:
     assert r["rx_errors"] == out["software_path"]["rx_errors"], (r, out["software_path"])
     out[f"{'registered' if registered else 'pageable'}_group{group}"
         + ("_devstage" if stage == "device" else "")] = r
+for registered in (False, True):
+    for same in (False, True):
+        out[f"direct_{'registered' if registered else 'pageable'}{'_same' if same else ''}"] = \
+            direct(registered, same)
 print(json.dumps(out))
