@@ -764,8 +764,10 @@ k_desc_mixed_x(uint8_t* __restrict__ frames, uint64_t frames_bytes,
 // class passes (and their 80 VGPRs) out of this kernel is what lets it run 8
 // waves per SIMD (round 4; before: 6 waves for the fill, 7 for the verify).  Reference
 // layout: PSIO's packed chunk (pslib.c:132-156, ps.h:181-213).
-template <int U_, int RMAX_, int OCC_, int NH_>
+template <int U_, int RMAX_, int OCC_, int NH_, int FG_ = 64, int FU_ = 1>
 struct StreamShape {
+    static constexpr int FG = FG_;        // a non-streaming block: lanes per frame ...
+    static constexpr int FU = FU_;        // ... and chunks per lane per trip
     static constexpr int U = U_;          // chunks per lane per trip (64 * U per wave)
     static constexpr int RMAX = RMAX_;    // region chunks a streaming block may span
     static constexpr int OCC = OCC_;      // waves per SIMD asked of the compiler
@@ -785,22 +787,22 @@ struct StreamShape {
 // 1500 B: 22 ms).  Rare in mTCP traffic: misordered or sparse descriptors,
 // regions over RMAX (256 frames of ~1500 B), IP options, frames padded past a
 // segment that ends beyond byte 48/64.
-template <bool COMPUTE>
+template <int G, int U, bool COMPUTE>
 __device__ __forceinline__ void
 desc_fallback_block(uint8_t* __restrict__ frames, uint64_t frames_bytes,
                     const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens,
                     uint64_t f0, int nf, uint8_t* __restrict__ out_code,
                     uint32_t* __restrict__ out_csum, u32 flags, uint8_t* spare)
 {
-    const int lane = threadIdx.x & 63;
-    for (int k = threadIdx.x >> 6; k < nf; k += kBlock / 64) {   // wave-uniform
+    const int sub = threadIdx.x & (G - 1);
+    for (int k = threadIdx.x / G; k < nf; k += kBlock / G) {     // group-uniform
         const uint64_t i = f0 + k;
         const uint64_t o = off[i];
         const u32 len = lens[i];
         const bool ok = (o & 15) == 0 && o <= frames_bytes && len <= frames_bytes - o;
         uint8_t* f = frames + (ok ? o : 0);
-        do_frame<64, 1, COMPUTE, true, true, kNT, WM_SECTOR_SC1>(
-            f, len, ok ? (int64_t)(frames_bytes - o) : 0, ok, lane, flags,
+        do_frame<G, U, COMPUTE, true, true, kNT, WM_SECTOR_SC1>(
+            f, len, ok ? (int64_t)(frames_bytes - o) : 0, ok, sub, flags,
             out_code ? out_code + i : spare + k, out_csum ? out_csum + i : nullptr);
     }
 }
@@ -815,81 +817,110 @@ k_desc_stream(uint8_t* __restrict__ frames, uint64_t frames_bytes,
     constexpr int HB = 16 * NH;            // header bytes stashed per frame
     static_assert(!COMPUTE || NH == 4, "TX stages sector 0 (chunks 0..3) in hdr");
     __shared__ uint4 hdr[NH * F];          // chunks 0..NH-1 per frame; TX: the staged sector 0
-    __shared__ u32 meta[F];                // start chunk << 16 | len
+    __shared__ u32 meta[F];                // pass-relative start chunk << 16 | len
     __shared__ u32 tail[F];                // wave-local Q(len) - Q(HB): words [HB, len)
     __shared__ uint64_t bm[RW];            // bit c: a frame starts at region chunk c
     __shared__ uint16_t rbase[RW];         // frames starting before chunk 64 * row
     __shared__ u32 wtot[NW];
     __shared__ uint8_t codes[F];           // TX statuses (the write-back's test); RX spare
-    __shared__ u32 nchunks_s;
+    __shared__ u32 nchunks_s, pbase_s;     // the pass region's chunks; its first, in the block's
 
     const uint32_t blk = XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
     const uint64_t f0 = (uint64_t)blk * F;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int nf = (int)((n - f0) < (uint64_t)F ? (n - f0) : (uint64_t)F);
 
-    // phase 0: validate; streamability, and each frame's place in the region
-    // (chunks from frame 0's start): its first chunk and the next frame's
-    uint64_t o = 0;
-    u32 len = 0, start = 0;
+    // A long block region is streamed in passes of at most RMAX chunks, one
+    // workgroup per pass (blockIdx.y; straight-line code: a pass loop around
+    // the stream made the compiler spill 23-38 VGPRs).  Pass p's frames are
+    // [p0, p1): greedily, the frames from p0 whose end lies within RMAX chunks
+    // of frame p0's start (in order, so contiguous).  An IMIX block is one
+    // pass (~91 KiB), and its pass-1.. workgroups leave after two loads; 256
+    // packed 1500 B frames are three passes.
+    const int pass = blockIdx.y;
+    const uint64_t r0 = off[f0];
+    if (pass > 0) {
+        const uint64_t ol = off[f0 + nf - 1];
+        if (ol >= r0 && ol - r0 + lens[f0 + nf - 1] <= 16ull * T::RMAX)
+            return;                        // block-uniform: a one-pass region
+    }
+
+    // phase 0: validate; streamability (in order, chunk-disjoint, gaps <= 64 B,
+    // the last frame's chunks inside the buffer); each frame's place in the
+    // block's region (chunks from frame 0's start): its first chunk, its end,
+    // the next frame's first chunk
+    u32 len = 0, start = 0, snext = 0;
     bool sok = true;
     if (t < nf) {
-        o = off[f0 + t];
+        const uint64_t o = off[f0 + t];
         len = lens[f0 + t];
-        sok = (o & 15) == 0 && o <= frames_bytes && len <= frames_bytes - o && len > 0;
-    }
-    const u32 nch = (len + 15) >> 4;
-    const uint64_t r0 = off[f0];
-    u32 snext = 0;
-    if (sok && t < nf) {
-        if (o < r0 || ((o - r0) >> 4) + nch > (uint64_t)T::RMAX) {
-            sok = false;
-        } else {
-            start = (u32)((o - r0) >> 4);
-            if (t + 1 < nf) {
-                const uint64_t on = off[f0 + t + 1], e = o + 16ull * nch;
-                sok = on >= e && on - e <= 64;
-                snext = (u32)((on - r0) >> 4);
-            } else {
-                sok = o + 16ull * nch <= frames_bytes;
-                snext = start + nch;
-                nchunks_s = snext;
-            }
+        sok = (o & 15) == 0 && o <= frames_bytes && len <= frames_bytes - o && len > 0 &&
+              o >= r0 && o - r0 < (1ull << 35);
+        const uint64_t e = o + 16ull * ((len + 15) >> 4);
+        start = (u32)((o - r0) >> 4);
+        if (sok && t + 1 < nf) {
+            const uint64_t on = off[f0 + t + 1];
+            sok = on >= e && on - e <= 64;
+            snext = (u32)((on - r0) >> 4);
+        } else if (sok) {
+            sok = e <= frames_bytes;
         }
     }
+    const u32 nch = (len + 15) >> 4, end = start + nch;
     for (int r = t; r < RW; r += kBlock)
         bm[r] = 0;
     if (!__syncthreads_and(sok)) {         // block-uniform: nothing written
-        desc_fallback_block<COMPUTE>(frames, frames_bytes, off, lens, f0, nf, out_code, out_csum,
-                                     flags, codes);
+        if (pass == 0)
+            desc_fallback_block<T::FG, T::FU, COMPUTE>(frames, frames_bytes, off, lens, f0, nf,
+                                                       out_code, out_csum, flags, codes);
         return;
     }
+    int p0 = 0, p1 = 0;
+    u32 pb = 0;
+    for (int k = 0; k <= pass; k++) {      // block-uniform
+        p0 = p1;
+        if (p0 >= nf)
+            return;                        // no pass p here
+        if (t == p0)
+            pbase_s = start;
+        __syncthreads();
+        pb = pbase_s;
+        p1 = p0 + __syncthreads_count(t >= p0 && t < nf && end - pb <= (u32)T::RMAX);
+    }
+    const bool in = t >= p0 && t < p1;
+    // frames past the last pass a launch has (PMAX) go to the per-frame path
+    const int fb_hi = pass + 1 == (int)gridDim.y ? nf : p1;
+    const u32 rs = start - pb;         // pass-relative first chunk
 
-    // phase 1: the region's first-chunk bitmap, per-frame metadata, and per
-    // 64-chunk row the number of frames starting before it (frame t owns the
-    // rows r with start_t < 64 r <= start_t+1)
-    const u32 NCH = nchunks_s, NR = (NCH + 63) >> 6;
-    if (t < nf) {
-        meta[t] = start << 16 | len;
+    // phase 1: the pass region's first-chunk bitmap, per-frame metadata,
+    // and per 64-chunk row the frame owning its first chunk, minus one
+    // for the mbcnt below (frame t owns the rows r with rs_t < 64 r <=
+    // rs_t+1; rbase[0] = p0: block frame indices throughout)
+    if (in) {
+        meta[t] = rs << 16 | len;
         tail[t] = 0;
 #pragma unroll
         for (int k = 0; k < NH; k++)
             if ((u32)k >= nch)
                 hdr[NH * t + k] = make_uint4(0, 0, 0, 0);
-        atomicOr((unsigned long long*)&bm[start >> 6], 1ull << (start & 63));
-        const u32 rhi = t + 1 < nf ? snext >> 6 : NR - 1;
-        for (u32 r = (start >> 6) + 1; r <= rhi; r++)
+        atomicOr((unsigned long long*)&bm[rs >> 6], 1ull << (rs & 63));
+        const bool last = t == p1 - 1;
+        const u32 rhi = last ? ((end - pb + 63) >> 6) - 1 : (snext - pb) >> 6;
+        for (u32 r = (rs >> 6) + 1; r <= rhi; r++)
             rbase[r] = (uint16_t)(t + 1);
+        if (last)
+            nchunks_s = end - pb;
     }
-    if (t == 0)
-        rbase[0] = 0;
+    if (t == p0)
+        rbase[0] = (uint16_t)p0;
     __syncthreads();
 
-    // phase 2: wave w streams chunks [w*QW, (w+1)*QW) of the region
+    // phase 2: wave w streams chunks [w*QW, (w+1)*QW) of the pass region
+    const u32 NCH = nchunks_s;
     const u32 QW = ((NCH + 4 * 64 - 1) / (4 * 64)) * 64;
+    uint8_t* const reg = frames + r0 + 16ull * pb;
     {
         const u32 lo = w * QW, hi = (lo + QW < NCH) ? lo + QW : NCH;
-        const uint8_t* reg = frames + r0;
         u32 run = 0;
         for (u32 base = lo; base < hi; base += 64 * U) {
             uint4 v[U];
@@ -934,8 +965,8 @@ k_desc_stream(uint8_t* __restrict__ frames, uint64_t frames_bytes,
     }
     __syncthreads();
 
-    // phase 3: one lane per frame
-    const int tf = t < nf ? t : 0;
+    // phase 3: one lane per frame of the pass
+    const int tf = in ? t : p0;
     const uint4 h4[4] = {hdr[NH * tf], hdr[NH * tf + 1], hdr[NH * tf + 2],
                          NH == 4 ? hdr[NH * tf + 3] : make_uint4(0, 0, 0, 0)};
     Hdr h;
@@ -946,19 +977,19 @@ k_desc_stream(uint8_t* __restrict__ frames, uint64_t frames_bytes,
     const int ts = 14 + 4 * ihl;
     const int te = 14 + (int)bswap16(h.d4 & 0xFFFFu);
     // NH = 3 (RX): doff (byte ts + 12) must lie in chunk 2: ihl == 5
-    const bool fast = t >= nf ||
-                      ((NH == 4 ? ihl <= 8 : ihl == 5) && (te <= HB || te == (int)len));
-    if (!__syncthreads_and(fast)) {        // block-uniform: nothing written yet
-        desc_fallback_block<COMPUTE>(frames, frames_bytes, off, lens, f0, nf, out_code, out_csum,
-                                     flags, codes);
+    const bool fast = !in || ((NH == 4 ? ihl <= 8 : ihl == 5) && (te <= HB || te == (int)len));
+    if (!__syncthreads_and(fast)) {    // block-uniform: this pass wrote nothing yet
+        desc_fallback_block<T::FG, T::FU, COMPUTE>(frames, frames_bytes, off, lens, f0 + p0,
+                                                   fb_hi - p0, out_code, out_csum, flags,
+                                                   codes + p0);
         return;
     }
-    // wave-uniform: every frame of the wave has ihl == 5, so the stash's word
-    // masks are constants (masks5, as the group kernels); and when every one
-    // also has te >= HB, no segment end lies in the stash
-    const bool all5 = NH == 3 || __all(t >= nf || ihl == 5);
-    const bool endh = __all(t >= nf || te >= HB);
-    if (t < nf) {
+    // wave-uniform: every frame of the wave has ihl == 5, so the stash's
+    // word masks are constants (masks5, as the group kernels); and when
+    // every one also has te >= HB, no segment end lies in the stash
+    const bool all5 = NH == 3 || __all(!in || ihl == 5);
+    const bool endh = __all(!in || te >= HB);
+    if (in) {
         Acc a = {0u, 0u, 0u};
         if (all5 && endh) {
 #pragma unroll
@@ -983,8 +1014,9 @@ k_desc_stream(uint8_t* __restrict__ frames, uint64_t frames_bytes,
                     b += (u32)k < q ? wtot[k] : 0u;
                 return b;
             };
-            a.tcp += tail[t] + wbase(start + nch - 1) - wbase(start + NH);
+            a.tcp += tail[t] + wbase(rs + nch - 1) - wbase(rs + NH);
         }
+        const uint64_t o = r0 + 16ull * (pb + rs);
         epilogue<1, 4, COMPUTE, WM, false>(
             h, a, frames + o, len, (int64_t)(frames_bytes - o), true, 0, flags,
             COMPUTE ? codes + t : (out_code ? out_code + f0 + t : codes + t),
@@ -992,26 +1024,32 @@ k_desc_stream(uint8_t* __restrict__ frames, uint64_t frames_bytes,
             COMPUTE ? reinterpret_cast<uint8_t*>(hdr + 4 * t) : nullptr);
     }
     if constexpr (COMPUTE) {
-        // the staged sectors leave together, in frame order, 16 B per lane:
-        // four lanes per sector, so two packed 64 B frames are one 128 B line
-        // of one store instruction.  A chunk goes out under exactly the
-        // epilogue's conditions: a status that fills, inside the frame (the
-        // region ends inside the buffer: phase 0).
+        // the staged sectors leave together, in frame order, 16 B per
+        // lane: four lanes per sector, so two packed 64 B frames are one
+        // 128 B line of one store instruction.  A chunk goes out under
+        // exactly the epilogue's conditions: a status that fills, inside
+        // the frame (the region ends inside the buffer: phase 0).
         __syncthreads();
         if (!(flags & GCS_CF_NO_INPLACE)) {
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 const int q = r * kBlock + t, ft = q >> 2, c = q & 3;
-                if (ft >= nf)
+                if (ft < p0 || ft >= p1)
                     continue;
                 const u32 st = codes[ft], m = meta[ft];
                 const bool wip = st == GCS_TX_OK || st == GCS_TX_IP_ONLY || st == GCS_TX_BAD_TCPLEN;
                 if (wip && (u32)(16 * c) < (m & 0xFFFFu))
-                    stg16<WM>(frames + r0 + 16ull * ((m >> 16) + c), hdr[q]);
+                    stg16<WM>(reg + 16ull * ((m >> 16) + c), hdr[q]);
             }
         }
-        if (out_code && t < nf)
+        if (out_code && in)
             out_code[f0 + t] = codes[t];
+    }
+    if (fb_hi > p1) {
+        __syncthreads();                   // codes[] is the per-frame path's spare
+        desc_fallback_block<T::FG, T::FU, COMPUTE>(frames, frames_bytes, off, lens, f0 + p1,
+                                                   fb_hi - p1, out_code, out_csum, flags,
+                                                   codes + p1);
     }
 }
 
@@ -2260,6 +2298,9 @@ hipError_t launch_classify_fixed(uint8_t* frames, uint64_t stride, u32 frame_len
 // class passes out of the kernel both run 8 waves per SIMD (round 4).
 template <bool COMPUTE>
 using StreamShip = StreamShape<8, 8192, 8, COMPUTE ? 4 : 3>;
+// passes per block region (blockIdx.y): 3 x 8,192 chunks hold 256 packed
+// frames of up to 1,536 B; what a block has beyond them goes per frame
+constexpr int kStreamPasses = 3;
 template <bool COMPUTE>
 static hipError_t launch_desc(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
                               const uint16_t* len, u32 n, uint8_t* code, uint32_t* csums,
@@ -2275,8 +2316,9 @@ static hipError_t launch_desc(uint8_t* frames, uint64_t frames_bytes, const uint
                            frames, frames_bytes, off, len, n, code, csums, flags, ext);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL((k_desc_stream<StreamShip<COMPUTE>, COMPUTE, WM_SECTOR_SC1, kXCD>), grid,
-                       dim3(kBlock), 0, s, frames, frames_bytes, off, len, n, code, csums, flags);
+    hipLaunchKernelGGL((k_desc_stream<StreamShip<COMPUTE>, COMPUTE, WM_SECTOR_SC1, kXCD>),
+                       dim3(grid.x, kStreamPasses), dim3(kBlock), 0, s, frames, frames_bytes, off,
+                       len, n, code, csums, flags);
     return hipGetLastError();
 }
 

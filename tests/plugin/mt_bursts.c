@@ -23,8 +23,21 @@ struct job {
 	int id, iters, server;
 	uint64_t mismatches, frames;
 	int rc;
-	double us;
+	double us, cpu_us;
 };
+
+/* Thread CPU time inside the gcs calls over wall time inside them, averaged
+ * over the threads of the last mt_bursts call: below 1 when threads were
+ * descheduled while they waited (more threads than the process's cores). */
+static double g_cpu_frac;
+double mt_last_cpu_frac(void) { return g_cpu_frac; }
+
+static double cpu_us(void)
+{
+	struct timespec t;
+	clock_gettime(CLOCK_THREAD_CPUTIME_ID, &t);
+	return t.tv_sec * 1e6 + t.tv_nsec * 1e-3;
+}
 
 static uint32_t xorshift(uint64_t *s)
 {
@@ -64,7 +77,7 @@ static void *run(void *arg)
 	uint32_t cs[BURST];
 	uint64_t rng = 0x9E3779B97F4A7C15ull ^ (uint64_t)(j->id + 1) * 0x100000001B3ull;
 	gcs_ctx *ctx = NULL;
-	double in_calls = 0;
+	double in_calls = 0, in_cpu = 0;
 	int it, i;
 
 	j->rc = gcs_ctx_create(&ctx, 0, 4096, 8u << 20);
@@ -81,9 +94,11 @@ static void *run(void *arg)
 			make_frame(ptrs[i], len[i], &rng);
 			memcpy(ref + (size_t)i * ROOM, ptrs[i], len[i]);
 		}
+		double c0 = cpu_us();
 		t0 = now_us();
 		j->rc = gcs_compute_ptrs(ctx, ptrs, len, BURST, st, cs);
 		in_calls += now_us() - t0;
+		in_cpu += cpu_us() - c0;
 		if (j->rc)
 			break;
 		for (i = 0; i < BURST; i++) {
@@ -99,9 +114,11 @@ static void *run(void *arg)
 				r[p] ^= x;
 			}
 		}
+		c0 = cpu_us();
 		t1 = now_us();
 		j->rc = gcs_verify_ptrs(ctx, ptrs, len, BURST, vd, GCS_VF_ZERO_BAD_TCP_CHECK);
 		in_calls += now_us() - t1;
+		in_cpu += cpu_us() - c0;
 		if (j->rc)
 			break;
 		for (i = 0; i < BURST; i++) {
@@ -113,6 +130,7 @@ static void *run(void *arg)
 		j->frames += 2 * BURST;
 	}
 	j->us = in_calls / (2.0 * (it ? it : 1));     /* inside the gcs calls only */
+	j->cpu_us = in_cpu / (2.0 * (it ? it : 1));
 	if (ctx)
 		gcs_ctx_destroy(ctx);
 	free(rooms);
@@ -141,6 +159,7 @@ int mt_bursts(int threads, int iters, int server, uint64_t *mismatches, uint64_t
 	}
 	*mismatches = *frames = 0;
 	*us_per_call = 0;
+	g_cpu_frac = 0;
 	for (t = 0; t < threads; t++) {
 		pthread_join(tid[t], NULL);
 		if (jobs[t].rc && !rc)
@@ -148,6 +167,7 @@ int mt_bursts(int threads, int iters, int server, uint64_t *mismatches, uint64_t
 		*mismatches += jobs[t].mismatches;
 		*frames += jobs[t].frames;
 		*us_per_call += jobs[t].us / threads;
+		g_cpu_frac += (jobs[t].us > 0 ? jobs[t].cpu_us / jobs[t].us : 1.0) / threads;
 	}
 	return rc;
 }

@@ -370,12 +370,76 @@ def test_desc_no_inplace_and_null_outputs(torch_dev, ctx, O):
     np.testing.assert_array_equal(host(d), ref)
 
 
-def test_desc_all_blocks_fall_back(torch_dev, ctx, O):
-    """A descriptor batch in which no block streams (256 x 1500 B frames span
-    more than the stream's region cap): every block runs its frames one wave
-    per frame, bit-exact against the oracle, and not serialised -- the first
-    round-4 form listed such blocks behind one atomic head for a second kernel
-    and took 22 ms per 1M frames (here: 256K frames in well under 3 ms)."""
+def mtu_frames(n, seed, lens=None):
+    """Packed (16 B-aligned) TCP frames of 1400-1514 B, all "fast" (ihl 5,
+    te == len), checks zeroed."""
+    rng = np.random.default_rng(seed)
+    if lens is None:
+        lens = rng.integers(1400, 1515, size=n).astype(np.uint16)
+    off, total = synth.packed_offsets(lens, 16)
+    buf = rng.integers(0, 256, size=total + 64, dtype=np.uint8)
+    for i in range(n):
+        set_tcp_headers(buf, int(off[i]), int(lens[i]), 5, int(lens[i]) - 14)
+    return buf, off, lens
+
+
+def set_tcp_headers(buf, o, L, ihl, tot):
+    f = buf[o:o + L]
+    ts = 14 + 4 * ihl
+    f[12], f[13], f[14] = 0x08, 0x00, 0x40 | ihl
+    f[16], f[17] = tot >> 8, tot & 0xFF
+    f[23] = 6
+    f[24] = f[25] = 0
+    f[ts + 12] = 5 << 4
+    f[ts + 16] = f[ts + 17] = 0
+
+
+def test_desc_stream_passes_vs_oracle(torch_dev, ctx, O):
+    """Block regions longer than one pass (RMAX chunks): 256 packed MTU frames
+    stream in three passes, one workgroup each (blockIdx.y).  A frame that is
+    not fast sends its pass and what follows to the per-frame path; frames
+    past the last pass go there too.  Bit-exact against the oracle, TX and RX
+    (with and without the tcp_in.c:1237 side effect)."""
+    t = torch_dev
+    n = 256 * 6 + 50
+    rng = np.random.default_rng(0x9A55)
+    lens = rng.integers(1400, 1515, size=n).astype(np.uint16)
+    lens[2 * 256:2 * 256 + 9] = 9000                 # block 2: more than three passes
+    buf, off, lens = mtu_frames(n, 0x9A56, lens)
+    set_tcp_headers(buf, int(off[256 + 200]), int(lens[256 + 200]), 12,
+                    int(lens[256 + 200]) - 14)        # block 1, pass 3: IP options
+    i = 3 * 256 + 120                                 # block 3, pass 2: padded (te < len)
+    set_tcp_headers(buf, int(off[i]), int(lens[i]), 5, int(lens[i]) - 14 - 30)
+    doff, dlen = dev(t, off.view(np.int64)), dev(t, lens.view(np.int16))
+    ref = buf.copy()
+    rst, rcs = O.compute_batch(ref, off, lens)
+    d = dev(t, buf)
+    st = t.zeros(n, dtype=t.uint8, device="cuda")
+    cs = t.zeros(n, dtype=t.int32, device="cuda")
+    ctx.compute(d, doff, dlen, n, st, cs)
+    ctx.sync()
+    np.testing.assert_array_equal(host(st), rst)
+    np.testing.assert_array_equal(host(cs).view(np.uint32), rcs)
+    np.testing.assert_array_equal(host(d), ref)
+    bad = synth.corrupt(ref, off, lens, frac_log2=3, seed=0x9A57)
+    for flags in (0, 1):
+        d = dev(t, ref)
+        v = t.full((n,), 0xEE, dtype=t.uint8, device="cuda")
+        ctx.verify(d, doff, dlen, n, v, flags=flags)
+        ctx.sync()
+        exp = ref.copy()
+        rv = O.verify_batch(exp, off, lens, flags=flags)
+        np.testing.assert_array_equal(host(v), rv)
+        np.testing.assert_array_equal(host(d), exp)
+        assert (rv[bad] != 0).all()
+
+
+def test_desc_mtu_batch_not_serialised(torch_dev, ctx, O):
+    """A descriptor batch of 256 x 1500 B frames per block (three passes of
+    the stream each, plus a frame per block on the per-frame path): bit-exact
+    against the oracle, and not serialised -- the first round-4 form listed
+    non-streaming blocks behind one atomic head for a second kernel and took
+    22 ms per 1M frames (here: 256K frames in well under 3 ms)."""
     t = torch_dev
     n, L = 1 << 18, 1500
     src, stride = synth.fixed_frames(n, L, seed=0xFB)

@@ -1847,21 +1847,20 @@ int imix_main(uint64_t n, int rounds)
         CK(launch_compute_desc(tx, total, doff, dlen, (u32)n, nullptr, nullptr,
                                (u32)GCS_CF_NO_INPLACE, st));
     }});
-#define STREAM4(C_, TAG, U_, RMAX_, OCC_, WM_)                                              \
+#define STREAM4(C_, TAG, U_, RMAX_, OCC_, WM_, PY_)                                         \
     vs.push_back({std::string(C_ ? "compute" : "verify ") + " stream4 " + TAG,              \
                   C_ ? cb : vb, [&](hipStream_t st) {                                      \
         using T_ = StreamShape<U_, RMAX_, OCC_, C_ ? 4 : 3>;                               \
-        hipLaunchKernelGGL((k_desc_stream<T_, C_, WM_, true>), dim3((n + 255) / 256),      \
+        hipLaunchKernelGGL((k_desc_stream<T_, C_, WM_, true>), dim3((n + 255) / 256, PY_), \
                            dim3(256), 0, st, C_ ? tx : rx, total, doff, dlen, (u32)n,       \
                            C_ ? nullptr : v1, nullptr, 0u);                                 \
     }});                                                                                    \
     if (C_)                                                                                 \
         vs.back().prep = zero_prep;
-    STREAM4(false, "U4 R8K occ8", 4, 8192, 8, WM_SECTOR_SC1)
-    STREAM4(true, "U4 R8K occ8 sc1 FRESH", 4, 8192, 8, WM_SECTOR_SC1)
-    STREAM4(true, "U8 R8K occ8 nt FRESH", 8, 8192, 8, WM_SECTOR_NT)
-    STREAM4(true, "U8 R8K occ8 plain FRESH", 8, 8192, 8, WM_SECTOR)
-    STREAM4(true, "U8 R12K occ7 sc1 FRESH", 8, 12288, 7, WM_SECTOR_SC1)
+    // the pass workgroups' cost on a one-pass batch: the shipped shape with
+    // one pass per block (gridDim.y = 1) against kStreamPasses
+    STREAM4(false, "shipped shape, 1 pass", 8, 8192, 8, WM_SECTOR_SC1, 1)
+    STREAM4(true, "shipped shape, 1 pass FRESH", 8, 8192, 8, WM_SECTOR_SC1, 1)
 #define STREAM3(C_, TAG, OCC_, HDR3_)                                                       \
     vs.push_back({std::string(C_ ? "compute" : "verify ") + " stream r03 " + TAG,           \
                   C_ ? cb : vb, [&](hipStream_t st) {                                      \

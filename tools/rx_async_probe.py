@@ -81,10 +81,12 @@ def run(iom, ctx, registered):
 
 
 def direct(registered, same):
-    """gcs_verify_ptrs on each burst's 64 frames, no decorator and no RX loop
-    (same: burst 0's frames every time, as bench plugin_bursts)."""
+    """gcs_verify_ptrs on each burst's 64 frames through the burst server, no
+    decorator and no RX loop (same: burst 0's frames every time, as bench
+    plugin_bursts)."""
     frames[:] = src
-    ctx = gpucsum.Context(0)
+    ctx = gpucsum.Context(0, max_frames=4096, max_bytes=8 << 20)
+    ctx.set_burst_server(True)                         # as the plugin's contexts
     verdict = np.zeros(BURST, np.uint8)
     ln = np.full(BURST, L, np.uint16)
     t = np.zeros(BURSTS, np.float64)
