@@ -66,6 +66,14 @@ int synth_set_rx(const uint8_t *buf, const uint64_t *off, const uint16_t *len, u
 
 uint32_t synth_tx_sent(void) { return S.tx_sent; }
 
+/* The RX rooms (rx_n x SYN_BUF bytes, the frames as the NIC "received" them):
+ * for registering them as an mbuf pool would be registered (gcs_host_register). */
+uint8_t *synth_rx_base(uint64_t *bytes)
+{
+	*bytes = (uint64_t)(S.rx_n ? S.rx_n : 1) * SYN_BUF;
+	return S.rx_bufs;
+}
+
 /* The TX rooms (SYN_MAX_TX x SYN_BUF bytes): for registering them as an mbuf
  * pool would be registered (gcs_host_register). */
 uint8_t *synth_tx_base(uint64_t *bytes)

@@ -159,6 +159,22 @@ __global__ void k_zero_checks_desc(uint8_t* f, const uint64_t* off, const uint16
     }
 }
 
+// The write side of an IMIX fill alone: each frame's first 64 B sector (the
+// write-back's bytes), 16 B per lane, four lanes per sector, frames in order,
+// no reads but the descriptors -- what scattered sector writes cost by
+// themselves (the fill's write-back writes the same sectors).
+template <int WM>
+__global__ void __launch_bounds__(256) k_sector_writes(uint8_t* __restrict__ buf,
+                                                       const uint64_t* __restrict__ off,
+                                                       const uint16_t* __restrict__ lens, u32 n)
+{
+    const uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x, f = q >> 2;
+    const u32 c = (u32)(q & 3);
+    if (f >= n || 16 * c >= lens[f])
+        return;
+    stg16<WM>(buf + off[f] + 16ull * c, make_uint4((u32)f, c, 0x5EC7u, 0u));
+}
+
 __global__ void k_hdr_desc(uint8_t* buf, const uint64_t* off, const uint16_t* lens, uint64_t n)
 {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1884,12 +1900,26 @@ int imix_main(uint64_t n, int rounds)
         hipLaunchKernelGGL((k_fill_ceiling<4, true, true, true>), dim3((n + 255) / 256), dim3(256), 0,
                            st, tx, doff, dlen, (u32)n, sink);
     }});
+    uint8_t* wbuf = nullptr;                 // a scratch copy: the writes change data
+    CK(hipMalloc(&wbuf, total));
+    CK(hipMemcpy(wbuf, tx, total, hipMemcpyDeviceToDevice));
+    vs.push_back({"write ceiling: 64 B sector per frame, sc1 (no reads)", 64.0 * n,
+                  [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_sector_writes<WM_SECTOR_SC1>), dim3((4ull * n + 255) / 256),
+                           dim3(256), 0, st, wbuf, doff, dlen, (u32)n);
+    }});
+    vs.push_back({"write ceiling: 64 B sector per frame, nt (no reads)", 64.0 * n,
+                  [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_sector_writes<WM_SECTOR_NT>), dim3((4ull * n + 255) / 256),
+                           dim3(256), 0, st, wbuf, doff, dlen, (u32)n);
+    }});
     vs.push_back({"read-ceiling uint4 NT (whole packed buffer)", (double)total,
                   [&](hipStream_t st) {
         hipLaunchKernelGGL((k_read<true>), dim3(cus * 8), dim3(256), 0, st, (const uint4*)rx,
                            total / 16, sink);
     }});
     run_variants(vs, s, rounds);
+    CK(hipFree(wbuf));
     std::vector<uint8_t> h(n);
     CK(hipMemcpy(h.data(), v1, n, hipMemcpyDeviceToHost));
     size_t bad = 0;

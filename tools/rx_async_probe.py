@@ -4,9 +4,9 @@ you go (groups of 8 / 16 / 32 / 64 frames posted in recv_pkts; get_rptr(i)
 waits only for frame i's group), through the reference's OWN RX code:
 oracle/_ref/libref_mtcp_stack.so's refs_rx_loop_timed, core.c's loop around
 mTCP's ProcessPacket (eth_in.c, ip_in.c, tcp_in.c; accepted segments stop at
-StreamHTSearch).  The synthetic NIC's frames sit in pageable memory (staged by
-the library into pinned or, GCS_ASYNC_STAGE=device, device memory) or in a
-registered region (read in place).  The software path -- the module alone,
+StreamHTSearch).  The synthetic NIC's RX rooms (2 KiB each, as mbufs) sit in pageable memory (staged by
+the library into pinned or, GCS_ASYNC_STAGE=device, device memory) or are
+registered with gcs_host_register, as an mbuf pool would be (read in place).  The software path -- the module alone,
 mTCP folding every frame on the CPU -- is timed the same way.  Prints one JSON
 object (tools/, not product)."""
 import ctypes as C
@@ -31,6 +31,8 @@ H.synth_reset.argtypes = [u32]
 H.synth_set_rx.argtypes = [vp, vp, vp, u32]
 H.mini_start.argtypes = [vp, vp]
 H.mini_stop.argtypes = [vp, vp]
+H.synth_rx_base.argtypes = [C.POINTER(C.c_uint64)]
+H.synth_rx_base.restype = vp
 R.refs_config.argtypes = [u32]
 R.refs_rx_loop_timed.argtypes = [vp, vp, C.c_int, vp, u32, C.POINTER(C.c_uint64), vp, vp, vp, u32]
 P.gpucsum_set_inner.argtypes = [vp]
@@ -60,8 +62,10 @@ def run(iom, ctx, registered):
     frames[:] = src                                    # fresh frames (the side effect writes)
     H.synth_reset(BURST)
     assert H.synth_set_rx(frames.ctypes.data, off.ctypes.data, lens.ctypes.data, n) == 0
+    rx_bytes = C.c_uint64()
+    rx_base = H.synth_rx_base(C.byref(rx_bytes))       # the NIC's RX rooms (its "mbuf pool")
     if registered:
-        gpucsum.check(P.gcs_host_register(vp(frames.ctypes.data), frames.nbytes), "register")
+        gpucsum.check(P.gcs_host_register(vp(rx_base), rx_bytes.value), "register")
     blocked = np.zeros(BURSTS, np.float64)
     burst = np.zeros(BURSTS, np.float64)
     recv = np.zeros(BURSTS, np.float64)
@@ -73,7 +77,7 @@ def run(iom, ctx, registered):
                                     BURSTS) == n
     finally:
         if registered:
-            gpucsum.check(P.gcs_host_unregister(vp(frames.ctypes.data)), "unregister")
+            gpucsum.check(P.gcs_host_unregister(vp(rx_base)), "unregister")
     b, w, rv = blocked[20:], burst[20:], recv[20:]     # past the first bursts' warm-up
     return {"blocked_us_median": float(np.median(b)), "blocked_us_p90": float(np.percentile(b, 90)),
             "recv_pkts_us_median": float(np.median(rv)),
