@@ -32,8 +32,8 @@ struct Ext {
 // requests while earlier ones are still being served (the plugin's TX fill
 // posts frames as mTCP completes them).  Every block of the ring's group
 // serves its requests in order.  Request q's frames go to the blocks in turn
-// starting at block q % kServerBlocks (kServerFPB frames per block and pass),
-// so a run of small requests is served by different blocks at once.
+// starting at block server_rot(q) (kServerFPB frames per block and pass), so
+// a run of small requests is served by different blocks at once.
 //
 // One poll is ONE load instruction of wave 0 of a block: lane 0 reads the
 // slot's line A, lane 1 its line B, lanes 2.. the descriptors of the block's
@@ -126,11 +126,20 @@ __host__ __device__ inline uint32_t server_next(uint32_t q)
     return (q & 0xFFFFu) == 0 ? q + 1 : q;
 }
 
-// Block holding frame i of request q: frames go out kServerFPB per block,
-// starting at block q % kServerBlocks.
+// Request q starts at block 2q mod kServerBlocks and goes out kServerFPB
+// frames per block: four consecutive requests of <= 16 frames (the plugin's
+// RX and TX groups) land on disjoint blocks and are served side by side.  (A
+// start of q mod 8 put consecutive 16-frame groups on overlapping blocks, so
+// each group waited for the one before: ~3 us per group, round 4.)
+constexpr uint32_t kServerRot = 2;
+__host__ __device__ inline uint32_t server_rot(uint32_t q)
+{
+    return (kServerRot * q) % kServerBlocks;
+}
+// Block holding frame i of request q.
 __host__ __device__ inline int server_block(uint32_t q, uint32_t i)
 {
-    return (int)((q + i / kServerFPB) % kServerBlocks);
+    return (int)((server_rot(q) + i / kServerFPB) % kServerBlocks);
 }
 
 // groups rings (group g serves ring pub->ring_of[g]); the grid is groups *

@@ -240,8 +240,9 @@ k_burst_server(HubMailbox* mb, HubPub* pub, uint64_t idle_ticks, uint64_t life_t
     static_assert(FPB == kServerFPB, "the mailbox's frames per block and pass");
     constexpr int kPass = kServerBlocks * FPB;          // frames of one request per pass
     constexpr int kLanes = 2 + FPB;                     // lines of a poll
+    constexpr int kAhead = kServerSlots - 1;            // + line A of the next requests
     __shared__ uint4 s_line[kLanes];
-    __shared__ uint32_t s_claim;
+    __shared__ uint32_t s_claim, s_last;
     __shared__ uint8_t s_code[FPB];          // a frame's results, packed into its record
     __shared__ uint32_t s_csum[FPB];
     const int t = threadIdx.x, sub = t & (G - 1), grp = t / G;
@@ -264,7 +265,7 @@ k_burst_server(HubMailbox* mb, HubPub* pub, uint64_t idle_ticks, uint64_t life_t
     for (;;) {
         const uint32_t q = server_next(last);            // the request this block serves next
         ServerSlot* sl = &rm->slot[q % kServerSlots];
-        const uint32_t first = (uint32_t)FPB * ((blk + kServerBlocks - q % kServerBlocks) %
+        const uint32_t first = (uint32_t)FPB * ((blk + kServerBlocks - server_rot(q)) %
                                                 kServerBlocks);   // this block's first frame of q
         if (wave == 0) {
             for (;;) {
@@ -277,8 +278,18 @@ k_burst_server(HubMailbox* mb, HubPub* pub, uint64_t idle_ticks, uint64_t life_t
                 // command for the leader; the leader's exit, every 8th poll,
                 // for the others)
                 const bool follow = !hot && !leader && lane == 0;
+                // hot, lanes kLanes..: line A of requests q_1..q_kAhead after
+                // q, so that one poll claims a run of requests none of whose
+                // frames are here (the plugin's small groups, posted together)
+                const bool ahead = hot && lane >= kLanes && lane < kLanes + kAhead;
+                uint32_t qk = q;
+                if (ahead)
+                    for (int j = kLanes; j <= lane; j++)
+                        qk = server_next(qk);
                 const volatile u32x4* src = nullptr;
-                if ((hot && lane < kLanes) || (leader && lane == 0))
+                if (ahead)
+                    src = reinterpret_cast<const volatile u32x4*>(&rm->slot[qk % kServerSlots].a);
+                else if ((hot && lane < kLanes) || (leader && lane == 0))
                     src = lane == 0   ? reinterpret_cast<const volatile u32x4*>(&sl->a)
                           : lane == 1 ? reinterpret_cast<const volatile u32x4*>(&sl->b)
                                       : reinterpret_cast<const volatile u32x4*>(&sl->desc[first + lane - 2]);
@@ -343,8 +354,25 @@ k_burst_server(HubMailbox* mb, HubPub* pub, uint64_t idle_ticks, uint64_t life_t
                             __builtin_amdgcn_s_sleep(63);   // ~4k cycles a nap
                     continue;
                 }
-                if (lane == 0)
+                // a WORK claim of q without frames here also claims the posted
+                // requests right after it that have none here either
+                int run = 0;
+                {
+                    const uint32_t fk = (uint32_t)FPB * ((blk + kServerBlocks - server_rot(qk)) %
+                                                         kServerBlocks);
+                    const uint64_t okm = __ballot(ahead && v.x == qk && fk >= v.z) >> kLanes;
+                    if (act == WORK && first >= z0)
+                        run = __builtin_ctzll(~okm);
+                    run = run < kAhead ? run : kAhead;
+                }
+                const uint32_t qlast = run ? (uint32_t)__shfl((int)qk, kLanes + run - 1) : q;
+                if (leader && ahead && lane < kLanes + run)
+                    __hip_atomic_store(&pub->ent[r][qk % kServerSlots], ((uint64_t)qk << 32) | v.z,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (lane == 0) {
                     s_claim = act;
+                    s_last = qlast;
+                }
                 if (act == WORK && lane < kLanes)
                     s_line[lane] = make_uint4(v.x, v.y, v.z, v.w);
                 break;
@@ -352,6 +380,7 @@ k_burst_server(HubMailbox* mb, HubPub* pub, uint64_t idle_ticks, uint64_t life_t
         }
         __syncthreads();
         const uint32_t act = s_claim;
+        const uint32_t qend = s_last;        // q, or the last request of a claimed run
         if (act == EXIT) {
             if (leader && t == 0)
                 __hip_atomic_store(&pub->exit[r].v, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -416,10 +445,11 @@ k_burst_server(HubMailbox* mb, HubPub* pub, uint64_t idle_ticks, uint64_t life_t
             if (mine)
                 __hip_atomic_store(&rm->ack[blk].v, q, __ATOMIC_RELEASE,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&pub->prog[r][blk], q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&pub->prog[r][blk], qend, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
             s_claim = IDLE;
         }
-        last = q;
+        last = qend;
         t_last = __builtin_amdgcn_s_memrealtime();
         if (act == WORK && hot_ticks != ~0ull) {
             const uint64_t gap = t_last - t_claim;
