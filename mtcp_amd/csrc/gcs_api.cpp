@@ -387,7 +387,9 @@ class ServerHub {
         // a ring without a request for this long goes cold: only the leader
         // block polls its host lines (0: never cold)
         e = std::getenv("GCS_SERVER_HOT_US");
-        const double hot_us = e ? std::atof(e) : 20.0;
+        // (at least 2 us: a block must stay hot from seeing its request to
+        // reading its lines, or it never serves)
+        const double hot_us = e ? (std::atof(e) > 0 ? std::max(std::atof(e), 2.0) : 0.0) : 20.0;
         hot_ticks_ = hot_us > 0 ? (uint64_t)(hot_us * ticks_per_us_) : ~0ull;
         // ... and stays hot longer, up to this, while its requests come in
         // short gaps (3 x the gap: a thread bursting every 50 us stays hot)
@@ -395,9 +397,12 @@ class ServerHub {
         const double hot_max_us = e ? std::atof(e) : 200.0;
         hot_max_ticks_ = hot_us > 0 ? (uint64_t)(std::max(hot_us, hot_max_us) * ticks_per_us_)
                                     : ~0ull;
-        // extra ~2 us naps between the polls of a block with no hot ring
+        // extra ~2 us naps between the polls of a block with no hot ring, and
+        // of a hot one (an A/B knob for the PCIe cost of hot polling)
         e = std::getenv("GCS_SERVER_COLD_NAPS");
-        cold_naps_ = e ? (uint32_t)std::atoi(e) : 0;
+        naps_ = e ? (uint32_t)std::min(std::atoi(e), 0xFFFF) : 0;
+        e = std::getenv("GCS_SERVER_HOT_NAPS");
+        naps_ |= (e ? (uint32_t)std::min(std::atoi(e), 0xFFFF) : 0u) << 16;
     }
 
     // Every block ends within life_ticks of its start (or at the exit
@@ -432,7 +437,7 @@ class ServerHub {
         HIP_TRY(hipMemcpyAsync(dpub_->ring_of, ring_of_, groups * sizeof(uint32_t),
                                hipMemcpyHostToDevice, stream_));
         HIP_TRY(gcs::launch_burst_server(dmb_, dpub_, groups, idle_ticks_, life_ticks_,
-                                         hot_ticks_, hot_max_ticks_, kMaxPolls, cold_naps_, prof_,
+                                         hot_ticks_, hot_max_ticks_, kMaxPolls, naps_, prof_,
                                          stream_));
         launched_.store(true, std::memory_order_release);
         return GCS_OK;
@@ -448,7 +453,7 @@ class ServerHub {
     std::atomic<bool> launched_{false};
     uint64_t idle_ticks_ = 0, life_ticks_ = 0, hot_ticks_ = 0, hot_max_ticks_ = 0;
     uint32_t ring_of_[gcs::kHubRings] = {};
-    uint32_t cold_naps_ = 0;
+    uint32_t naps_ = 0;                   // cold naps | hot naps << 16
     bool prof_ = false;
     double ticks_per_us_ = 100.0;
 };

@@ -149,7 +149,7 @@ __host__ __device__ inline int server_block(uint32_t q, uint32_t i)
 // does not).
 hipError_t launch_burst_server(HubMailbox* mb, HubPub* pub, int groups, uint64_t idle_ticks,
                                uint64_t life_ticks, uint64_t hot_ticks, uint64_t hot_max_ticks,
-                               uint32_t max_polls, uint32_t cold_naps, bool prof, hipStream_t s);
+                               uint32_t max_polls, uint32_t naps, bool prof, hipStream_t s);
 
 hipError_t launch_verify_fixed(uint8_t* frames, uint64_t stride, uint32_t frame_len, uint32_t n,
                                uint8_t* verdict, uint32_t flags, hipStream_t s);

@@ -233,7 +233,7 @@ k_desc(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __re
 template <int G, int U, bool PROF>
 __global__ void __launch_bounds__(kBlock)
 k_burst_server(HubMailbox* mb, HubPub* pub, uint64_t idle_ticks, uint64_t life_ticks,
-               uint64_t hot_ticks, uint64_t hot_max_ticks, uint32_t max_polls, uint32_t cold_naps)
+               uint64_t hot_ticks, uint64_t hot_max_ticks, uint32_t max_polls, uint32_t naps)
 {
     enum { IDLE = 0, WORK = 1, EXIT = 2, SKIP = 3 };
     constexpr int FPB = kBlock / G;
@@ -348,10 +348,11 @@ k_burst_server(HubMailbox* mb, HubPub* pub, uint64_t idle_ticks, uint64_t life_t
                     (act == IDLE && now - t_last > idle_ticks))
                     act = EXIT;
                 if (act == IDLE) {
+                    // naps: extra ~4k-cycle naps between polls, the low 16 bits
+                    // for a cold block, the high 16 for a hot one
                     __builtin_amdgcn_s_sleep(2);
-                    if (!hot)
-                        for (uint32_t k = 0; k < cold_naps; k++)
-                            __builtin_amdgcn_s_sleep(63);   // ~4k cycles a nap
+                    for (uint32_t k = 0, m = hot ? naps >> 16 : naps & 0xFFFFu; k < m; k++)
+                        __builtin_amdgcn_s_sleep(63);
                     continue;
                 }
                 // a WORK claim of q without frames here also claims the posted
@@ -470,17 +471,17 @@ k_burst_server(HubMailbox* mb, HubPub* pub, uint64_t idle_ticks, uint64_t life_t
 
 hipError_t launch_burst_server(HubMailbox* mb, HubPub* pub, int groups, uint64_t idle_ticks,
                                uint64_t life_ticks, uint64_t hot_ticks, uint64_t hot_max_ticks,
-                               uint32_t max_polls, uint32_t cold_naps, bool prof, hipStream_t s)
+                               uint32_t max_polls, uint32_t naps, bool prof, hipStream_t s)
 {
     if (groups < 1 || groups > kHubRings)
         return hipErrorInvalidValue;
     const dim3 grid(kServerBlocks * groups);
     if (prof)
         hipLaunchKernelGGL((k_burst_server<32, 3, true>), grid, dim3(kBlock), 0, s, mb, pub,
-                           idle_ticks, life_ticks, hot_ticks, hot_max_ticks, max_polls, cold_naps);
+                           idle_ticks, life_ticks, hot_ticks, hot_max_ticks, max_polls, naps);
     else
         hipLaunchKernelGGL((k_burst_server<32, 3, false>), grid, dim3(kBlock), 0, s, mb, pub,
-                           idle_ticks, life_ticks, hot_ticks, hot_max_ticks, max_polls, cold_naps);
+                           idle_ticks, life_ticks, hot_ticks, hot_max_ticks, max_polls, naps);
     return hipGetLastError();
 }
 
