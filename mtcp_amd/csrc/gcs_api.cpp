@@ -109,6 +109,11 @@ struct Slot {
     uint32_t* m_csum = nullptr;
     uint32_t* m_hash = nullptr;
     uint16_t* m_queue = nullptr;
+    // GCS_DIRECT_STAGE=device: a direct-mode batch is gathered into this
+    // fine-grained device memory (host writes over the BAR, posted) instead
+    // of the pinned staging, so the kernel reads its frames from HBM rather
+    // than over PCIe; allocated on first use (ctx->direct_max bytes)
+    uint8_t* v_frames = nullptr;
     // bookkeeping of the chunk in flight
     bool busy = false;
     bool served = false;           // results already complete (burst server)
@@ -690,6 +695,7 @@ struct gcs_ctx {
         bool stage_dev = false;             // staging is device memory (hipFree)
     };
     bool async_stage_dev = false;           // GCS_ASYNC_STAGE=device
+    bool direct_stage_dev = false;          // GCS_DIRECT_STAGE=device
     // test-only: GCS_FAULT_INJECT was set (to anything) when the context was
     // made, so the per-burst entry points look up its value per call; an
     // unarmed context never reads the environment on the burst path
@@ -752,6 +758,7 @@ void free_slot(Slot& s)
     if (s.d_frames) (void)hipFree(s.d_frames);
     if (s.d_off) (void)hipFree(s.d_off);
     if (s.d_len) (void)hipFree(s.d_len);
+    if (s.v_frames) (void)hipFree(s.v_frames);
     if (s.d_code) (void)hipFree(s.d_code);
     if (s.d_csum) (void)hipFree(s.d_csum);
     if (s.done) (void)hipEventDestroy(s.done);
@@ -1061,6 +1068,7 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
             h2d_src = base + s0;
         }
         // gather mode
+        uint8_t* gdst = s.h_frames;
         if (cnt == 0) {
             h2d_src = s.h_frames;
             while (next + cnt < n && cnt < ctx->max_frames) {
@@ -1075,14 +1083,24 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
             }
             if (cnt == 0)
                 return GCS_ERANGE;   // a single frame larger than the staging
+            if (ctx->direct_stage_dev && next == 0 && cnt == n && used <= ctx->direct_max) {
+                if (!s.v_frames)
+                    HIP_TRY(hipExtMallocWithFlags((void**)&s.v_frames, ctx->direct_max,
+                                                  hipDeviceMallocFinegrained));
+                gdst = s.v_frames;
+            }
             const uint32_t first = next;
             ctx->gather_run(cnt, used, [&, first](uint32_t lo, uint32_t hi) {
                 for (uint32_t k = lo; k < hi; k++) {
                     const uint8_t* src = frame_ptr(first + k);
                     if (src)
-                        std::memcpy(s.h_frames + s.h_off[k], src, s.h_len[k]);
+                        std::memcpy(gdst + s.h_off[k], src, s.h_len[k]);
                 }
             });
+            // device staging is written over the BAR, write-combined: drain
+            // it before the request's seq publishes the batch
+            if (gdst != s.h_frames)
+                __builtin_ia32_sfence();
         }
         s.first = next;
         s.count = cnt;
@@ -1093,7 +1111,7 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
         // submission latency.
         const bool direct = h2d_src == s.h_frames && next == 0 && cnt == n &&
                             used <= ctx->direct_max;
-        uint8_t* frames_d = direct ? s.m_frames : s.d_frames;
+        uint8_t* frames_d = direct ? (gdst != s.h_frames ? s.v_frames : s.m_frames) : s.d_frames;
         uint64_t* off_d = direct ? s.m_off : s.d_off;
         uint16_t* len_d = direct ? s.m_len : s.d_len;
         uint8_t* code_d = direct ? s.m_code : s.d_code;
@@ -1235,6 +1253,8 @@ try {
         ctx->direct_spread = std::atoi(e) != 0;
     if (const char* e = std::getenv("GCS_ASYNC_STAGE"))
         ctx->async_stage_dev = std::strcmp(e, "device") == 0;
+    if (const char* e = std::getenv("GCS_DIRECT_STAGE"))
+        ctx->direct_stage_dev = std::strcmp(e, "device") == 0;
     ctx->faults = std::getenv("GCS_FAULT_INJECT") != nullptr;
     if (const char* e = std::getenv("GCS_BURST_SERVER")) {
         // a context beyond the grid's kHubRings runs without it (GCS_ERANGE)

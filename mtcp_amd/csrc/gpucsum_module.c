@@ -247,17 +247,23 @@ static void gpucsum_init_handle(struct mtcp_thread_context *ctx)
 		 * device's grid; this one launches per burst */
 		/* fill as you go: a TX frame is complete once mTCP asks for the next
 		 * one or for its checksum (tcp_out.c:239-333); every
-		 * GPUCSUM_TX_GROUP (default 8, 0 = off) completed frames go to the
+		 * GPUCSUM_TX_GROUP (default 16, 0 = off) completed frames go to the
 		 * server while mTCP builds the rest, so send_pkts waits only for
-		 * the last group */
+		 * the last group (round 4, tools/tx_async_probe.py: send_pkts blocks
+		 * 6.6 / 6.2 us registered / pageable with 16, 8.7 / 5.8 with 8, 8.5 /
+		 * 9.1 with one batch) */
 		env = getenv("GPUCSUM_TX_GROUP");
-		g->tx_group = rc ? 0 : env ? (uint32_t)atoi(env) : 8;
-		/* verify as you go: recv_pkts posts the burst in groups of
-		 * GPUCSUM_RX_GROUP (default 16, 0 = off) frames and returns; get_rptr(i)
-		 * waits only for the group holding frame i, so mTCP processes the
-		 * first frames (core.c:792-795) while the GPU verifies the rest */
+		g->tx_group = rc ? 0 : env ? (uint32_t)atoi(env) : 16;
+		/* verify as you go (GPUCSUM_RX_GROUP > 0): recv_pkts posts the burst
+		 * in groups of that many frames and returns; get_rptr(i) waits only
+		 * for the group holding frame i, so mTCP processes the first frames
+		 * (core.c:792-795) while the GPU verifies the rest.  Default 0, one
+		 * batch per burst: under the reference's RX loop it blocks 9.5 us
+		 * per 64 x 1500 B burst in a registered pool against 11.5 us in
+		 * groups of 16 (pageable: 13.9 vs 13.0; tools/rx_async_probe.py) --
+		 * every group past the first costs its serving blocks one more poll */
 		env = getenv("GPUCSUM_RX_GROUP");
-		g->rx_group = rc ? 0 : env ? (uint32_t)atoi(env) : 16;
+		g->rx_group = rc ? 0 : env ? (uint32_t)atoi(env) : 0;
 	}
 	env = getenv("GPUCSUM_RSS_QUEUES");
 	if (env && atoi(env) > 0) {

@@ -128,15 +128,19 @@ def bursts(n_bursts, n, seed, jumbo=False):
     return out
 
 
-@pytest.mark.parametrize("idle_us,life_us,gap_s", [(200, 2000, 0.0), (30, 2000, 0.002),
-                                                   (200, 150, 0.0)])
-def test_burst_server_matches_oracle(torch_dev, monkeypatch, idle_us, life_us, gap_s):
+@pytest.mark.parametrize("idle_us,life_us,gap_s,stage", [(200, 2000, 0.0, "host"),
+                                                         (30, 2000, 0.002, "host"),
+                                                         (200, 150, 0.0, "host"),
+                                                         (200, 2000, 0.0, "device")])
+def test_burst_server_matches_oracle(torch_dev, monkeypatch, idle_us, life_us, gap_s, stage):
     """Bursts through the resident grid, including grids that leave between
     bursts (idle exit: gaps longer than GCS_SERVER_IDLE_US) and in the middle
-    of a run (lifetime exit): every burst is exact."""
+    of a run (lifetime exit), staged in pinned host or (GCS_DIRECT_STAGE)
+    device memory: every burst is exact."""
     import time
     monkeypatch.setenv("GCS_SERVER_IDLE_US", str(idle_us))
     monkeypatch.setenv("GCS_SERVER_LIFE_US", str(life_us))
+    monkeypatch.setenv("GCS_DIRECT_STAGE", stage)
     O = Oracle()
     with gpucsum.Context(0, max_frames=1024, max_bytes=4 << 20) as c:
         c.set_burst_server(True)

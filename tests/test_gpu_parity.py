@@ -573,14 +573,19 @@ def test_host_batches_chunked(torch_dev, O):
         assert (rv[bad] != 0).all()
 
 
-@pytest.mark.parametrize("direct,spread", [(0, 1), (1 << 30, 0), (1 << 30, 1)])
+@pytest.mark.parametrize("direct,spread,stage", [(0, 1, "host"), (1 << 30, 0, "host"),
+                                                 (1 << 30, 1, "host"), (1 << 30, 1, "device"),
+                                                 (1 << 30, 0, "device")])
 @pytest.mark.parametrize("n", [1, 64, 700])
-def test_host_bursts_direct_and_dma(torch_dev, O, monkeypatch, direct, spread, n):
+def test_host_bursts_direct_and_dma(torch_dev, O, monkeypatch, direct, spread, stage, n):
     """Small host batches (an mTCP burst) through both staging modes: DMA
-    copies, and direct mode (the kernel reads pinned staging over PCIe) on
-    the mixed and the spread descriptor kernel; jumbo frames included."""
+    copies, and direct mode (the kernel reads the staging in place) on the
+    mixed and the spread descriptor kernel, staged in pinned host memory or
+    (GCS_DIRECT_STAGE=device) in device memory written over the BAR; jumbo
+    frames included."""
     monkeypatch.setenv("GCS_DIRECT_MAX_BYTES", str(direct))
     monkeypatch.setenv("GCS_DIRECT_SPREAD", str(spread))
+    monkeypatch.setenv("GCS_DIRECT_STAGE", stage)
     lens = synth.imix_lengths(n, seed=41 + n)
     if n > 1:
         lens[n // 2] = 9000

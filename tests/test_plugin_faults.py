@@ -76,7 +76,11 @@ def unfilled(buf, off, lens):
 
 
 @pytest.mark.gpu
-def test_rx_verify_failure_returns_null(H, P, monkeypatch):  # noqa: F811
+@pytest.mark.parametrize("group", ["0", "16"])
+def test_rx_verify_failure_returns_null(H, P, monkeypatch, group):  # noqa: F811
+    """A failing RX verify, one batch per burst (group 0) or posted in groups
+    (16: the first post of each burst fails): every frame comes back NULL."""
+    monkeypatch.setenv("GPUCSUM_RX_GROUP", group)
     d = load("frames_rx")
     n = len(d["off"])
     c = Ctx(H, P, monkeypatch)
