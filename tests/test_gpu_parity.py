@@ -416,6 +416,13 @@ def test_desc_stream_passes_vs_oracle(torch_dev, ctx, O):
     d = dev(t, buf)
     st = t.zeros(n, dtype=t.uint8, device="cuda")
     cs = t.zeros(n, dtype=t.int32, device="cuda")
+    ctx.compute(d, doff, dlen, n, st, cs, flags=K["GCS_CF_NO_INPLACE"])
+    ctx.sync()
+    np.testing.assert_array_equal(host(d), buf)                 # untouched
+    np.testing.assert_array_equal(host(st), rst)
+    np.testing.assert_array_equal(host(cs).view(np.uint32), rcs)
+    st.zero_()
+    cs.zero_()
     ctx.compute(d, doff, dlen, n, st, cs)
     ctx.sync()
     np.testing.assert_array_equal(host(st), rst)
