@@ -726,9 +726,10 @@ def plugin_threads():
     """Bursts from several mTCP-like threads per GPU (tools/mt_probe.py), in a
     child process with HIP's default hardware queues, as the plugin runs."""
     import subprocess
+    env = dict(os.environ, MTP_LIGHT_THREADS="1,16,24")
     try:
         r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "mt_probe.py")],
-                           capture_output=True, text=True, timeout=180)
+                           capture_output=True, text=True, timeout=300, env=env)
         return json.loads(r.stdout.strip().splitlines()[-1])
     except Exception as e:   # a side measurement: report, never fail the bench line
         return {"error": repr(e)[:200]}

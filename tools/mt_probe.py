@@ -46,7 +46,7 @@ for threads in [int(x) for x in os.environ.get("MTP_THREADS", "1,4,8,12,16,24").
 # the same with new frames and the oracle check on every 16th burst only: the
 # threads' own CPU work no longer crowds the job's cores (cgroup quota above)
 os.environ["MT_CHECK_EVERY"] = "16"
-for threads in (1, 8, 12, 16, 24):
+for threads in [int(x) for x in os.environ.get("MTP_LIGHT_THREADS", "1,8,12,16,24").split(",") if x]:
     mis, fr, us = C.c_uint64(), C.c_uint64(), C.c_double()
     rc = M.mt_bursts(threads, 600, 1, C.byref(mis), C.byref(fr), C.byref(us))
     assert rc == 0 and mis.value == 0, (rc, mis.value)
