@@ -396,6 +396,7 @@ k_burst_server(HubMailbox* mb, HubPub* pub, uint64_t idle_ticks, uint64_t life_t
         }
         bool mine = false;
         uint64_t t_seen = 0, t_served = 0;
+        bool writes = false;
         if (act == WORK) {
             // a request: its lines were written before its seq (fence-acquire
             // after observing it: later loads see everything the host wrote)
@@ -403,6 +404,10 @@ k_burst_server(HubMailbox* mb, HubPub* pub, uint64_t idle_ticks, uint64_t life_t
             t_seen = __builtin_amdgcn_s_memrealtime();
             const uint4 a = s_line[0], b = s_line[1];
             const uint32_t n = a.z, compute = a.w & 1u, flags = a.w >> 1;
+            // frames written in place: a fill's check fields, or a verify's
+            // tcp_in.c:1237 side effect
+            writes = compute ? !(flags & GCS_CF_NO_INPLACE)
+                             : (flags & GCS_VF_ZERO_BAD_TCP_CHECK) != 0;
             uint8_t* frames = reinterpret_cast<uint8_t*>((uint64_t)b.x | ((uint64_t)b.y << 32));
             const uint64_t bytes = (uint64_t)b.z * 16;
             const uint4 d0 = s_line[2 + grp];
@@ -432,8 +437,12 @@ k_burst_server(HubMailbox* mb, HubPub* pub, uint64_t idle_ticks, uint64_t life_t
                 __syncthreads();
                 t_served = __builtin_amdgcn_s_memrealtime();
             }
-            if (mine)
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // this wave's results reach host memory
+            // frames written in place reach host memory before the ack; the
+            // records are system-scope stores of their own, so a request that
+            // writes no frame needs neither the release (an L2 write-back of
+            // the whole XCD) nor the ack
+            if (mine && writes)
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         }
         __syncthreads();                     // every wave done with s_line / s_claim
         if (t == 0) {
@@ -443,7 +452,7 @@ k_burst_server(HubMailbox* mb, HubPub* pub, uint64_t idle_ticks, uint64_t life_t
                 rm->prof[blk][2] = __builtin_amdgcn_s_memrealtime();
                 rm->prof[blk][3] = polls;
             }
-            if (mine)
+            if (mine && writes)
                 __hip_atomic_store(&rm->ack[blk].v, q, __ATOMIC_RELEASE,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(&pub->prog[r][blk], qend, __ATOMIC_RELAXED,
