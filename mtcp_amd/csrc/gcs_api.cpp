@@ -1084,8 +1084,10 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
             if (cnt == 0)
                 return GCS_ERANGE;   // a single frame larger than the staging
             if (ctx->direct_stage_dev && next == 0 && cnt == n && used <= ctx->direct_max) {
+                // a gathered batch never exceeds the slot's pinned staging
                 if (!s.v_frames)
-                    HIP_TRY(hipExtMallocWithFlags((void**)&s.v_frames, ctx->direct_max,
+                    HIP_TRY(hipExtMallocWithFlags((void**)&s.v_frames,
+                                                  std::min(ctx->direct_max, ctx->max_bytes),
                                                   hipDeviceMallocFinegrained));
                 gdst = s.v_frames;
             }

@@ -2265,6 +2265,7 @@ static hipError_t launch_fixed(uint8_t* frames, uint64_t stride, u32 frame_len, 
 }
 
 // (G, U) by frame size: G*16 B per load instruction of a group, U loads per lane.
+constexpr u32 kSmallMaxFrames = 4u << 20;   // RX <= 64 B: one lane per frame up to here
 template <bool COMPUTE, bool EXT>
 static hipError_t dispatch_fixed(uint8_t* frames, uint64_t stride, u32 frame_len, u32 n,
                                  uint8_t* code, uint32_t* csum, u32 flags, const Ext& ext,
@@ -2279,10 +2280,18 @@ static hipError_t dispatch_fixed(uint8_t* frames, uint64_t stride, u32 frame_len
         if (COMPUTE)
             return launch_fixed<4, 1, COMPUTE, false, EXT>(frames, stride, frame_len, n, code,
                                                            csum, flags, ext, s);
-        // Plain RX: 4 lanes per frame, 2 frames per group with both loads issued
-        // first.  8M x 64 B: 128 -> 95 us against one lane per frame, whose
-        // 64-B-strided loads fall behind once the batch leaves the Infinity
-        // Cache; 1M: 16.8 vs 16.6 us.
+        // Plain RX up to 4M frames: one lane per frame, plain loads (k_small):
+        // 14.0 / 22.9 / 40.3 us per 1M / 2M / 4M frames after a cache scrub
+        // against 16.2 / 31.2 / 51.6 us for 4 lanes and 2 frames per group
+        // (round 4, tools/kbench 64, KB_SCRUB; warm the same).  Beyond 4M the
+        // 64-B-strided loads of one lane per frame fall behind (8M: 108 vs
+        // 94 us), so larger batches take the 4-lane, 2-frame groups.
+        if (!EXT && n <= kSmallMaxFrames) {
+            hipLaunchKernelGGL((k_small<false, false, kXCD>), dim3((n + kBlock - 1) / kBlock),
+                               dim3(kBlock), 0, s, frames, stride, frame_len, n, code, csum,
+                               flags);
+            return hipGetLastError();
+        }
         if (!EXT)
             return launch_fixed<4, 1, COMPUTE, false, EXT, 2>(frames, stride, frame_len, n, code,
                                                               csum, flags, ext, s);

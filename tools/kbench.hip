@@ -1877,6 +1877,11 @@ int imix_main(uint64_t n, int rounds)
     // one pass per block (gridDim.y = 1) against kStreamPasses
     STREAM4(false, "shipped shape, 1 pass", 8, 8192, 8, WM_SECTOR_SC1, 1)
     STREAM4(true, "shipped shape, 1 pass FRESH", 8, 8192, 8, WM_SECTOR_SC1, 1)
+    // the verify's shape against round 3's (7 waves, 12K-chunk regions)
+    STREAM4(false, "U8 R12K occ8", 8, 12288, 8, WM_SECTOR_SC1, 3)
+    STREAM4(false, "U8 R8K occ7", 8, 8192, 7, WM_SECTOR_SC1, 3)
+    STREAM4(false, "U4 R8K occ8", 4, 8192, 8, WM_SECTOR_SC1, 3)
+    STREAM4(false, "U6 R8K occ8", 6, 8192, 8, WM_SECTOR_SC1, 3)
 #define STREAM3(C_, TAG, OCC_, HDR3_)                                                       \
     vs.push_back({std::string(C_ ? "compute" : "verify ") + " stream r03 " + TAG,           \
                   C_ ? cb : vb, [&](hipStream_t st) {                                      \
