@@ -302,8 +302,9 @@ int gcs_compute_ptrs(gcs_ctx *ctx, uint8_t *const *pkts, const uint16_t *len,
  * frame's check fields filled in place.  Until then the frames and the output
  * arrays must stay valid and the frames unmodified.  Frames all in one
  * registered region (gcs_host_register) at 16 B-aligned addresses are read
- * where they are; others are copied into the context's pinned async staging
- * (GCS_ASYNC_STAGE=device: into device memory over the BAR).  The checks come
+ * where they are; others are copied into the context's async staging: device
+ * memory written over the BAR (default), or pinned host memory
+ * (GCS_ASYNC_STAGE=host, or when the device allocation fails).  The checks come
  * back with the results; gcs_wait writes them into the frames.  Without the server, or for a batch larger than one request
  * (512 frames / 256 KiB staged), the fill runs synchronously and *ticket = 0.
  * gcs_wait(ctx, t) completes every async fill posted on ctx up to ticket t;

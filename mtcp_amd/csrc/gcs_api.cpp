@@ -694,8 +694,12 @@ struct gcs_ctx {
         uint8_t* d_stage = nullptr;         // its device view
         bool stage_dev = false;             // staging is device memory (hipFree)
     };
-    bool async_stage_dev = false;           // GCS_ASYNC_STAGE=device
-    bool direct_stage_dev = false;          // GCS_DIRECT_STAGE=device
+    // Bursts from pageable memory are staged in fine-grained device memory
+    // written over the BAR (default; GCS_ASYNC_STAGE / GCS_DIRECT_STAGE=host
+    // for pinned host staging): the GPU then reads HBM instead of PCIe.  A
+    // failed device allocation turns it off for the context (host staging).
+    bool async_stage_dev = true;            // gcs_*_ptrs_async
+    bool direct_stage_dev = true;           // direct-mode (burst) host batches
     // test-only: GCS_FAULT_INJECT was set (to anything) when the context was
     // made, so the per-burst entry points look up its value per call; an
     // unarmed context never reads the environment on the burst path
@@ -1085,11 +1089,16 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
                 return GCS_ERANGE;   // a single frame larger than the staging
             if (ctx->direct_stage_dev && next == 0 && cnt == n && used <= ctx->direct_max) {
                 // a gathered batch never exceeds the slot's pinned staging
-                if (!s.v_frames)
-                    HIP_TRY(hipExtMallocWithFlags((void**)&s.v_frames,
-                                                  std::min(ctx->direct_max, ctx->max_bytes),
-                                                  hipDeviceMallocFinegrained));
-                gdst = s.v_frames;
+                if (!s.v_frames &&
+                    hipExtMallocWithFlags((void**)&s.v_frames,
+                                          std::min(ctx->direct_max, ctx->max_bytes),
+                                          hipDeviceMallocFinegrained) != hipSuccess) {
+                    (void)hipGetLastError();
+                    s.v_frames = nullptr;
+                    ctx->direct_stage_dev = false;      // no host-mapped device memory
+                }
+                if (s.v_frames)
+                    gdst = s.v_frames;
             }
             const uint32_t first = next;
             ctx->gather_run(cnt, used, [&, first](uint32_t lo, uint32_t hi) {
@@ -1254,9 +1263,9 @@ try {
     if (const char* e = std::getenv("GCS_DIRECT_SPREAD"))
         ctx->direct_spread = std::atoi(e) != 0;
     if (const char* e = std::getenv("GCS_ASYNC_STAGE"))
-        ctx->async_stage_dev = std::strcmp(e, "device") == 0;
+        ctx->async_stage_dev = std::strcmp(e, "host") != 0;
     if (const char* e = std::getenv("GCS_DIRECT_STAGE"))
-        ctx->direct_stage_dev = std::strcmp(e, "device") == 0;
+        ctx->direct_stage_dev = std::strcmp(e, "host") != 0;
     ctx->faults = std::getenv("GCS_FAULT_INJECT") != nullptr;
     if (const char* e = std::getenv("GCS_BURST_SERVER")) {
         // a context beyond the grid's kHubRings runs without it (GCS_ERANGE)
@@ -1772,11 +1781,16 @@ int post_async(gcs_ctx* ctx, uint8_t* const* pkts, const uint16_t* len, uint32_t
     uint64_t bytes = reg.bytes & ~15ull;
     if (a.staged) {
         if (!a.h_stage) {
-            if (ctx->async_stage_dev) {
+            if (ctx->async_stage_dev &&
+                hipExtMallocWithFlags((void**)&a.h_stage, kAsyncStageBytes,
+                                      hipDeviceMallocFinegrained) != hipSuccess) {
+                (void)hipGetLastError();
+                a.h_stage = nullptr;
+                ctx->async_stage_dev = false;           // no host-mapped device memory
+            }
+            if (a.h_stage) {
                 // staging in fine-grained device memory, written by the host
                 // over the BAR: the GPU then reads the frames from HBM
-                HIP_TRY(hipExtMallocWithFlags((void**)&a.h_stage, kAsyncStageBytes,
-                                              hipDeviceMallocFinegrained));
                 a.d_stage = a.h_stage;
                 a.stage_dev = true;
             } else {

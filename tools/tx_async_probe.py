@@ -69,7 +69,7 @@ out = {"workload": f"{BURSTS} bursts of {BURST} x {L}B TCP frames through mini_t
        "timer": "C clock_gettime around each send_pkts and each burst"}
 ctx = C.create_string_buffer(64)
 out["software_path"] = run(vtab(H, "synth_module_func"), C.addressof(ctx), False)
-MODES = [(False, g, "host") for g in ("0", "8", "16")] + [(False, "8", "device")] + \
+MODES = [(False, g, "host") for g in ("0", "8", "16")] + [(False, "8", "device"), (False, "16", "device")] + \
         [(True, g, "host") for g in ("0", "8", "16")] + [(True, None, "host"), (False, None, "host")]
 if os.environ.get("TXP_SMALL_GROUPS"):
     MODES += [(False, g, st) for g in ("2", "4") for st in ("host", "device")]
