@@ -2538,6 +2538,34 @@ int lro_main(uint64_t n, int rounds)
     }});
     // (round 3's k_gro PROBE = 1, phases A-C + D1 alone: 69-91 us for this batch,
     // profiles/r03/kbench_lro_*.log; the knob left the product kernel in round 4)
+    // the same frames in 2 KiB rooms (sparse descriptors: no block streams)
+    const uint64_t sstride = 2048;
+    uint8_t *sp, *vd2;
+    uint64_t* sp_off;
+    CK(hipMalloc(&sp, n * sstride));
+    CK(hipMalloc(&vd2, n));
+    CK(hipMalloc(&sp_off, 8 * n));
+    CK(hipMemcpy2DAsync(sp, sstride, in, stride, stride, n, hipMemcpyDeviceToDevice, s));
+    {
+        std::vector<uint64_t> h(n);
+        for (uint64_t i = 0; i < n; i++) h[i] = i * sstride;
+        CK(hipMemcpy(sp_off, h.data(), 8 * n, hipMemcpyHostToDevice));
+    }
+    vs.push_back({"verify sparse 2 KiB rooms (launch_verify_desc: 7 waves, 32x3)", (double)n * (L + 1),
+                  [&](hipStream_t st) {
+        CK(launch_verify_desc(sp, n * sstride, sp_off, lens, (u32)n, vd, 0u, st));
+    }});
+    vs.push_back({"verify sparse 2 KiB rooms (8 waves, 64x1: round-4 first form)", (double)n * (L + 1),
+                  [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_desc_stream<StreamShape<8, 8192, 8, 3, 64, 1>, false, WM_SECTOR_SC1, true>),
+                           dim3((n + 255) / 256, 3), dim3(256), 0, st, sp, n * sstride, sp_off, lens,
+                           (u32)n, vd2, nullptr, 0u);
+    }});
+    vs.push_back({"verify packed 1536 B (8 waves, 64x1)", (double)n * (L + 1), [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_desc_stream<StreamShape<8, 8192, 8, 3, 64, 1>, false, WM_SECTOR_SC1, true>),
+                           dim3((n + 255) / 256, 3), dim3(256), 0, st, in, n * stride, off, lens,
+                           (u32)n, vd2, nullptr, 0u);
+    }});
     vs.push_back({"verify (launch_verify_desc) for scale", (double)n * (L + 1), [&](hipStream_t st) {
         CK(launch_verify_desc(in, n * stride, off, lens, (u32)n, vd, 0u, st));
     }});
