@@ -1877,6 +1877,13 @@ int imix_main(uint64_t n, int rounds)
     // one pass per block (gridDim.y = 1) against kStreamPasses
     STREAM4(false, "shipped shape, 1 pass", 8, 8192, 8, WM_SECTOR_SC1, 1)
     STREAM4(true, "shipped shape, 1 pass FRESH", 8, 8192, 8, WM_SECTOR_SC1, 1)
+    // TX at 7 waves with a 32 x 2 per-frame path (the shipped fill: 8 waves, 64 x 1)
+    vs.push_back({"compute stream 7 waves, 32x2 per-frame path FRESH", cb, [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_desc_stream<StreamShape<8, 8192, 7, 4, 32, 2>, true, WM_SECTOR_SC1, true>),
+                           dim3((n + 255) / 256, 3), dim3(256), 0, st, tx, total, doff, dlen,
+                           (u32)n, nullptr, nullptr, 0u);
+    }});
+    vs.back().prep = zero_prep;
     // the verify's shape against round 3's (7 waves, 12K-chunk regions)
     STREAM4(false, "U8 R12K occ8", 8, 12288, 8, WM_SECTOR_SC1, 3)
     STREAM4(false, "U8 R8K occ7", 8, 8192, 7, WM_SECTOR_SC1, 3)
@@ -2560,6 +2567,15 @@ int lro_main(uint64_t n, int rounds)
         hipLaunchKernelGGL((k_desc_stream<StreamShape<8, 8192, 8, 3, 64, 1>, false, WM_SECTOR_SC1, true>),
                            dim3((n + 255) / 256, 3), dim3(256), 0, st, sp, n * sstride, sp_off, lens,
                            (u32)n, vd2, nullptr, 0u);
+    }});
+    vs.push_back({"fill sparse 2 KiB rooms (launch_compute_desc: 8 waves, 64x1)", (double)n * (L + 4),
+                  [&](hipStream_t st) {
+        CK(launch_compute_desc(sp, n * sstride, sp_off, lens, (u32)n, nullptr, nullptr, 0u, st));
+    }});
+    vs.push_back({"fill sparse 2 KiB rooms (7 waves, 32x2)", (double)n * (L + 4), [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_desc_stream<StreamShape<8, 8192, 7, 4, 32, 2>, true, WM_SECTOR_SC1, true>),
+                           dim3((n + 255) / 256, 3), dim3(256), 0, st, sp, n * sstride, sp_off, lens,
+                           (u32)n, nullptr, nullptr, 0u);
     }});
     vs.push_back({"verify packed 1536 B (8 waves, 64x1)", (double)n * (L + 1), [&](hipStream_t st) {
         hipLaunchKernelGGL((k_desc_stream<StreamShape<8, 8192, 8, 3, 64, 1>, false, WM_SECTOR_SC1, true>),
