@@ -2345,12 +2345,13 @@ hipError_t launch_classify_fixed(uint8_t* frames, uint64_t stride, u32 frame_len
 // kbench_imix_stream_wm*.log), RX chunks 0..2 (ihl = 5 fast frames; HDR3:
 // 240.7-245.7 vs 249-255 us interleaved, kbench_imix_stream_h3*.log).  With the
 // class passes out of the kernel both run 8 waves per SIMD (round 4).
-// The verify runs 7 waves per SIMD: 72 VGPRs hold its per-frame path in
-// k_desc<32,3>'s shape (32 lanes x 3 chunks, no spill), for blocks that do not
-// stream (sparse descriptors such as 2 KiB mbuf rooms); at 8 waves only 64 x 1
-// fits.  The fill keeps 8 waves (329 vs 345 us for C3 at 6), and 64 x 1.
+// Both run 7 waves per SIMD: 72 VGPRs hold the per-frame path in k_desc's
+// shape (verify 32 lanes x 3 chunks, fill 32 x 2, no spill), for blocks that do
+// not stream (sparse descriptors such as 2 KiB mbuf rooms); at 8 waves only
+// 64 x 1 fits.  Sparse 2 KiB rooms: verify 274 vs 402 us, fill 365 vs 448 us;
+// packed C3 fill 333.8 vs 331.3 us at 8 waves (r04_kbench_*_tx7.log).
 template <bool COMPUTE>
-using StreamShip = std::conditional_t<COMPUTE, StreamShape<8, 8192, 8, 4, 64, 1>,
+using StreamShip = std::conditional_t<COMPUTE, StreamShape<8, 8192, 7, 4, 32, 2>,
                                       StreamShape<8, 8192, 7, 3, 32, 3>>;
 // passes per block region (blockIdx.y): 3 x 8,192 chunks hold 256 packed
 // frames of up to 1,536 B; what a block has beyond them goes per frame
