@@ -480,6 +480,59 @@ def test_desc_mtu_batch_not_serialised(torch_dev, ctx, O):
     assert min(ms) < 3.0, ms
 
 
+def test_desc_sparse_rooms_vs_oracle(torch_dev, ctx, O):
+    """Frames one per 2 KiB room, as mbufs hand them over (dpdk_module.c's
+    rings): no block streams, so every frame takes the stream kernel's
+    per-frame path (TX 32 x 2, RX 32 x 3 at 7 waves per SIMD).  Mixed lengths
+    (empty, runts, odd, MTU), IP options, padded segments and UDP frames, TX
+    and RX (with and without the tcp_in.c:1237 side effect) bit-exact against
+    the oracle."""
+    t = torch_dev
+    n, room = 256 * 5 + 33, 2048
+    rng = np.random.default_rng(0x5A2E)
+    lens = rng.integers(60, 1515, size=n).astype(np.uint16)
+    lens[::97] = 0
+    lens[5::89] = rng.integers(1, 54, size=len(lens[5::89]))
+    off = np.arange(n, dtype=np.uint64) * room
+    buf = rng.integers(0, 256, size=n * room, dtype=np.uint8)
+    for i in range(n):
+        L = int(lens[i])
+        if L < 54:
+            continue
+        ihl = 5 if rng.random() > 0.1 else int(rng.integers(6, 16))
+        if 14 + 4 * ihl + 20 > L:
+            ihl = 5
+        tot = L - 14
+        if rng.random() < 0.1:                                   # Ethernet padding
+            tot = max(4 * ihl + 20, tot - int(rng.integers(1, 40)))
+        set_tcp_headers(buf, int(off[i]), L, ihl, tot)
+        if rng.random() < 0.03:
+            buf[int(off[i]) + 23] = 17
+    doff, dlen = dev(t, off.view(np.int64)), dev(t, lens.view(np.int16))
+    ref = buf.copy()
+    rst, rcs = O.compute_batch(ref, off, lens)
+    assert len(np.unique(rst)) >= 3
+    d = dev(t, buf)
+    st = t.zeros(n, dtype=t.uint8, device="cuda")
+    cs = t.zeros(n, dtype=t.int32, device="cuda")
+    ctx.compute(d, doff, dlen, n, st, cs)
+    ctx.sync()
+    np.testing.assert_array_equal(host(st), rst)
+    np.testing.assert_array_equal(host(cs).view(np.uint32), rcs)
+    np.testing.assert_array_equal(host(d), ref)
+    synth.corrupt(ref, off, np.maximum(lens, 15), frac_log2=3, seed=0x5A2F)
+    for flags in (0, 1):
+        d = dev(t, ref)
+        v = t.full((n,), 0xEE, dtype=t.uint8, device="cuda")
+        ctx.verify(d, doff, dlen, n, v, flags=flags)
+        ctx.sync()
+        exp = ref.copy()
+        rv = O.verify_batch(exp, off, lens, flags=flags)
+        np.testing.assert_array_equal(host(v), rv)
+        np.testing.assert_array_equal(host(d), exp)
+        assert len(np.unique(rv)) >= 3
+
+
 def test_desc_stream_region_at_buffer_end(torch_dev, ctx, O):
     """A streaming block whose region ends exactly at frames_bytes (16 B-
     aligned: streamed; not aligned: the block falls back to guarded loads)."""
