@@ -70,7 +70,8 @@ out = {"workload": f"{BURSTS} bursts of {BURST} x {L}B TCP frames through mini_t
 ctx = C.create_string_buffer(64)
 out["software_path"] = run(vtab(H, "synth_module_func"), C.addressof(ctx), False)
 MODES = [(False, g, "host") for g in ("0", "8", "16")] + [(False, "8", "device"), (False, "16", "device")] + \
-        [(True, g, "host") for g in ("0", "8", "16")] + [(True, None, "host"), (False, None, "host")]
+        [(True, g, "host") for g in ("0", "8", "16")] + [(True, None, "host"), (False, None, "host")] + \
+        [(True, "16", "regstage")]
 if os.environ.get("TXP_SMALL_GROUPS"):
     MODES += [(False, g, st) for g in ("2", "4") for st in ("host", "device")]
 for registered, group, stage in MODES:
@@ -78,7 +79,8 @@ for registered, group, stage in MODES:
             os.environ.pop("GPUCSUM_TX_GROUP", None)
         else:
             os.environ["GPUCSUM_TX_GROUP"] = group
-        os.environ["GCS_ASYNC_STAGE"] = stage
+        os.environ["GCS_ASYNC_STAGE"] = "device" if stage == "regstage" else stage
+        os.environ["GCS_ASYNC_REGISTERED"] = "stage" if stage == "regstage" else "inplace"
         assert P.gpucsum_set_inner(vtab(H, "synth_module_func")) == 0
         iom = vtab(P, "gpucsum_module_func")
         dctx = C.create_string_buffer(64)
@@ -88,5 +90,5 @@ for registered, group, stage in MODES:
         finally:
             H.mini_stop(iom, C.addressof(dctx))
         out[f"{'registered' if registered else 'pageable'}_group{group or 'default'}"
-            + ("_devstage" if stage == "device" else "")] = r
+            + {"device": "_devstage", "regstage": "_devstage"}.get(stage, "")] = r
 print(json.dumps(out))
