@@ -154,6 +154,33 @@ int gcs_sync(gcs_ctx *ctx);                               /* wait for ctx stream
  * the environment variable GCS_BURST_SERVER=1 at gcs_ctx_create. */
 int gcs_ctx_set_burst_server(gcs_ctx *ctx, int on);
 
+/* The burst server's figures for this context's ring since it was turned on
+ * (like mTCP's per-thread NETSTAT, core.c:189-218).  requests and
+ * post_to_done_us always; the GPU-side parts only when the process ran with
+ * GCS_SERVER_PROF set (a profiling build of the grid: clock reads and a wait
+ * after each phase), else 0.  Per-block figures are means over the (block,
+ * request) pairs that served frames.  GCS_EINVAL without the server. */
+typedef struct gcs_server_stats {
+    uint64_t requests;        /* requests completed on this ring                      */
+    uint64_t block_requests;  /* (block, request) pairs that served frames            */
+    uint64_t polls;           /* polls by the ring's blocks                           */
+    double post_to_done_us;   /* mean per request: posted -> completed (host clock)   */
+    double gpu_span_us;       /* mean: first serving block saw it -> last one's
+                                 records stored (GPU clock)                           */
+    double poll_us;           /* one poll: issue -> data back, every poll             */
+    double seen_poll_us;      /* ... the polls that saw a request                     */
+    double acquire_us;        /* the acquire fence after that poll                    */
+    double frames_us;         /* frame loads and folds, record stores issued          */
+    double records_us;        /* the record stores acknowledged                       */
+    double release_us;        /* release fence + ack (requests that wrote frames)     */
+    double seen_skew_us;      /* mean per request: last serving block saw it - first  */
+    double block_serve_us;    /* mean per request: the slowest block, saw it -> its
+                                 records stored                                       */
+    double cold_frac;         /* (block, request) pairs whose block was cold (polling
+                                 the leader's copy) when the request came             */
+} gcs_server_stats;
+int gcs_server_stats_get(gcs_ctx *ctx, gcs_server_stats *out);
+
 /* Pinned host memory for zero-copy host batches: when every frame of a
  * gcs_verify / gcs_compute call lies in pinned memory (allocated here, or an
  * existing buffer such as an mbuf pool registered with gcs_host_register) and
@@ -320,7 +347,13 @@ int gcs_compute_ptrs_async(gcs_ctx *ctx, uint8_t *const *pkts, const uint16_t *l
  * and the frames unmodified until then.  Flags other than
  * GCS_VF_ZERO_BAD_TCP_CHECK, no server, or more than one request's frames:
  * verified synchronously, *ticket = 0.  Async fills and verifies share the
- * context's request ring and complete in posting order. */
+ * context's request ring and complete in posting order.
+ * A gcs_wait that fails (no answer from the GPU) cancels every pending async
+ * request: their outputs and frames are never written.  That failure is the
+ * report for every cancelled request of the kind (fill or verify) of the
+ * ticket it waited for; a cancelled request of the other kind is reported
+ * once, by the first later gcs_wait for a ticket of its kind that covers it
+ * (GCS_EHIP).  Requests posted after the failure are never reported for it. */
 int gcs_verify_ptrs_async(gcs_ctx *ctx, uint8_t *const *pkts, const uint16_t *len,
                           uint32_t n, uint8_t *verdict, uint32_t flags, uint64_t *ticket);
 int gcs_wait(gcs_ctx *ctx, uint64_t ticket);

@@ -22,6 +22,8 @@
 #include <thread>
 #include <vector>
 
+#include <emmintrin.h>
+
 #include "gcs_internal.h"
 
 namespace {
@@ -282,16 +284,23 @@ class ServerHub {
         if (rc) return rc;
         read_knobs();
         std::memset(&mb_->ring[k], 0, sizeof(gcs::ServerMailbox));
+        std::memset(&rq_->req[k], 0, sizeof rq_->req[k]);
         // every slot reads as holding `start` (done): a slot left at 0 would
         // read as NEWER than the next request near the 32-bit wrap, and be
         // skipped as done
-        for (auto& sl : mb_->ring[k].slot)
+        for (auto& sl : rq_->req[k])
             sl.a.seq = start;
+        if (dev_mailbox_)
+            _mm_sfence();                 // write-combined over the BAR
         // ... and every block's ack reads as `start` (nothing served yet): an
         // ack left at 0 would read as NEWER than a request >= 2^31 past it,
         // and complete an in-place request before its release fence
+        // (test-only GCS_SERVER_ACK_SKEW: join with acks that stale, as after
+        // 2^31 requests that wrote no frame; the grid must refresh them)
+        const char* sk = std::getenv("GCS_SERVER_ACK_SKEW");
+        const uint32_t skew = sk ? (uint32_t)std::strtoul(sk, nullptr, 0) : 0u;
         for (auto& a : mb_->ring[k].ack)
-            a.v = start;
+            a.v = start + skew;
         // the ring starts at `start` on the device too: nothing claimed yet
         uint32_t prog[gcs::kServerBlocks];
         for (auto& p : prog)
@@ -351,6 +360,8 @@ class ServerHub {
     }
 
     gcs::ServerMailbox* ring(int r) { return &mb_->ring[r]; }
+    gcs::ServerReq* reqs(int r) { return rq_->req[r]; }
+    bool dev_mailbox() const { return dev_mailbox_; }
     bool prof() const { return prof_; }
     double ticks_per_us() const { return ticks_per_us_; }
 
@@ -361,6 +372,41 @@ class ServerHub {
                               hipHostMallocCoherent | hipHostMallocMapped));
         std::memset(mb_, 0, sizeof(gcs::HubMailbox));
         HIP_TRY(hipHostGetDevicePointer((void**)&dmb_, mb_, 0));
+        // The request lines: uncached device memory the host writes over the
+        // BAR (default), so a poll reads HBM and puts nothing on the PCIe
+        // link: a poll takes 0.64-0.68 us at 1-16 rings, against 1.8 -> 8 us
+        // over PCIe in pinned host memory (GCS_SERVER_MAILBOX=host, or when
+        // the allocation fails).  The records stay in host
+        // memory either way.
+        const char* mbx = std::getenv("GCS_SERVER_MAILBOX");
+        if (!mbx || std::strcmp(mbx, "host") != 0) {
+            if (hipExtMallocWithFlags((void**)&rq_, sizeof(gcs::HubReqs),
+                                      hipDeviceMallocUncached) == hipSuccess) {
+                drq_ = rq_;
+                dev_mailbox_ = true;
+            } else {
+                (void)hipGetLastError();
+                rq_ = nullptr;
+            }
+        }
+        if (!rq_) {
+            HIP_TRY(hipHostMalloc((void**)&rq_, sizeof(gcs::HubReqs),
+                                  hipHostMallocCoherent | hipHostMallocMapped));
+            HIP_TRY(hipHostGetDevicePointer((void**)&drq_, rq_, 0));
+        }
+        std::memset(rq_, 0, sizeof(gcs::HubReqs));
+        if (dev_mailbox_)
+            _mm_sfence();
+        // GCS_SERVER_ACQUIRE (A/B knobs, gcs_internal.h kServerAcq*): agent =
+        // every acquire at agent scope (frames in registered host memory may
+        // then be read from a stale L2 line); none = no acquire for frames in
+        // device staging.  Default: agent scope for device frames, system
+        // scope for host frames.
+        const char* acq = std::getenv("GCS_SERVER_ACQUIRE");
+        opts_ = !acq                         ? 0u
+                : std::strcmp(acq, "agent") == 0 ? gcs::kServerAcqAgent
+                : std::strcmp(acq, "none") == 0  ? gcs::kServerAcqNone
+                                                 : 0u;
         HIP_TRY(hipMalloc((void**)&dpub_, sizeof(gcs::HubPub)));
         HIP_TRY(hipMemset(dpub_, 0, sizeof(gcs::HubPub)));
         // the highest priority: a queue pool of its own, so the resident grid
@@ -404,10 +450,12 @@ class ServerHub {
                                     : ~0ull;
         // extra ~2 us naps between the polls of a block with no hot ring, and
         // of a hot one (an A/B knob for the PCIe cost of hot polling)
+        // (clamped to [0, 0xFFFF]: a negative value must not become a huge
+        // unsigned nap count that stops the grid from serving)
         e = std::getenv("GCS_SERVER_COLD_NAPS");
-        naps_ = e ? (uint32_t)std::min(std::atoi(e), 0xFFFF) : 0;
+        naps_ = e ? (uint32_t)std::clamp(std::atoi(e), 0, 0xFFFF) : 0u;
         e = std::getenv("GCS_SERVER_HOT_NAPS");
-        naps_ |= (e ? (uint32_t)std::min(std::atoi(e), 0xFFFF) : 0u) << 16;
+        naps_ |= (e ? (uint32_t)std::clamp(std::atoi(e), 0, 0xFFFF) : 0u) << 16;
     }
 
     // Every block ends within life_ticks of its start (or at the exit
@@ -441,9 +489,9 @@ class ServerHub {
         // this copy completed (stop_locked synchronises the stream)
         HIP_TRY(hipMemcpyAsync(dpub_->ring_of, ring_of_, groups * sizeof(uint32_t),
                                hipMemcpyHostToDevice, stream_));
-        HIP_TRY(gcs::launch_burst_server(dmb_, dpub_, groups, idle_ticks_, life_ticks_,
-                                         hot_ticks_, hot_max_ticks_, kMaxPolls, naps_, prof_,
-                                         stream_));
+        HIP_TRY(gcs::launch_burst_server(dmb_, drq_, dpub_, groups, idle_ticks_, life_ticks_,
+                                         hot_ticks_, hot_max_ticks_, kMaxPolls, naps_, opts_,
+                                         prof_, stream_));
         launched_.store(true, std::memory_order_release);
         return GCS_OK;
     }
@@ -452,6 +500,10 @@ class ServerHub {
     std::mutex mu_;
     gcs::HubMailbox* mb_ = nullptr;       // host view
     gcs::HubMailbox* dmb_ = nullptr;      // device view
+    gcs::HubReqs* rq_ = nullptr;          // request lines, host view
+    gcs::HubReqs* drq_ = nullptr;         // ... device view
+    bool dev_mailbox_ = false;            // rq_ is device memory (write-combined BAR)
+    uint32_t opts_ = 0;                   // launch_burst_server opts
     gcs::HubPub* dpub_ = nullptr;         // device memory
     hipStream_t stream_ = nullptr;
     uint32_t mask_ = 0;                   // rings in use
@@ -470,13 +522,20 @@ class BurstServer {
   public:
     ~BurstServer()
     {
-        if (prof_n_)
+        if (prof_n_) {
+            gcs_server_stats st;
+            stats(&st);
             std::fprintf(stderr,
                          "[gcs burst server] %llu requests: request writes %.2f us; post->done "
-                         "%.2f us, of which serving %.2f us and release fence %.2f us "
-                         "(slowest block)\n",
-                         (unsigned long long)prof_n_, prof_write_ / prof_n_, prof_total_ / prof_n_,
-                         prof_serve_ / prof_n_, prof_release_ / prof_n_);
+                         "%.2f us, GPU span %.2f us (%llu measured); per block: poll %.2f us "
+                         "(seen %.2f), acquire %.2f, frames %.2f, records %.2f, release %.2f; "
+                         "seen skew %.2f, slowest block %.2f, cold %.2f\n",
+                         (unsigned long long)st.requests, prof_write_ / prof_n_,
+                         st.post_to_done_us, st.gpu_span_us, (unsigned long long)prof_n_,
+                         st.poll_us, st.seen_poll_us, st.acquire_us, st.frames_us,
+                         st.records_us, st.release_us, st.seen_skew_us, st.block_serve_us,
+                         st.cold_frac);
+        }
         if (hub_ && r_ >= 0) {
             (void)wait(posted_);
             (void)hub_->leave(r_);
@@ -497,6 +556,8 @@ class BurstServer {
         int rc = hub_->join(done_, &r_);
         if (rc) return rc;
         mb_ = hub_->ring(r_);
+        rq_ = hub_->reqs(r_);
+        dev_ = hub_->dev_mailbox();
         return GCS_OK;
     }
 
@@ -507,9 +568,11 @@ class BurstServer {
     // in_place: the kernel writes the frames themselves (host memory), so
     // completion also waits for the serving blocks' release + ack; otherwise
     // the tagged result records alone complete it.
+    // dev_frames: the frames are in device memory (device staging), so an
+    // agent-scope acquire makes them visible (gcs_internal.h kModeDevFrames).
     int post(uint8_t* frames, uint64_t bytes, const uint64_t* off, const uint16_t* len,
              uint32_t n, bool compute, uint32_t flags, uint8_t* code, uint32_t* csum,
-             bool in_place, uint32_t* ticket)
+             bool in_place, bool dev_frames, uint32_t* ticket)
     {
         const uint32_t q = gcs::server_next(posted_);
         Req& r = req_[q % gcs::kServerSlots];
@@ -519,24 +582,48 @@ class BurstServer {
         }
         int rc = hub_->ensure(r_);
         if (rc) return rc;
-        gcs::ServerSlot& sl = mb_->slot[q % gcs::kServerSlots];
+        gcs::ServerReq& sl = rq_[q % gcs::kServerSlots];
         const auto tw = std::chrono::steady_clock::now();
-        std::memset(sl.rec, 0, n * sizeof(uint64_t));   // no record of an older request
-        // each 16 B line: its fields, then its seq (x86 keeps the order)
-        for (uint32_t i = 0; i < n; i++) {
-            gcs::ServerDesc& d = sl.desc[i];
-            d.off = off[i];
-            d.len = len[i];
-            __atomic_store_n(&d.seq, q, __ATOMIC_RELEASE);
+        std::memset(mb_->res[q % gcs::kServerSlots].rec, 0, n * sizeof(uint64_t));   // no record
+                                                                                     // of an older request
+        const uint32_t mode = (compute ? 1u : 0u) | (flags << 1) |
+                              (dev_frames ? gcs::kModeDevFrames : 0u);
+        if (dev_) {
+            // Device memory over the BAR, write-combined: each 16 B line goes
+            // out as ONE aligned 16 B store carrying its seq (a line is read
+            // in one piece), the descriptors and line B first, then (sfence)
+            // line A, then sfence again so the request leaves the
+            // write-combining buffers now.
+            for (uint32_t i = 0; i < n; i++)
+                _mm_store_si128(reinterpret_cast<__m128i*>(&sl.desc[i]),
+                                _mm_set_epi32((int)q, (int)len[i], (int)(uint32_t)(off[i] >> 32),
+                                              (int)(uint32_t)off[i]));
+            const uint64_t fa = reinterpret_cast<uint64_t>(frames);
+            _mm_store_si128(reinterpret_cast<__m128i*>(&sl.b),
+                            _mm_set_epi32((int)q, (int)(uint32_t)(bytes / 16),
+                                          (int)(uint32_t)(fa >> 32), (int)(uint32_t)fa));
+            _mm_sfence();
+            r = Req{q, n, compute, in_place, true, code, csum, 0, std::chrono::steady_clock::now()};
+            _mm_store_si128(reinterpret_cast<__m128i*>(&sl.a),
+                            _mm_set_epi32((int)mode, (int)n, 0, (int)q));
+            _mm_sfence();
+        } else {
+            // each 16 B line: its fields, then its seq (x86 keeps the order)
+            for (uint32_t i = 0; i < n; i++) {
+                gcs::ServerDesc& d = sl.desc[i];
+                d.off = off[i];
+                d.len = len[i];
+                __atomic_store_n(&d.seq, q, __ATOMIC_RELEASE);
+            }
+            sl.b.frames = reinterpret_cast<uint64_t>(frames);
+            sl.b.bytes16 = (uint32_t)(bytes / 16);
+            __atomic_store_n(&sl.b.seq, q, __ATOMIC_RELEASE);
+            sl.a.n = n;
+            sl.a.mode = mode;
+            sl.a.cmd = 0;
+            r = Req{q, n, compute, in_place, true, code, csum, 0, std::chrono::steady_clock::now()};
+            __atomic_store_n(&sl.a.seq, q, __ATOMIC_RELEASE);
         }
-        sl.b.frames = reinterpret_cast<uint64_t>(frames);
-        sl.b.bytes16 = (uint32_t)(bytes / 16);
-        __atomic_store_n(&sl.b.seq, q, __ATOMIC_RELEASE);
-        sl.a.n = n;
-        sl.a.mode = (compute ? 1u : 0u) | (flags << 1);
-        sl.a.cmd = 0;
-        r = Req{q, n, compute, in_place, true, code, csum, 0, std::chrono::steady_clock::now()};
-        __atomic_store_n(&sl.a.seq, q, __ATOMIC_RELEASE);
         if (hub_->prof())
             prof_write_ += std::chrono::duration<double, std::micro>(r.t0 - tw).count();
         posted_ = q;
@@ -561,13 +648,14 @@ class BurstServer {
     // Serve one batch (n <= gcs::kServerMaxFrames) and return when it is done.
     int serve(uint8_t* frames, uint64_t bytes, const uint64_t* off, const uint16_t* len,
               uint32_t n, bool compute, uint32_t flags, uint8_t* code, uint32_t* csum,
-              bool in_place = false)
+              bool in_place, bool dev_frames)
     {
         uint32_t q = done_;
         for (uint32_t k = 0; k < n; k += gcs::kSlotFrames) {
             const uint32_t m = std::min<uint32_t>(gcs::kSlotFrames, n - k);
             int rc = post(frames, bytes, off + k, len + k, m, compute, flags,
-                          code ? code + k : nullptr, csum ? csum + k : nullptr, in_place, &q);
+                          code ? code + k : nullptr, csum ? csum + k : nullptr, in_place,
+                          dev_frames, &q);
             if (rc) return rc;
         }
         return wait(q);
@@ -591,7 +679,7 @@ class BurstServer {
     int complete(Req& r)
     {
         const uint64_t tag = (uint64_t)(r.q & 0xFFFFu) << 48;
-        gcs::ServerSlot& sl = mb_->slot[r.q % gcs::kServerSlots];
+        gcs::ServerRes& sl = mb_->res[r.q % gcs::kServerSlots];
         const int nb = (int)std::min<uint32_t>(gcs::kServerBlocks,
                                                (r.n + gcs::kServerFPB - 1) / gcs::kServerFPB);
         const auto t0 = std::chrono::steady_clock::now();
@@ -628,32 +716,87 @@ class BurstServer {
             if (r.compute && r.csum) r.csum[i] = (uint32_t)v;
         }
         r.pending = false;
-        if (hub_->prof()) {
-            // GCS_SERVER_PROF: per request, the slowest serving block's serve
-            // and release times (wall clock), averaged and printed at exit
-            double sv = 0, rl = 0;
+        const double total = std::chrono::duration<double, std::micro>(
+                                 std::chrono::steady_clock::now() - r.t0).count();
+        n_done_++;
+        total_us_ += total;
+        if (hub_->prof() && r.n) {
+            // GCS_SERVER_PROF: the request's GPU span, from the first serving
+            // block's poll that saw it to the last one's records stored (GPU
+            // wall clock).  A block writes its marks after its records, so
+            // wait briefly for each serving block's tag; a block that has
+            // already moved on to a later request is left out.
+            uint64_t seen = ~0ull, seen_max = 0, rec = 0, serve = 0;
+            const auto tp = std::chrono::steady_clock::now();
             for (int k = 0; k < nb; k++) {
                 const int b = gcs::server_block(r.q, (uint32_t)k * gcs::kServerFPB);
-                sv = std::max(sv, (double)(mb_->prof[b][1] - mb_->prof[b][0]));
-                rl = std::max(rl, (double)(mb_->prof[b][2] - mb_->prof[b][1]));
+                int32_t d;
+                while ((d = (int32_t)((uint32_t)__atomic_load_n(&mb_->prof[b][gcs::kProfTag],
+                                                                __ATOMIC_ACQUIRE) - r.q)) < 0 &&
+                       std::chrono::steady_clock::now() - tp < std::chrono::microseconds(200))
+                    __builtin_ia32_pause();
+                if (d != 0)
+                    continue;
+                const uint64_t s0 = mb_->prof[b][gcs::kProfSeen], r0 = mb_->prof[b][gcs::kProfRec];
+                seen = std::min(seen, s0);
+                seen_max = std::max(seen_max, s0);
+                rec = std::max(rec, r0);
+                serve = std::max(serve, r0 > s0 ? r0 - s0 : 0);
             }
-            prof_n_++;
-            prof_serve_ += sv / hub_->ticks_per_us();
-            prof_release_ += rl / hub_->ticks_per_us();
-            prof_total_ += std::chrono::duration<double, std::micro>(
-                               std::chrono::steady_clock::now() - r.t0).count();
+            if (rec > seen) {
+                const double tu = hub_->ticks_per_us();
+                prof_n_++;
+                prof_span_ += (double)(rec - seen) / tu;
+                prof_skew_ += (double)(seen_max - seen) / tu;
+                prof_serve_ += (double)serve / tu;
+            }
         }
         return GCS_OK;
     }
 
+  public:
+    // gcs_server_stats_get: this ring's figures so far (GPU parts with
+    // GCS_SERVER_PROF only).
+    void stats(gcs_server_stats* st) const
+    {
+        std::memset(st, 0, sizeof *st);
+        st->requests = n_done_;
+        st->post_to_done_us = n_done_ ? total_us_ / n_done_ : 0.0;
+        if (!hub_->prof())
+            return;
+        st->gpu_span_us = prof_n_ ? prof_span_ / prof_n_ : 0.0;
+        st->seen_skew_us = prof_n_ ? prof_skew_ / prof_n_ : 0.0;
+        st->block_serve_us = prof_n_ ? prof_serve_ / prof_n_ : 0.0;
+        uint64_t sum[gcs::kProfWords] = {};
+        for (int b = 0; b < gcs::kServerBlocks; b++)
+            for (int k = gcs::kProfN; k < gcs::kProfWords; k++)
+                sum[k] += __atomic_load_n(&mb_->prof[b][k], __ATOMIC_RELAXED);
+        const double tu = hub_->ticks_per_us();
+        const double nreq = sum[gcs::kProfN] ? (double)sum[gcs::kProfN] : 1.0;
+        st->block_requests = sum[gcs::kProfN];
+        st->polls = sum[gcs::kProfPolls];
+        st->poll_us = sum[gcs::kProfPolls] ? sum[gcs::kProfPollRtt] / tu / sum[gcs::kProfPolls]
+                                           : 0.0;
+        st->seen_poll_us = sum[gcs::kProfSeenRtt] / tu / nreq;
+        st->acquire_us = sum[gcs::kProfAcq] / tu / nreq;
+        st->frames_us = sum[gcs::kProfFrames] / tu / nreq;
+        st->records_us = sum[gcs::kProfRecs] / tu / nreq;
+        st->release_us = sum[gcs::kProfRel] / tu / nreq;
+        st->cold_frac = sum[gcs::kProfCold] / nreq;
+    }
+
+  private:
+
     ServerHub* hub_ = nullptr;
     int r_ = -1;                          // ring index in the hub
     gcs::ServerMailbox* mb_ = nullptr;    // this ring (host view)
+    gcs::ServerReq* rq_ = nullptr;        // its request lines (host view)
+    bool dev_ = false;                    // ... in device memory, over the BAR
     uint32_t posted_ = 0;                 // last request posted
     uint32_t done_ = 0;                   // last request completed (all before it too)
     Req req_[gcs::kServerSlots] = {};
-    uint64_t prof_n_ = 0;
-    double prof_total_ = 0, prof_serve_ = 0, prof_release_ = 0, prof_write_ = 0;
+    uint64_t n_done_ = 0, prof_n_ = 0;
+    double total_us_ = 0, prof_span_ = 0, prof_skew_ = 0, prof_serve_ = 0, prof_write_ = 0;
 };
 
 }  // namespace
@@ -1024,7 +1167,7 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
             if (ctx->server && n <= (uint32_t)gcs::kServerMaxFrames) {
                 int rc = ctx->server->serve(reg.dev, reg.bytes & ~15ull, s.h_off, s.h_len, n,
                                             compute, 0u, s.h_code, compute ? s.h_csum : nullptr,
-                                            /*in_place=*/compute);
+                                            /*in_place=*/compute, /*dev_frames=*/false);
                 if (rc) return rc;
             } else {
                 if (ctx->server) {
@@ -1147,7 +1290,8 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
             // resident grid: no launch, no event; results complete on return
             int rc = ctx->server->serve(frames_d, (used + 15) / 16 * 16, s.h_off, s.h_len, cnt,
                                         compute, compute ? GCS_CF_NO_INPLACE : 0u, s.h_code,
-                                        compute ? s.h_csum : nullptr);
+                                        compute ? s.h_csum : nullptr, false,
+                                        /*dev_frames=*/gdst != s.h_frames);
             if (rc) return rc;
             s.busy = true;
             s.served = true;
@@ -1571,6 +1715,14 @@ try {
     return GCS_OK;
 } GCS_CATCH
 
+int gcs_server_stats_get(gcs_ctx* ctx, gcs_server_stats* out)
+try {
+    if (!ctx || !out || !ctx->server)
+        return GCS_EINVAL;
+    ctx->server->stats(out);
+    return GCS_OK;
+} GCS_CATCH
+
 int gcs_ctx_set_rss(gcs_ctx* ctx, const uint8_t* key, uint32_t key_len, uint32_t num_queues,
                     int endian_check)
 try {
@@ -1689,7 +1841,17 @@ void async_finish(gcs_ctx::AsyncReq& a)
     a.pending = false;
 }
 
-int async_wait(gcs_ctx* ctx, uint32_t q)
+// The kind of async request q (1: fill, 0: verify), or -1 when its slot no
+// longer holds it.
+int ticket_kind(const gcs_ctx* ctx, uint32_t q)
+{
+    const gcs_ctx::AsyncReq& a = ctx->areq[q % gcs::kServerSlots];
+    return a.q == q ? (a.compute ? 1 : 0) : -1;
+}
+
+// report = false: a post draining its slot's previous request, which leaves
+// the loss of cancelled requests to their own waiters.
+int async_wait(gcs_ctx* ctx, uint32_t q, bool report = true)
 {
     DeviceGuard g(ctx->device);
     if (ctx->server) {
@@ -1697,30 +1859,45 @@ int async_wait(gcs_ctx* ctx, uint32_t q)
         int rc = ctx->faults && fault("wait") ? hip_fail(hipErrorLaunchFailure, "injected (wait)")
                                : ctx->server->wait(q);
         if (rc) {
-            // The server did not answer: cancel every pending async fill, so
-            // that no later wait writes an old request's checks into buffers
-            // the caller has since reused (the caller treats the frames as
-            // unfilled; the library forgets their addresses here).  The
-            // staging slot itself is reused only after its server request
-            // completes (BurstServer::post waits for it first).
-            for (auto& a : ctx->areq)
+            // The server did not answer: cancel every pending async request,
+            // so that no later wait writes an old request's checks into
+            // buffers the caller has since reused (the caller treats the
+            // frames as unfilled / unverified; the library forgets their
+            // addresses here).  The staging slot itself is reused only after
+            // its server request completes (BurstServer::post waits for it
+            // first).  This failure is the report for every cancelled request
+            // of the waiter's kind (the plugin drops the rest of a burst when
+            // one of its waits fails); one of the other kind is reported
+            // once, to the first later wait of its kind that covers it.
+            const int kind = ticket_kind(ctx, q);
+            for (auto& a : ctx->areq) {
+                const bool own = kind < 0 || kind == a.compute;
                 if (a.pending) {
                     a.pending = false;
-                    a.cancelled = true;
+                    a.cancelled = !own;
                     std::fill(a.ptrs.begin(), a.ptrs.end(), nullptr);
                     a.status = nullptr;
                     a.csums = nullptr;
+                } else if (own) {
+                    a.cancelled = false;        // reported by this failure
                 }
+            }
             return rc;
         }
     }
-    // A request a failed wait cancelled stays "lost" for every later wait
-    // covering it until its slot is reused: fills and verifies share the ring,
-    // so each of their waiters learns that a request it may own was dropped.
+    // A request a failed wait cancelled is "lost" for the first later wait
+    // that covers it and waits for a request of the same kind (fills and
+    // verifies share the ring; the plugin's TX and RX paths each wait for
+    // their own tickets): it is reported once and forgotten, so requests
+    // posted after the failure that the server completed are never reported.
+    const int kind = ticket_kind(ctx, q);
     bool lost = false;
     for (auto& a : ctx->areq) {
-        if (a.cancelled && (int32_t)(q - a.q) >= 0)
+        if (report && a.cancelled && (int32_t)(q - a.q) >= 0 &&
+            (kind < 0 || kind == a.compute)) {
             lost = true;
+            a.cancelled = false;
+        }
         if (a.pending && (int32_t)(q - a.q) >= 0)
             async_finish(a);
     }
@@ -1773,7 +1950,7 @@ int post_async(gcs_ctx* ctx, uint8_t* const* pkts, const uint16_t* len, uint32_t
     const uint32_t q = gcs::server_next(ctx->server->posted());
     gcs_ctx::AsyncReq& a = ctx->areq[q % gcs::kServerSlots];
     if (a.pending) {                     // the slot's previous async request: finish it first
-        int rc = async_wait(ctx, a.q);
+        int rc = async_wait(ctx, a.q, /*report=*/false);
         if (rc) return rc;
     }
     a.cancelled = false;                 // nobody waited for that one: the slot is reused
@@ -1849,7 +2026,8 @@ int post_async(gcs_ctx* ctx, uint8_t* const* pkts, const uint16_t* len, uint32_t
     uint32_t got = 0;
     int rc = ctx->server->post(frames_d, bytes, a.off.data(), a.dlen.data(), n, compute,
                                compute ? (uint32_t)GCS_CF_NO_INPLACE : 0u, a.st.data(),
-                               compute ? a.cs.data() : nullptr, /*in_place=*/false, &got);
+                               compute ? a.cs.data() : nullptr, /*in_place=*/false,
+                               /*dev_frames=*/a.staged && a.stage_dev, &got);
     if (rc) return rc;
     a.q = got;
     a.pending = true;

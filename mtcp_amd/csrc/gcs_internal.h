@@ -77,28 +77,55 @@ struct alignas(64) ServerLine {
     uint32_t v;
     uint32_t pad[15];
 };
-struct alignas(64) ServerSlot {
-    ServerReqA a;                        // host
-    ServerReqB b;                        // host
+// A request slot's lines: written by the host, read by the grid.  They live
+// in HubReqs, which is pinned host memory (the grid polls it over PCIe) or,
+// with GCS_SERVER_MAILBOX=device, uncached device memory the host writes over
+// the BAR (the grid polls HBM: no PCIe read per poll).
+struct alignas(64) ServerReq {
+    ServerReqA a;
+    ServerReqB b;
     uint8_t pad0[32];
-    ServerDesc desc[kSlotFrames];        // host
-    // device: one record per frame, written in ONE 8 B store once the frame
-    // is done: csum (ip | tcp << 16) | code << 32 | (seq & 0xFFFF) << 48.  The
-    // host sees a request's results complete when every record carries its
-    // seq -- without waiting for the blocks' release fence and ack.
+    ServerDesc desc[kSlotFrames];
+};
+// A request slot's results (pinned host memory): one record per frame, written
+// in ONE 8 B store once the frame is done: csum (ip | tcp << 16) | code << 32
+// | (seq & 0xFFFF) << 48.  The host sees a request's results complete when
+// every record carries its seq -- without waiting for the blocks' release
+// fence and ack.
+struct alignas(64) ServerRes {
     uint64_t rec[kSlotFrames];
 };
-// One context's request ring.
+// GCS_SERVER_PROF (the k_burst_server<PROF> instantiation): per block, the
+// marks of the last request it served frames of (GPU wall clock, 100 MHz),
+// tagged with its number (written last), and running sums over its requests.
+enum ServerProf {
+    kProfSeen = 0,      // the poll that saw the request returned
+    kProfRec = 1,       // its records were stored (acknowledged)
+    kProfTag = 4,       // request number of the marks above
+    kProfN = 8,         // requests with frames in this block
+    kProfSeenRtt = 9,   // sum: issue -> return of the poll that saw a request
+    kProfAcq = 10,      // sum: the acquire after the poll
+    kProfFrames = 11,   // sum: frame loads, folds, record stores issued
+    kProfRecs = 12,     // sum: the record stores' acknowledgement
+    kProfPolls = 13,    // sum: polls (all)
+    kProfPollRtt = 14,  // sum: issue -> return, all polls
+    kProfRel = 15,      // sum: release fence + ack (requests that wrote frames)
+    kProfCold = 16,     // sum: requests the block was cold for when they came
+    kProfWords = 24
+};
+// One context's ring (pinned host memory).
 struct ServerMailbox {
     ServerLine ack[kServerBlocks];       // device: the last request each block served frames of
     ServerLine state[kServerBlocks];     // device: 1 serving, 2 exited (this launch's group)
-    uint64_t prof[kServerBlocks][8];     // device, GCS_SERVER_PROF: wall-clock marks of
-                                         // the block's last request (seen, served, released)
-    ServerSlot slot[kServerSlots];
+    uint64_t prof[kServerBlocks][kProfWords];   // device, GCS_SERVER_PROF (ServerProf)
+    ServerRes res[kServerSlots];
 };
 struct HubMailbox {
     ServerLine cmd;                      // host: 1 = leave now (the group leaders poll it)
     ServerMailbox ring[kHubRings];
+};
+struct HubReqs {
+    ServerReq req[kHubRings][kServerSlots];
 };
 
 // Device memory.  ent[r][q % kServerSlots] = q << 32 | n for each request q
@@ -147,9 +174,22 @@ __host__ __device__ inline int server_block(uint32_t q, uint32_t i)
 // for 3 x the gap between its last two requests when that is <= hot_max_ticks
 // (a thread bursting every 50 us keeps its ring hot; one bursting every 200 us
 // does not).
-hipError_t launch_burst_server(HubMailbox* mb, HubPub* pub, int groups, uint64_t idle_ticks,
+hipError_t launch_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, int groups,
+                               uint64_t idle_ticks,
                                uint64_t life_ticks, uint64_t hot_ticks, uint64_t hot_max_ticks,
-                               uint32_t max_polls, uint32_t naps, bool prof, hipStream_t s);
+                               uint32_t max_polls, uint32_t naps, uint32_t opts, bool prof,
+                               hipStream_t s);
+// launch_burst_server opts, the acquire after a poll (A/B knobs,
+// GCS_SERVER_ACQUIRE): by default a request whose frames are in device
+// memory (ServerReqA::mode bit kModeDevFrames: device staging, which the
+// host writes over the BAR and the XCD L2s keep coherent) takes an
+// agent-scope acquire (the CU's L1 only), one whose frames are in host memory
+// a system-scope one (which also invalidates the L2's non-coherent lines: a
+// registered mbuf pool).  kServerAcqAgent: agent scope always; kServerAcqNone:
+// no acquire for device frames.
+constexpr uint32_t kServerAcqAgent = 1u;
+constexpr uint32_t kServerAcqNone = 2u;
+constexpr uint32_t kModeDevFrames = 1u << 31;
 
 hipError_t launch_verify_fixed(uint8_t* frames, uint64_t stride, uint32_t frame_len, uint32_t n,
                                uint8_t* verdict, uint32_t flags, hipStream_t s);

@@ -230,10 +230,19 @@ k_desc(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __re
 // always drains.  All decisions are taken by wave 0 from the poll's lines
 // and broadcast through LDS (block-uniform control flow: no wave leaves the
 // loop while another waits at a barrier).
+// GCS_SERVER_PROF: the wall clock once every vector-memory access of this
+// wave issued so far has completed (loads returned, stores acknowledged).
+__device__ __forceinline__ uint64_t clock_after_vmem()
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return __builtin_amdgcn_s_memrealtime();
+}
+
 template <int G, int U, bool PROF>
 __global__ void __launch_bounds__(kBlock)
-k_burst_server(HubMailbox* mb, HubPub* pub, uint64_t idle_ticks, uint64_t life_ticks,
-               uint64_t hot_ticks, uint64_t hot_max_ticks, uint32_t max_polls, uint32_t naps)
+k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, uint64_t life_ticks,
+               uint64_t hot_ticks, uint64_t hot_max_ticks, uint32_t max_polls, uint32_t naps,
+               uint32_t opts)
 {
     enum { IDLE = 0, WORK = 1, EXIT = 2, SKIP = 3 };
     constexpr int FPB = kBlock / G;
@@ -251,20 +260,39 @@ k_burst_server(HubMailbox* mb, HubPub* pub, uint64_t idle_ticks, uint64_t life_t
     const int r = (int)(pub->ring_of[blockIdx.x / kServerBlocks] % kHubRings);
     const bool leader = blk == 0;
     ServerMailbox* rm = &mb->ring[r];
+    ServerReq* rr = rq->req[r];
     uint32_t last = pub->prog[r][blk], polls = 0;
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     uint64_t t_last = t_start;               // this block's last request (hot window, idle exit)
     // adaptive hot window: 3 x the gap between this block's last two
     // requests when that is <= hot_max_ticks, at least hot_ticks
     uint64_t win = hot_ticks, t_claim = t_start;
+    // GCS_SERVER_PROF (thread 0): this launch's additions to the block's sums
+    uint64_t p_issue = 0, p_seen = 0, p_rtt = 0, p_sum[kProfWords - kProfN] = {};
+    uint64_t p_polls0 = 0, p_rtt0 = 0;
+    bool p_cold = false;                     // a cold poll since the last request
+    // ack[blk] must stay within 2^31 of the ring's requests (the host reads
+    // it as a 32-bit serial number): a block acks each request that wrote
+    // frames in place, and otherwise refreshes it at the start and every 2^30
+    // requests.  Acking q without a fence is sound: every earlier in-place
+    // request was acked behind its own release (a previous grid's ended with
+    // its kernel), and q itself wrote nothing.
+    uint32_t acked = last;
     if (t == 0) {
         s_claim = IDLE;
+        if (PROF)                            // the sums go on from the block's last launch
+            for (int k = 0; k < kProfWords - kProfN; k++)
+                p_sum[k] = __hip_atomic_load(&rm->prof[blk][kProfN + k], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&rm->ack[blk].v, last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&rm->state[blk].v, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    p_polls0 = p_sum[kProfPolls - kProfN];
+    p_rtt0 = p_sum[kProfPollRtt - kProfN];
     __syncthreads();
     for (;;) {
         const uint32_t q = server_next(last);            // the request this block serves next
-        ServerSlot* sl = &rm->slot[q % kServerSlots];
+        ServerReq* sl = &rr[q % kServerSlots];
         const uint32_t first = (uint32_t)FPB * ((blk + kServerBlocks - server_rot(q)) %
                                                 kServerBlocks);   // this block's first frame of q
         if (wave == 0) {
@@ -288,7 +316,7 @@ k_burst_server(HubMailbox* mb, HubPub* pub, uint64_t idle_ticks, uint64_t life_t
                         qk = server_next(qk);
                 const volatile u32x4* src = nullptr;
                 if (ahead)
-                    src = reinterpret_cast<const volatile u32x4*>(&rm->slot[qk % kServerSlots].a);
+                    src = reinterpret_cast<const volatile u32x4*>(&rr[qk % kServerSlots].a);
                 else if ((hot && lane < kLanes) || (leader && lane == 0))
                     src = lane == 0   ? reinterpret_cast<const volatile u32x4*>(&sl->a)
                           : lane == 1 ? reinterpret_cast<const volatile u32x4*>(&sl->b)
@@ -302,6 +330,13 @@ k_burst_server(HubMailbox* mb, HubPub* pub, uint64_t idle_ticks, uint64_t life_t
                 u32x4 v = {0, 0, 0, 0};
                 if (src)
                     v = *src;
+                if (PROF) {
+                    const uint64_t back = clock_after_vmem();
+                    p_issue = now;
+                    p_seen = back;
+                    p_rtt += back - now;
+                    p_cold |= !hot;
+                }
                 // line A's (seq, n), or the leader's entry's (q, n)
                 uint32_t dq = v.x, dn = v.z;
                 if (follow) {
@@ -395,15 +430,22 @@ k_burst_server(HubMailbox* mb, HubPub* pub, uint64_t idle_ticks, uint64_t life_t
                                __HIP_MEMORY_SCOPE_AGENT);
         }
         bool mine = false;
-        uint64_t t_seen = 0, t_served = 0;
+        uint64_t t_acq = 0, t_frames = 0, t_rec = 0;
         bool writes = false;
         if (act == WORK) {
             // a request: its lines were written before its seq (fence-acquire
             // after observing it: later loads see everything the host wrote)
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-            t_seen = __builtin_amdgcn_s_memrealtime();
             const uint4 a = s_line[0], b = s_line[1];
-            const uint32_t n = a.z, compute = a.w & 1u, flags = a.w >> 1;
+            const bool dev = (a.w & kModeDevFrames) != 0;   // block-uniform
+            if (dev && (opts & kServerAcqNone))
+                ;
+            else if (dev || (opts & kServerAcqAgent))
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            else
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            if (PROF)
+                t_acq = clock_after_vmem();
+            const uint32_t n = a.z, compute = a.w & 1u, flags = (a.w & ~kModeDevFrames) >> 1;
             // frames written in place: a fill's check fields, or a verify's
             // tcp_in.c:1237 side effect
             writes = compute ? !(flags & GCS_CF_NO_INPLACE)
@@ -411,9 +453,14 @@ k_burst_server(HubMailbox* mb, HubPub* pub, uint64_t idle_ticks, uint64_t life_t
             uint8_t* frames = reinterpret_cast<uint8_t*>((uint64_t)b.x | ((uint64_t)b.y << 32));
             const uint64_t bytes = (uint64_t)b.z * 16;
             const uint4 d0 = s_line[2 + grp];
+            uint64_t* rec = rm->res[q % kServerSlots].rec;
             mine = first < n;                            // block-uniform: frames of q here
             for (uint32_t i = first + grp, pass = 0; i < n; i += kPass, pass++) {
-                const uint4 d = pass == 0 ? d0 : *reinterpret_cast<const uint4*>(&sl->desc[i]);
+                uint4 d = d0;
+                if (pass != 0) {
+                    const u32x4 w = *reinterpret_cast<const volatile u32x4*>(&sl->desc[i]);
+                    d = make_uint4(w.x, w.y, w.z, w.w);
+                }
                 const uint64_t o = (uint64_t)d.x | ((uint64_t)d.y << 32);
                 const u32 len = d.z & 0xFFFFu;
                 const bool ok = (o & 15) == 0 && o <= bytes && len <= bytes - o;
@@ -429,13 +476,15 @@ k_burst_server(HubMailbox* mb, HubPub* pub, uint64_t idle_ticks, uint64_t life_t
                 if (sub == 0) {                  // the group's results, in one 8 B store
                     const uint64_t rv = (uint64_t)s_csum[grp] | ((uint64_t)s_code[grp] << 32) |
                                         ((uint64_t)(q & 0xFFFFu) << 48);
-                    __hip_atomic_store(&sl->rec[i], rv, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(&rec[i], rv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 }
             }
             if (PROF && mine) {
                 __syncthreads();
-                t_served = __builtin_amdgcn_s_memrealtime();
+                t_frames = __builtin_amdgcn_s_memrealtime();
+                (void)clock_after_vmem();        // every wave's record stores acknowledged
+                __syncthreads();
+                t_rec = __builtin_amdgcn_s_memrealtime();
             }
             // frames written in place reach host memory before the ack; the
             // records are system-scope stores of their own, so a request that
@@ -446,20 +495,41 @@ k_burst_server(HubMailbox* mb, HubPub* pub, uint64_t idle_ticks, uint64_t life_t
         }
         __syncthreads();                     // every wave done with s_line / s_claim
         if (t == 0) {
-            if (PROF && mine) {
-                rm->prof[blk][0] = t_seen;
-                rm->prof[blk][1] = t_served;
-                rm->prof[blk][2] = __builtin_amdgcn_s_memrealtime();
-                rm->prof[blk][3] = polls;
-            }
-            if (mine && writes)
+            if (mine && writes) {
                 __hip_atomic_store(&rm->ack[blk].v, q, __ATOMIC_RELEASE,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
+                acked = q;
+            } else if (qend - acked >= (1u << 30)) {
+                __hip_atomic_store(&rm->ack[blk].v, qend, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+                acked = qend;
+            }
+            if (PROF && mine) {
+                const uint64_t t_rel = clock_after_vmem();
+                p_sum[kProfN - kProfN] += 1;
+                p_sum[kProfSeenRtt - kProfN] += p_seen - p_issue;
+                p_sum[kProfAcq - kProfN] += t_acq - p_seen;
+                p_sum[kProfFrames - kProfN] += t_frames - t_acq;
+                p_sum[kProfRecs - kProfN] += t_rec - t_frames;
+                p_sum[kProfRel - kProfN] += writes ? t_rel - t_rec : 0;
+                p_sum[kProfPolls - kProfN] = p_polls0 + polls;
+                p_sum[kProfPollRtt - kProfN] = p_rtt0 + p_rtt;
+                p_sum[kProfCold - kProfN] += p_cold ? 1 : 0;
+                uint64_t* pr = rm->prof[blk];
+                pr[kProfSeen] = p_seen;
+                pr[kProfRec] = t_rec;
+                for (int k = 0; k < kProfWords - kProfN; k++)
+                    pr[kProfN + k] = p_sum[k];
+                __hip_atomic_store(&pr[kProfTag], (uint64_t)q, __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            }
             __hip_atomic_store(&pub->prog[r][blk], qend, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
             s_claim = IDLE;
         }
         last = qend;
+        if (PROF && act == WORK)
+            p_cold = false;
         t_last = __builtin_amdgcn_s_memrealtime();
         if (act == WORK && hot_ticks != ~0ull) {
             const uint64_t gap = t_last - t_claim;
@@ -478,19 +548,22 @@ k_burst_server(HubMailbox* mb, HubPub* pub, uint64_t idle_ticks, uint64_t life_t
         __hip_atomic_store(&rm->state[blk].v, 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-hipError_t launch_burst_server(HubMailbox* mb, HubPub* pub, int groups, uint64_t idle_ticks,
-                               uint64_t life_ticks, uint64_t hot_ticks, uint64_t hot_max_ticks,
-                               uint32_t max_polls, uint32_t naps, bool prof, hipStream_t s)
+hipError_t launch_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, int groups,
+                               uint64_t idle_ticks, uint64_t life_ticks, uint64_t hot_ticks,
+                               uint64_t hot_max_ticks, uint32_t max_polls, uint32_t naps,
+                               uint32_t opts, bool prof, hipStream_t s)
 {
     if (groups < 1 || groups > kHubRings)
         return hipErrorInvalidValue;
     const dim3 grid(kServerBlocks * groups);
     if (prof)
-        hipLaunchKernelGGL((k_burst_server<32, 3, true>), grid, dim3(kBlock), 0, s, mb, pub,
-                           idle_ticks, life_ticks, hot_ticks, hot_max_ticks, max_polls, naps);
+        hipLaunchKernelGGL((k_burst_server<32, 3, true>), grid, dim3(kBlock), 0, s, mb, rq, pub,
+                           idle_ticks, life_ticks, hot_ticks, hot_max_ticks, max_polls, naps,
+                           opts);
     else
-        hipLaunchKernelGGL((k_burst_server<32, 3, false>), grid, dim3(kBlock), 0, s, mb, pub,
-                           idle_ticks, life_ticks, hot_ticks, hot_max_ticks, max_polls, naps);
+        hipLaunchKernelGGL((k_burst_server<32, 3, false>), grid, dim3(kBlock), 0, s, mb, rq, pub,
+                           idle_ticks, life_ticks, hot_ticks, hot_max_ticks, max_polls, naps,
+                           opts);
     return hipGetLastError();
 }
 

@@ -20,11 +20,75 @@
 #define BURST 64
 
 struct job {
-	int id, iters, server;
+	int id, iters, server, rings;
 	uint64_t mismatches, frames;
 	int rc;
 	double us, cpu_us;
+	gcs_server_stats sst;     /* summed over the thread's rings (means weighted below) */
 };
+
+/* Server figures of the last mt_bursts / mt_rings call, over every ring:
+ * out[0] requests, [1] post->done us, [2] GPU span us, [3] poll us, [4] seen
+ * poll us, [5] acquire us, [6] frames us, [7] records us, [8] release us,
+ * [9] polls per block request, [10] seen skew us, [11] slowest block us,
+ * [12] cold fraction. */
+static double g_sst[13];
+int mt_last_server_stats(double *out, int n)
+{
+	int k;
+	for (k = 0; k < n && k < 13; k++)
+		out[k] = g_sst[k];
+	return 0;
+}
+
+static void sst_add(gcs_server_stats *acc, const gcs_server_stats *s)
+{
+	/* weights: requests for the host figures, block requests for the rest */
+	double w0 = (double)acc->requests, w1 = (double)s->requests;
+	double b0 = (double)acc->block_requests, b1 = (double)s->block_requests;
+	double p0 = (double)acc->polls, p1 = (double)s->polls;
+	if (w0 + w1 > 0) {
+		acc->post_to_done_us = (acc->post_to_done_us * w0 + s->post_to_done_us * w1) / (w0 + w1);
+		acc->gpu_span_us = (acc->gpu_span_us * w0 + s->gpu_span_us * w1) / (w0 + w1);
+		acc->seen_skew_us = (acc->seen_skew_us * w0 + s->seen_skew_us * w1) / (w0 + w1);
+		acc->block_serve_us = (acc->block_serve_us * w0 + s->block_serve_us * w1) / (w0 + w1);
+	}
+	if (b0 + b1 > 0) {
+		acc->seen_poll_us = (acc->seen_poll_us * b0 + s->seen_poll_us * b1) / (b0 + b1);
+		acc->acquire_us = (acc->acquire_us * b0 + s->acquire_us * b1) / (b0 + b1);
+		acc->frames_us = (acc->frames_us * b0 + s->frames_us * b1) / (b0 + b1);
+		acc->records_us = (acc->records_us * b0 + s->records_us * b1) / (b0 + b1);
+		acc->release_us = (acc->release_us * b0 + s->release_us * b1) / (b0 + b1);
+		acc->cold_frac = (acc->cold_frac * b0 + s->cold_frac * b1) / (b0 + b1);
+	}
+	if (p0 + p1 > 0)
+		acc->poll_us = (acc->poll_us * p0 + s->poll_us * p1) / (p0 + p1);
+	acc->requests += s->requests;
+	acc->block_requests += s->block_requests;
+	acc->polls += s->polls;
+}
+
+static void sst_publish(struct job *jobs, int threads)
+{
+	gcs_server_stats acc;
+	int t;
+	memset(&acc, 0, sizeof acc);
+	for (t = 0; t < threads; t++)
+		sst_add(&acc, &jobs[t].sst);
+	g_sst[0] = (double)acc.requests;
+	g_sst[1] = acc.post_to_done_us;
+	g_sst[2] = acc.gpu_span_us;
+	g_sst[3] = acc.poll_us;
+	g_sst[4] = acc.seen_poll_us;
+	g_sst[5] = acc.acquire_us;
+	g_sst[6] = acc.frames_us;
+	g_sst[7] = acc.records_us;
+	g_sst[8] = acc.release_us;
+	g_sst[9] = acc.block_requests ? (double)acc.polls / (double)acc.block_requests : 0.0;
+	g_sst[10] = acc.seen_skew_us;
+	g_sst[11] = acc.block_serve_us;
+	g_sst[12] = acc.cold_frac;
+}
 
 /* Thread CPU time inside the gcs calls over wall time inside them, averaged
  * over the threads of the last mt_bursts call: below 1 when threads were
@@ -136,6 +200,8 @@ static void *run(void *arg)
 	}
 	j->us = in_calls / (2.0 * (it ? it : 1));     /* inside the gcs calls only */
 	j->cpu_us = in_cpu / (2.0 * (it ? it : 1));
+	if (ctx && j->server && gcs_server_stats_get(ctx, &j->sst) != 0)
+		memset(&j->sst, 0, sizeof j->sst);
 	if (ctx)
 		gcs_ctx_destroy(ctx);
 	free(rooms);
@@ -177,5 +243,130 @@ int mt_bursts(int threads, int iters, int server, uint64_t *mismatches, uint64_t
 		*us_per_call += jobs[t].us / threads;
 		g_cpu_frac += (jobs[t].us > 0 ? jobs[t].cpu_us / jobs[t].us : 1.0) / threads;
 	}
+	sst_publish(jobs, threads);
+	return rc;
+}
+
+/* One thread drives `rings` contexts (rings of the one grid) at once, as the
+ * async entry points let it: per iteration it posts a 64-frame IMIX fill on
+ * every context, waits for each, then does the same with a verify.  Runs
+ * `threads` such threads, so threads x rings rings are hot with only
+ * `threads` CPUs busy: the GPU side's scaling with rings, without the CPU
+ * oversubscription of one spinning thread per ring. */
+static void *run_rings(void *arg)
+{
+	struct job *j = arg;
+	enum { R = 8 };
+	uint8_t *rooms[R], *ref[R], *ptrs[R][BURST], st[R][BURST], vd[R][BURST];
+	uint16_t len[R][BURST];
+	uint32_t cs[R][BURST];
+	uint64_t tk[R];
+	uint64_t rng = 0xC2B2AE3D27D4EB4Full ^ (uint64_t)(j->id + 1) * 0x9E3779B97F4A7C15ull;
+	gcs_ctx *ctx[R] = {0};
+	double in_calls = 0, in_cpu = 0;
+	int it, i, k, nr = j->rings < R ? j->rings : R;
+
+	for (k = 0; k < nr; k++) {
+		rooms[k] = malloc((size_t)BURST * ROOM);
+		ref[k] = malloc((size_t)BURST * ROOM);
+		if (!j->rc)
+			j->rc = gcs_ctx_create(&ctx[k], 0, 4096, 8u << 20);
+		if (!j->rc)
+			j->rc = gcs_ctx_set_burst_server(ctx[k], 1);
+	}
+	for (it = 0; it < j->iters && !j->rc; it++) {
+		const int check = it % g_check_every == 0;
+		for (k = 0; check && k < nr; k++)
+			for (i = 0; i < BURST; i++) {
+				uint32_t u = xorshift(&rng) % 12;
+				len[k][i] = (uint16_t)(u < 7 ? 64 : u < 11 ? 576 : 1500);
+				ptrs[k][i] = rooms[k] + (size_t)i * ROOM;
+				make_frame(ptrs[k][i], len[k][i], &rng);
+				memcpy(ref[k] + (size_t)i * ROOM, ptrs[k][i], len[k][i]);
+			}
+		double c0 = cpu_us(), t0 = now_us();
+		for (k = 0; k < nr && !j->rc; k++)
+			j->rc = gcs_compute_ptrs_async(ctx[k], ptrs[k], len[k], BURST, st[k], cs[k], &tk[k]);
+		for (k = 0; k < nr && !j->rc; k++)
+			j->rc = gcs_wait(ctx[k], tk[k]);
+		in_calls += now_us() - t0;
+		in_cpu += cpu_us() - c0;
+		if (j->rc)
+			break;
+		for (k = 0; check && k < nr; k++)
+			for (i = 0; i < BURST; i++) {
+				uint32_t rc2 = 0;
+				uint8_t *r = ref[k] + (size_t)i * ROOM;
+				int rs = ref_tx_fill(r, len[k][i], &rc2);
+				if (rs != st[k][i] || rc2 != cs[k][i] || memcmp(r, ptrs[k][i], len[k][i]))
+					j->mismatches++;
+			}
+		c0 = cpu_us();
+		t0 = now_us();
+		for (k = 0; k < nr && !j->rc; k++)
+			j->rc = gcs_verify_ptrs_async(ctx[k], ptrs[k], len[k], BURST, vd[k], 0, &tk[k]);
+		for (k = 0; k < nr && !j->rc; k++)
+			j->rc = gcs_wait(ctx[k], tk[k]);
+		in_calls += now_us() - t0;
+		in_cpu += cpu_us() - c0;
+		if (j->rc)
+			break;
+		for (k = 0; check && k < nr; k++)
+			for (i = 0; i < BURST; i++)
+				if (ref_rx_verdict(ref[k] + (size_t)i * ROOM, len[k][i], 0) != vd[k][i])
+					j->mismatches++;
+		j->frames += 2 * BURST * nr;
+	}
+	/* per round (all rings' posts, then their waits) */
+	j->us = in_calls / (2.0 * (it ? it : 1));
+	j->cpu_us = in_cpu / (2.0 * (it ? it : 1));
+	memset(&j->sst, 0, sizeof j->sst);
+	for (k = 0; k < nr; k++) {
+		gcs_server_stats s1;
+		if (ctx[k] && gcs_server_stats_get(ctx[k], &s1) == 0)
+			sst_add(&j->sst, &s1);
+		if (ctx[k])
+			gcs_ctx_destroy(ctx[k]);
+		free(rooms[k]);
+		free(ref[k]);
+	}
+	return NULL;
+}
+
+/* threads x rings_per_thread rings; *us_per_round = mean time of one round
+ * (posts on all of a thread's rings + their waits). */
+int mt_rings(int threads, int rings_per_thread, int iters, uint64_t *mismatches,
+             uint64_t *frames, double *us_per_round)
+{
+	pthread_t tid[64];
+	struct job jobs[64];
+	int t, rc = 0;
+
+	if (threads < 1 || threads > 64 || rings_per_thread < 1 || rings_per_thread > 8)
+		return GCS_EINVAL;
+	g_check_every = getenv("MT_CHECK_EVERY") ? atoi(getenv("MT_CHECK_EVERY")) : 1;
+	if (g_check_every < 1)
+		g_check_every = 1;
+	for (t = 0; t < threads; t++) {
+		memset(&jobs[t], 0, sizeof(jobs[t]));
+		jobs[t].id = t;
+		jobs[t].iters = iters;
+		jobs[t].server = 1;
+		jobs[t].rings = rings_per_thread;
+		pthread_create(&tid[t], NULL, run_rings, &jobs[t]);
+	}
+	*mismatches = *frames = 0;
+	*us_per_round = 0;
+	g_cpu_frac = 0;
+	for (t = 0; t < threads; t++) {
+		pthread_join(tid[t], NULL);
+		if (jobs[t].rc && !rc)
+			rc = jobs[t].rc;
+		*mismatches += jobs[t].mismatches;
+		*frames += jobs[t].frames;
+		*us_per_round += jobs[t].us / threads;
+		g_cpu_frac += (jobs[t].us > 0 ? jobs[t].cpu_us / jobs[t].us : 1.0) / threads;
+	}
+	sst_publish(jobs, threads);
 	return rc;
 }

@@ -176,10 +176,13 @@ def test_burst_server_yields_to_large_batches(torch_dev):
         np.testing.assert_array_equal(v, O.verify_batch(buf.copy(), off, lens))
 
 
-@pytest.mark.parametrize("server,start", [(False, None), (True, None), (True, 0x80000002),
-                                          (True, 0xFFFFFFFF - 4)],
-                         ids=["direct", "server", "server_seq_2^31", "server_seq_wrap"])
-def test_registered_rooms_in_place(torch_dev, monkeypatch, server, start):
+@pytest.mark.parametrize("server,start,skew", [(False, None, None), (True, None, None),
+                                               (True, 0x80000002, None),
+                                               (True, 0xFFFFFFFF - 4, None),
+                                               (True, 0xFFFF0, 0x7FFFFFF0)],
+                         ids=["direct", "server", "server_seq_2^31", "server_seq_wrap",
+                              "server_stale_ack"])
+def test_registered_rooms_in_place(torch_dev, monkeypatch, server, start, skew):
     """Frames in one registered region (an mbuf pool) are verified and filled
     in place over PCIe -- no gather, no scatter -- with the same results; a
     frame outside the region, or misaligned, sends the batch down the staged
@@ -187,10 +190,14 @@ def test_registered_rooms_in_place(torch_dev, monkeypatch, server, start):
     blocks' acks; with the request numbers starting >= 2^31 past 0 or at the
     32-bit wrap, an ack the ring joined with at 0 would read as newer than the
     request and complete it before its release: every result must
-    still equal the oracle."""
+    still equal the oracle.  server_stale_ack joins the ring with acks 2^31 + 16
+    requests behind it (GCS_SERVER_ACK_SKEW), as after 2^31 requests that
+    wrote no frame: the grid refreshes them before it serves."""
     import ctypes as C
     if start is not None:
         monkeypatch.setenv("GCS_SERVER_SEQ_START", str(start))
+    if skew is not None:
+        monkeypatch.setenv("GCS_SERVER_ACK_SKEW", str(skew))
     L = gpucsum.lib()
     O = Oracle()
     n = 64

@@ -183,3 +183,49 @@ def test_tx_shadow_failure_withholds_frames(S, P, monkeypatch):  # noqa: F811
             np.testing.assert_array_equal(a, b)
     finally:
         c.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", ["tx", "rx"])
+def test_lost_requests_reported_once(H, P, monkeypatch, path):  # noqa: F811
+    """Every async wait fails for one 64-frame burst (fills in groups of 8,
+    verifies in groups of 16: the failed burst leaves cancelled requests in
+    up to 8 ring slots), then the fault is lifted and a SHORTER burst follows,
+    which reuses fewer slots than were cancelled.  Its waits cover the old
+    cancelled requests' numbers; they must not report them: the
+    second burst is filled / verified exactly as the software path does."""
+    monkeypatch.setenv("GPUCSUM_TX_GROUP", "8")
+    monkeypatch.setenv("GPUCSUM_RX_GROUP", "16")
+    c = Ctx(H, P, monkeypatch)
+    try:
+        if path == "tx":
+            buf, off, lens = tx_frames(200, 44)
+            monkeypatch.setenv("GCS_FAULT_INJECT", "wait")
+            tx_run(H, c.iom, c.ctx, buf, off[:64], lens[:64], 64)
+            g = c.stats()
+            assert g.tx_unfilled_sent == 64
+            monkeypatch.setenv("GCS_FAULT_INJECT", "none")
+            for k0, k1 in ((64, 84), (84, 200)):
+                sw = tx_run(H, vtab(H, "synth_module_func"), c.ctx, buf, off[k0:k1],
+                            lens[k0:k1], 64)
+                hw = tx_run(H, c.iom, c.ctx, buf, off[k0:k1], lens[k0:k1], 64)
+                for a, b in zip(hw, sw):
+                    np.testing.assert_array_equal(a, b)
+            assert c.stats().tx_unfilled_sent == 64
+        else:
+            d = load("frames_rx")
+            buf, off, lens = d["buf"], d["off"], d["len"]
+            monkeypatch.setenv("GCS_FAULT_INJECT", "wait")
+            disp, st = rx_run(H, c.iom, c.ctx, buf.copy(), off[:64], lens[:64], 64)
+            assert (disp == MINI_NULL).all()
+            g = c.stats()
+            assert g.rx_unverified == 64
+            monkeypatch.setenv("GCS_FAULT_INJECT", "none")
+            for k0, k1 in ((64, 84), (84, 300)):
+                sw_disp, sw = rx_run(H, vtab(H, "synth_module_func"), c.ctx, buf.copy(),
+                                     off[k0:k1], lens[k0:k1], 64)
+                hw_disp, hw = rx_run(H, c.iom, c.ctx, buf.copy(), off[k0:k1], lens[k0:k1], 64)
+                assert hw.rx_errors == sw.rx_errors and hw.accepted == sw.accepted
+            assert c.stats().rx_unverified == 64
+    finally:
+        c.close()
