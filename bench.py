@@ -461,6 +461,50 @@ def c3_imix(ctx, torch, n=4 << 20):
             "verify_cold_frac_peak": rx_alg / (vcold * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
+def c2_rooms(ctx, torch, n=1 << 20, L=1500, room=2048):
+    """C2's frames one per 2 KiB room (DPDK mbufs, dpdk_module.c:44-49,
+    184-193) as a device descriptor batch: RX verify and TX fill per launch
+    through the packed stream kernel (no hint: no block streams, every frame
+    on its per-frame path) and with the rooms hint (GCS_VF_ROOMS /
+    GCS_CF_ROOMS: one 32-lane group per frame, line write-back).  The fills
+    are timed over zeroed check fields (fresh, as mTCP hands frames over) and
+    as back-to-back refills."""
+    from mtcp_amd import synth
+    stream = torch.cuda.current_stream().cuda_stream
+    buf, stride = synth.fixed_frames_device(n, L, stride=room, seed=0x800F)
+    off = torch.arange(n, device="cuda", dtype=torch.int64) * room
+    ln = torch.full((n,), L, dtype=torch.int16, device="cuda")
+    hint = gpucsum_K()["GCS_VF_ROOMS"]
+    rows = buf.view(n, room)
+    v = torch.empty(n, dtype=torch.uint8, device="cuda")
+    st = torch.empty(n, dtype=torch.uint8, device="cuda")
+
+    def zero_checks():
+        rows[:, 24:26] = 0
+        rows[:, 50:52] = 0
+
+    out = {"workload": f"{n} x {L}B frames in {room} B rooms, descriptor batch, per launch"}
+    for name, fl in (("stream", 0), ("rooms", hint)):
+        ctx.compute(buf, off, ln, n, st, flags=fl, stream=stream)
+        out[f"{name}_verify_ms"] = _launch_ms(
+            torch, lambda: ctx.verify(buf, off, ln, n, v, flags=fl, stream=stream))
+        assert int((v != 0).sum()) == 0
+        out[f"{name}_compute_refill_ms"] = _launch_ms(
+            torch, lambda: ctx.compute(buf, off, ln, n, st, flags=fl, stream=stream))
+        out[f"{name}_compute_ms"] = _launch_ms_fresh(
+            torch, lambda: ctx.compute(buf, off, ln, n, st, flags=fl, stream=stream), zero_checks)
+        assert int((st != 0).sum()) == 0
+        ctx.verify(buf, off, ln, n, v, stream=stream)
+        torch.cuda.synchronize()
+        assert int((v != 0).sum()) == 0
+        out[f"{name}_verify_frac_peak"] = n * (L + 1) / (out[f"{name}_verify_ms"] * 1e-3) / 1e9 \
+            / HBM_PEAK_GBS
+        out[f"{name}_compute_frac_peak"] = n * (L + 4) / (out[f"{name}_compute_ms"] * 1e-3) \
+            / 1e9 / HBM_PEAK_GBS
+    del buf
+    return out
+
+
 def rows_8f(ctx, torch, n=1 << 20, L=1500):
     """SURVEY §8f rows 2-4 on C2-shaped data (1M x 1500 B), per launch:
     ICMP flag on TCP traffic, classify (verify + RSS), TX payload copy + fill,
@@ -891,6 +935,8 @@ def main():
             line["c2_1514B"] = c2_max_frame(ctx, torch)
             torch.cuda.empty_cache()
             line["c3_imix"] = c3_imix(ctx, torch)
+            torch.cuda.empty_cache()
+            line["c2_rooms"] = c2_rooms(ctx, torch)
             torch.cuda.empty_cache()
             line["rows_8f"] = rows_8f(ctx, torch)
             torch.cuda.empty_cache()

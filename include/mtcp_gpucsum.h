@@ -97,6 +97,13 @@ extern "C" {
                                            bytes; a message past the frame is TRUNC;
                                            tot_len < ihl*4 is BADCSUM (the reference
                                            folds nothing and gets 0xFFFF)              */
+#define GCS_VF_ROOMS              0x8u  /* descriptor batches (gcs_verify_dev): a hint that
+                                           the frames lie one per room (mbuf-shaped, e.g.
+                                           2 KiB rooms, dpdk_module.c:44-49), not packed:
+                                           each frame is verified by its own 32-lane group
+                                           (k_desc rooms kernel) instead of the packed
+                                           stream's per-frame fallback.  Same results;
+                                           ignored with GCS_VF_ICMP                         */
 
 /* ---- TX status: one byte per frame (optional output) ------------------- */
 #define GCS_TX_OK           0  /* iph->check and tcph->check written                   */
@@ -120,6 +127,10 @@ extern "C" {
                                      holding the check fields, never whole 128 B lines
                                      (the line write-back is chosen by batch size,
                                      DESIGN.md §4 "TX write-back"; a measurement knob) */
+#define GCS_CF_ROOMS        0x8u  /* gcs_compute_dev: the rooms hint of GCS_VF_ROOMS; the
+                                     fill then writes back each frame's whole first 128 B
+                                     line (its own bytes only) while the batch's lines fit
+                                     the Infinity Cache, as fixed-stride fills do       */
 
 typedef struct gcs_ctx gcs_ctx;
 
@@ -178,6 +189,13 @@ typedef struct gcs_server_stats {
                                  records stored                                       */
     double cold_frac;         /* (block, request) pairs whose block was cold (polling
                                  the leader's copy) when the request came             */
+    uint64_t slow_polls_2us;  /* polls whose round trip took over 2 us                */
+    uint64_t slow_polls_5us;  /* ... over 5 us                                        */
+    uint64_t torn_polls;      /* polls that saw a request's line A before all its
+                                 other lines had landed                               */
+    double max_poll_us;       /* the longest poll round trip                          */
+    double late_us[8];        /* mean per request: how long after the first serving
+                                 block each of the ring's blocks saw it (block index) */
 } gcs_server_stats;
 int gcs_server_stats_get(gcs_ctx *ctx, gcs_server_stats *out);
 

@@ -727,6 +727,8 @@ class BurstServer {
             // wait briefly for each serving block's tag; a block that has
             // already moved on to a later request is left out.
             uint64_t seen = ~0ull, seen_max = 0, rec = 0, serve = 0;
+            uint64_t seen_b[gcs::kServerBlocks] = {};
+            bool have_b[gcs::kServerBlocks] = {};
             const auto tp = std::chrono::steady_clock::now();
             for (int k = 0; k < nb; k++) {
                 const int b = gcs::server_block(r.q, (uint32_t)k * gcs::kServerFPB);
@@ -740,6 +742,8 @@ class BurstServer {
                 const uint64_t s0 = mb_->prof[b][gcs::kProfSeen], r0 = mb_->prof[b][gcs::kProfRec];
                 seen = std::min(seen, s0);
                 seen_max = std::max(seen_max, s0);
+                seen_b[b] = s0;
+                have_b[b] = true;
                 rec = std::max(rec, r0);
                 serve = std::max(serve, r0 > s0 ? r0 - s0 : 0);
             }
@@ -749,6 +753,11 @@ class BurstServer {
                 prof_span_ += (double)(rec - seen) / tu;
                 prof_skew_ += (double)(seen_max - seen) / tu;
                 prof_serve_ += (double)serve / tu;
+                for (int b = 0; b < gcs::kServerBlocks; b++)
+                    if (have_b[b]) {
+                        late_[b] += (double)(seen_b[b] - seen) / tu;
+                        late_n_[b]++;
+                    }
             }
         }
         return GCS_OK;
@@ -783,6 +792,16 @@ class BurstServer {
         st->records_us = sum[gcs::kProfRecs] / tu / nreq;
         st->release_us = sum[gcs::kProfRel] / tu / nreq;
         st->cold_frac = sum[gcs::kProfCold] / nreq;
+        st->slow_polls_2us = sum[gcs::kProfSlow2];
+        st->slow_polls_5us = sum[gcs::kProfSlow5];
+        st->torn_polls = sum[gcs::kProfTorn];
+        uint64_t mx = 0;
+        for (int b = 0; b < gcs::kServerBlocks; b++)
+            mx = std::max<uint64_t>(mx, __atomic_load_n(&mb_->prof[b][gcs::kProfMaxRtt],
+                                                        __ATOMIC_RELAXED));
+        st->max_poll_us = mx / tu;
+        for (int b = 0; b < gcs::kServerBlocks; b++)
+            st->late_us[b] = late_n_[b] ? late_[b] / late_n_[b] : 0.0;
     }
 
   private:
@@ -797,6 +816,8 @@ class BurstServer {
     Req req_[gcs::kServerSlots] = {};
     uint64_t n_done_ = 0, prof_n_ = 0;
     double total_us_ = 0, prof_span_ = 0, prof_skew_ = 0, prof_serve_ = 0, prof_write_ = 0;
+    double late_[gcs::kServerBlocks] = {};
+    uint64_t late_n_[gcs::kServerBlocks] = {};
 };
 
 }  // namespace

@@ -111,6 +111,10 @@ enum ServerProf {
     kProfPollRtt = 14,  // sum: issue -> return, all polls
     kProfRel = 15,      // sum: release fence + ack (requests that wrote frames)
     kProfCold = 16,     // sum: requests the block was cold for when they came
+    kProfSlow2 = 17,    // polls whose round trip took over 2 us
+    kProfSlow5 = 18,    // ... over 5 us
+    kProfMaxRtt = 19,   // the longest poll round trip (ticks)
+    kProfTorn = 20,     // polls that saw line A of the request but not all its lines
     kProfWords = 24
 };
 // One context's ring (pinned host memory).

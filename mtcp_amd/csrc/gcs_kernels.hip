@@ -192,8 +192,13 @@ k_small_x(uint8_t* __restrict__ frames, uint64_t stride, u32 frame_len, u32 n,
                                         ext);
 }
 
-// Descriptor batch: frame i at frames + off[i], length len[i].
-template <int G, int U, bool COMPUTE, bool NT, int WM>
+// Descriptor batch: frame i at frames + off[i], length len[i], one frame per
+// G-lane group (longer frames in further batches of G*U chunks).  Direct-mode
+// host batches (launch_desc_spread), and device batches with the rooms hint
+// (GCS_VF_ROOMS / GCS_CF_ROOMS: frames one per mbuf room, which the packed
+// stream cannot stream; XCD-contiguous blocks, and for a fill of lines that
+// fit the Infinity Cache the whole-line write-back of k_fixed).
+template <int G, int U, bool COMPUTE, bool NT, int WM, bool XCD = false>
 __global__ void __launch_bounds__(kBlock)
 k_desc(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __restrict__ off,
        const uint16_t* __restrict__ lens, u32 n, uint8_t* __restrict__ out_code,
@@ -201,7 +206,8 @@ k_desc(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __re
 {
     constexpr int FPB = kBlock / G;
     const int sub = threadIdx.x & (G - 1);
-    const uint64_t i = (uint64_t)blockIdx.x * FPB + threadIdx.x / G;
+    const uint32_t blk = XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint64_t i = (uint64_t)blk * FPB + threadIdx.x / G;
     if (i >= n)
         return;
     const uint64_t o = off[i];
@@ -269,7 +275,7 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
     uint64_t win = hot_ticks, t_claim = t_start;
     // GCS_SERVER_PROF (thread 0): this launch's additions to the block's sums
     uint64_t p_issue = 0, p_seen = 0, p_rtt = 0, p_sum[kProfWords - kProfN] = {};
-    uint64_t p_polls0 = 0, p_rtt0 = 0;
+    uint64_t p_polls0 = 0, p_rtt0 = 0, p_slow2 = 0, p_slow5 = 0, p_maxrtt = 0, p_torn = 0;
     bool p_cold = false;                     // a cold poll since the last request
     // ack[blk] must stay within 2^31 of the ring's requests (the host reads
     // it as a 32-bit serial number): a block acks each request that wrote
@@ -289,6 +295,10 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
     }
     p_polls0 = p_sum[kProfPolls - kProfN];
     p_rtt0 = p_sum[kProfPollRtt - kProfN];
+    p_slow2 = p_sum[kProfSlow2 - kProfN];
+    p_slow5 = p_sum[kProfSlow5 - kProfN];
+    p_maxrtt = p_sum[kProfMaxRtt - kProfN];
+    p_torn = p_sum[kProfTorn - kProfN];
     __syncthreads();
     for (;;) {
         const uint32_t q = server_next(last);            // the request this block serves next
@@ -336,6 +346,9 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
                     p_seen = back;
                     p_rtt += back - now;
                     p_cold |= !hot;
+                    p_slow2 += back - now > 200 ? 1 : 0;     // 100 MHz clock
+                    p_slow5 += back - now > 500 ? 1 : 0;
+                    p_maxrtt = back - now > p_maxrtt ? back - now : p_maxrtt;
                 }
                 // line A's (seq, n), or the leader's entry's (q, n)
                 uint32_t dq = v.x, dn = v.z;
@@ -351,6 +364,8 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
                 const bool ok = __ballot(torn) == 0;
                 uint32_t act = IDLE;
                 if (hot) {
+                    if (PROF && x0 == q && !ok)
+                        p_torn++;
                     if (x0 == q)
                         act = ok ? WORK : IDLE;  // torn poll: look again
                     else if ((int32_t)(x0 - q) > 0)
@@ -515,6 +530,10 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
                 p_sum[kProfPolls - kProfN] = p_polls0 + polls;
                 p_sum[kProfPollRtt - kProfN] = p_rtt0 + p_rtt;
                 p_sum[kProfCold - kProfN] += p_cold ? 1 : 0;
+                p_sum[kProfSlow2 - kProfN] = p_slow2;
+                p_sum[kProfSlow5 - kProfN] = p_slow5;
+                p_sum[kProfMaxRtt - kProfN] = p_maxrtt;
+                p_sum[kProfTorn - kProfN] = p_torn;
                 uint64_t* pr = rm->prof[blk];
                 pr[kProfSeen] = p_seen;
                 pr[kProfRec] = t_rec;
@@ -2436,6 +2455,24 @@ static hipError_t launch_desc(uint8_t* frames, uint64_t frames_bytes, const uint
 {
     if (n == 0)
         return hipSuccess;
+    if (!ext_on && (flags & GCS_VF_ROOMS)) {
+        // frames one per room: one 32-lane group per frame, 3 chunks per lane
+        // and batch (k_fixed<32, 3>'s shape for MTU frames)
+        static_assert(GCS_VF_ROOMS == GCS_CF_ROOMS, "one rooms bit");
+        constexpr int G = 32, U = 3, FPB = kBlock / G;
+        const dim3 rg((n + FPB - 1) / FPB);
+        if constexpr (COMPUTE) {
+            if ((uint64_t)n * 128 <= line_wb_bytes() && !(flags & GCS_CF_SECTOR_WB)) {
+                hipLaunchKernelGGL((k_desc<G, U, COMPUTE, kNT, WM_LINE_SC1, kXCD>), rg,
+                                   dim3(kBlock), 0, s, frames, frames_bytes, off, len, n, code,
+                                   csums, flags);
+                return hipGetLastError();
+            }
+        }
+        hipLaunchKernelGGL((k_desc<G, U, COMPUTE, kNT, kWM, kXCD>), rg, dim3(kBlock), 0, s,
+                           frames, frames_bytes, off, len, n, code, csums, flags);
+        return hipGetLastError();
+    }
     const dim3 grid((n + kDescFrames - 1) / kDescFrames);
     static_assert(kDescFrames == kBlock, "one descriptor per thread");
     if (ext_on) {

@@ -31,12 +31,14 @@ struct job {
  * out[0] requests, [1] post->done us, [2] GPU span us, [3] poll us, [4] seen
  * poll us, [5] acquire us, [6] frames us, [7] records us, [8] release us,
  * [9] polls per block request, [10] seen skew us, [11] slowest block us,
- * [12] cold fraction. */
-static double g_sst[13];
+ * [12] cold fraction, [13] polls over 2 us, [14] over 5 us, [15] torn polls,
+ * [16] longest poll us, [17..24] mean lateness of blocks 0..7 us. */
+#define NSST 25
+static double g_sst[NSST];
 int mt_last_server_stats(double *out, int n)
 {
 	int k;
-	for (k = 0; k < n && k < 13; k++)
+	for (k = 0; k < n && k < NSST; k++)
 		out[k] = g_sst[k];
 	return 0;
 }
@@ -52,6 +54,8 @@ static void sst_add(gcs_server_stats *acc, const gcs_server_stats *s)
 		acc->gpu_span_us = (acc->gpu_span_us * w0 + s->gpu_span_us * w1) / (w0 + w1);
 		acc->seen_skew_us = (acc->seen_skew_us * w0 + s->seen_skew_us * w1) / (w0 + w1);
 		acc->block_serve_us = (acc->block_serve_us * w0 + s->block_serve_us * w1) / (w0 + w1);
+		for (int b = 0; b < 8; b++)
+			acc->late_us[b] = (acc->late_us[b] * w0 + s->late_us[b] * w1) / (w0 + w1);
 	}
 	if (b0 + b1 > 0) {
 		acc->seen_poll_us = (acc->seen_poll_us * b0 + s->seen_poll_us * b1) / (b0 + b1);
@@ -63,6 +67,11 @@ static void sst_add(gcs_server_stats *acc, const gcs_server_stats *s)
 	}
 	if (p0 + p1 > 0)
 		acc->poll_us = (acc->poll_us * p0 + s->poll_us * p1) / (p0 + p1);
+	acc->slow_polls_2us += s->slow_polls_2us;
+	acc->slow_polls_5us += s->slow_polls_5us;
+	acc->torn_polls += s->torn_polls;
+	if (s->max_poll_us > acc->max_poll_us)
+		acc->max_poll_us = s->max_poll_us;
 	acc->requests += s->requests;
 	acc->block_requests += s->block_requests;
 	acc->polls += s->polls;
@@ -88,6 +97,12 @@ static void sst_publish(struct job *jobs, int threads)
 	g_sst[10] = acc.seen_skew_us;
 	g_sst[11] = acc.block_serve_us;
 	g_sst[12] = acc.cold_frac;
+	g_sst[13] = (double)acc.slow_polls_2us;
+	g_sst[14] = (double)acc.slow_polls_5us;
+	g_sst[15] = (double)acc.torn_polls;
+	g_sst[16] = acc.max_poll_us;
+	for (t = 0; t < 8; t++)
+		g_sst[17 + t] = acc.late_us[t];
 }
 
 /* Thread CPU time inside the gcs calls over wall time inside them, averaged

@@ -480,19 +480,24 @@ def test_desc_mtu_batch_not_serialised(torch_dev, ctx, O):
     assert min(ms) < 3.0, ms
 
 
-def test_desc_sparse_rooms_vs_oracle(torch_dev, ctx, O):
+@pytest.mark.parametrize("rooms", [False, True], ids=["stream", "rooms_hint"])
+def test_desc_sparse_rooms_vs_oracle(torch_dev, ctx, O, rooms):
     """Frames one per 2 KiB room, as mbufs hand them over (dpdk_module.c's
     rings): no block streams, so every frame takes the stream kernel's
-    per-frame path (TX 32 x 2, RX 32 x 3 at 7 waves per SIMD).  Mixed lengths
-    (empty, runts, odd, MTU), IP options, padded segments and UDP frames, TX
-    and RX (with and without the tcp_in.c:1237 side effect) bit-exact against
-    the oracle."""
+    per-frame path (TX 32 x 2, RX 32 x 3 at 7 waves per SIMD) -- or, with the
+    rooms hint (GCS_VF_ROOMS / GCS_CF_ROOMS), the 32-lane group kernel with
+    line write-back.  Mixed lengths (empty, runts, odd, MTU, jumbo past one
+    batch of 96 chunks), IP options, padded segments and UDP frames, TX and
+    RX (with and without the tcp_in.c:1237 side effect) bit-exact against the
+    oracle."""
+    hint = gpucsum.K["GCS_VF_ROOMS"] if rooms else 0
     t = torch_dev
     n, room = 256 * 5 + 33, 2048
     rng = np.random.default_rng(0x5A2E)
     lens = rng.integers(60, 1515, size=n).astype(np.uint16)
     lens[::97] = 0
     lens[5::89] = rng.integers(1, 54, size=len(lens[5::89]))
+    lens[7::211] = rng.integers(1537, 2049, size=len(lens[7::211]))   # > one batch
     off = np.arange(n, dtype=np.uint64) * room
     buf = rng.integers(0, 256, size=n * room, dtype=np.uint8)
     for i in range(n):
@@ -515,7 +520,7 @@ def test_desc_sparse_rooms_vs_oracle(torch_dev, ctx, O):
     d = dev(t, buf)
     st = t.zeros(n, dtype=t.uint8, device="cuda")
     cs = t.zeros(n, dtype=t.int32, device="cuda")
-    ctx.compute(d, doff, dlen, n, st, cs)
+    ctx.compute(d, doff, dlen, n, st, cs, flags=hint)
     ctx.sync()
     np.testing.assert_array_equal(host(st), rst)
     np.testing.assert_array_equal(host(cs).view(np.uint32), rcs)
@@ -524,7 +529,7 @@ def test_desc_sparse_rooms_vs_oracle(torch_dev, ctx, O):
     for flags in (0, 1):
         d = dev(t, ref)
         v = t.full((n,), 0xEE, dtype=t.uint8, device="cuda")
-        ctx.verify(d, doff, dlen, n, v, flags=flags)
+        ctx.verify(d, doff, dlen, n, v, flags=flags | hint)
         ctx.sync()
         exp = ref.copy()
         rv = O.verify_batch(exp, off, lens, flags=flags)
