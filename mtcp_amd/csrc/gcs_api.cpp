@@ -726,28 +726,43 @@ class BurstServer {
             // wall clock).  A block writes its marks after its records, so
             // wait briefly for each serving block's tag; a block that has
             // already moved on to a later request is left out.
-            uint64_t seen = ~0ull, seen_max = 0, rec = 0, serve = 0;
-            uint64_t seen_b[gcs::kServerBlocks] = {};
+            // (marks are the low 32 bits of the 100 MHz clock: differences
+            // within one request are taken modulo 2^32)
+            bool first = true;
+            uint32_t seen = 0, seen_max = 0, rec = 0, serve = 0;
+            uint32_t seen_b[gcs::kServerBlocks] = {};
             bool have_b[gcs::kServerBlocks] = {};
             const auto tp = std::chrono::steady_clock::now();
             for (int k = 0; k < nb; k++) {
                 const int b = gcs::server_block(r.q, (uint32_t)k * gcs::kServerFPB);
+                const __m128i* mp = reinterpret_cast<const __m128i*>(&mb_->prof[b][gcs::kProfMarks]);
+                alignas(16) uint32_t mk[4];
                 int32_t d;
-                while ((d = (int32_t)((uint32_t)__atomic_load_n(&mb_->prof[b][gcs::kProfTag],
-                                                                __ATOMIC_ACQUIRE) - r.q)) < 0 &&
-                       std::chrono::steady_clock::now() - tp < std::chrono::microseconds(200))
+                for (;;) {
+                    asm volatile("" ::: "memory");   // the grid writes it: reload
+                    _mm_store_si128(reinterpret_cast<__m128i*>(mk), _mm_load_si128(mp));
+                    d = (int32_t)(mk[2] - r.q);
+                    if (d >= 0 || std::chrono::steady_clock::now() - tp >
+                                      std::chrono::microseconds(200))
+                        break;
                     __builtin_ia32_pause();
+                }
                 if (d != 0)
                     continue;
-                const uint64_t s0 = mb_->prof[b][gcs::kProfSeen], r0 = mb_->prof[b][gcs::kProfRec];
-                seen = std::min(seen, s0);
-                seen_max = std::max(seen_max, s0);
+                const uint32_t s0 = mk[0], r0 = mk[1];
+                if (first) {
+                    seen = seen_max = s0;
+                    rec = r0;
+                    first = false;
+                }
+                if ((int32_t)(s0 - seen) < 0) seen = s0;
+                if ((int32_t)(s0 - seen_max) > 0) seen_max = s0;
+                if ((int32_t)(r0 - rec) > 0) rec = r0;
+                if ((int32_t)(r0 - s0) > (int32_t)serve) serve = r0 - s0;
                 seen_b[b] = s0;
                 have_b[b] = true;
-                rec = std::max(rec, r0);
-                serve = std::max(serve, r0 > s0 ? r0 - s0 : 0);
             }
-            if (rec > seen) {
+            if (!first && (int32_t)(rec - seen) > 0) {
                 const double tu = hub_->ticks_per_us();
                 prof_n_++;
                 prof_span_ += (double)(rec - seen) / tu;
@@ -755,7 +770,7 @@ class BurstServer {
                 prof_serve_ += (double)serve / tu;
                 for (int b = 0; b < gcs::kServerBlocks; b++)
                     if (have_b[b]) {
-                        late_[b] += (double)(seen_b[b] - seen) / tu;
+                        late_[b] += (double)(int32_t)(seen_b[b] - seen) / tu;
                         late_n_[b]++;
                     }
             }

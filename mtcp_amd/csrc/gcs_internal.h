@@ -99,9 +99,11 @@ struct alignas(64) ServerRes {
 // marks of the last request it served frames of (GPU wall clock, 100 MHz),
 // tagged with its number (written last), and running sums over its requests.
 enum ServerProf {
-    kProfSeen = 0,      // the poll that saw the request returned
-    kProfRec = 1,       // its records were stored (acknowledged)
-    kProfTag = 4,       // request number of the marks above
+    kProfMarks = 0,     // words 0-1: ONE 16 B store {seen, rec, q, 0} (u32 each):
+                        // the low 32 bits of the clock when the poll that saw
+                        // request q returned and when its records were stored
+                        // (acknowledged); one store, so no fence orders the
+                        // marks before their tag
     kProfN = 8,         // requests with frames in this block
     kProfSeenRtt = 9,   // sum: issue -> return of the poll that saw a request
     kProfAcq = 10,      // sum: the acquire after the poll

@@ -220,6 +220,104 @@ k_desc(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __re
                                                 out_csum ? out_csum + i : nullptr);
 }
 
+// Descriptor batch with the rooms hint (GCS_VF_ROOMS / GCS_CF_ROOMS: frames
+// one per mbuf room): one G-lane group per frame as k_desc, XCD-contiguous
+// blocks, K frames per group, FPB apart: the K descriptors are loaded
+// together, then all K frames' first batches, before the first is folded --
+// so a wave waits on one descriptor trip per K frames instead of one per
+// frame (k_fixed has no descriptor trip at all).
+// SEQ: the K frames' loads are not issued together; only their descriptors
+// are (fewer VGPRs: K = 2 unrolled takes 92-102, 4-5 waves per SIMD).
+template <int G, int U, bool COMPUTE, int WM, int K, bool SEQ = false>
+__global__ void __launch_bounds__(kBlock)
+k_rooms(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __restrict__ off,
+        const uint16_t* __restrict__ lens, u32 n, uint8_t* __restrict__ out_code,
+        uint32_t* __restrict__ out_csum, u32 flags)
+{
+    constexpr int FPB = kBlock / G;
+    const int sub = threadIdx.x & (G - 1);
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);
+    const uint64_t i0 = (uint64_t)blk * FPB * K + threadIdx.x / G;
+    if (i0 >= n)
+        return;                                        // whole group leaves together
+    uint64_t o[K];
+    u32 len[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint64_t i = i0 + (uint64_t)k * FPB;
+        o[k] = i < n ? off[i] : 0;
+        len[k] = i < n ? lens[i] : 0;
+    }
+    if constexpr (SEQ) {
+#pragma unroll 1
+        for (int k = 0; k < K; k++) {
+            const uint64_t i = i0 + (uint64_t)k * FPB;
+            if (i >= n)
+                break;
+            const bool ok = (o[k] & 15) == 0 && o[k] <= frames_bytes &&
+                            len[k] <= frames_bytes - o[k];
+            do_frame<G, U, COMPUTE, true, true, kNT, WM>(
+                frames + (ok ? o[k] : 0), len[k], ok ? (int64_t)(frames_bytes - o[k]) : 0, ok,
+                sub, flags, out_code ? out_code + i : nullptr, out_csum ? out_csum + i : nullptr);
+        }
+        return;
+    }
+    uint4 v[K][U];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const bool ok = (o[k] & 15) == 0 && o[k] <= frames_bytes && len[k] <= frames_bytes - o[k];
+        const int nch = ok ? (int)((len[k] + 15) >> 4) : 0;
+        load_first<G, U, true, kNT>(frames + (ok ? o[k] : 0), nch,
+                                    ok ? (int64_t)(frames_bytes - o[k]) : 0, sub, v[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint64_t i = i0 + (uint64_t)k * FPB;
+        if (i >= n)
+            break;                                     // group-uniform, and so are later k
+        const bool ok = (o[k] & 15) == 0 && o[k] <= frames_bytes && len[k] <= frames_bytes - o[k];
+        uint8_t* f = frames + (ok ? o[k] : 0);
+        frame_body<G, U, COMPUTE, true, true, kNT, WM>(
+            v[k], f, f, len[k], ok ? (int64_t)(frames_bytes - o[k]) : 0, ok, sub, flags,
+            out_code ? out_code + i : nullptr, out_csum ? out_csum + i : nullptr, true);
+    }
+}
+
+// k_rooms with the block's K * 256 / G descriptors loaded into LDS first (one
+// coalesced trip), then each group walks its K frames from LDS.
+template <int G, int U, bool COMPUTE, int WM, int K>
+__global__ void __launch_bounds__(kBlock, COMPUTE ? 7 : 8)
+k_rooms_lds(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __restrict__ off,
+            const uint16_t* __restrict__ lens, u32 n, uint8_t* __restrict__ out_code,
+            uint32_t* __restrict__ out_csum, u32 flags)
+{
+    constexpr int FPB = kBlock / G, FB = FPB * K;
+    static_assert(FB <= kBlock, "one descriptor per thread");
+    __shared__ uint64_t s_off[FB];
+    __shared__ uint16_t s_len[FB];
+    const int t = threadIdx.x, sub = t & (G - 1), g = t / G;
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);
+    const uint64_t base = (uint64_t)blk * FB;
+    if (t < FB && base + t < n) {
+        s_off[t] = off[base + t];
+        s_len[t] = lens[base + t];
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int k = 0; k < K; k++) {
+        const int l = k * FPB + g;
+        const uint64_t i = base + l;
+        if (i >= n)
+            break;                                     // group-uniform
+        const uint64_t o = s_off[l];
+        const u32 len = s_len[l];
+        const bool ok = (o & 15) == 0 && o <= frames_bytes && len <= frames_bytes - o;
+        do_frame<G, U, COMPUTE, true, true, kNT, WM>(
+            frames + (ok ? o : 0), len, ok ? (int64_t)(frames_bytes - o) : 0, ok, sub, flags,
+            out_code ? out_code + i : nullptr, out_csum ? out_csum + i : nullptr);
+    }
+}
+
 // Burst server: a grid of kServerBlocks blocks per ring in use that stays
 // resident for at most life_ticks (wall clock) and serves the host batches
 // posted in the contexts' request rings (gcs_internal.h HubMailbox) -- each
@@ -534,13 +632,15 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
                 p_sum[kProfSlow5 - kProfN] = p_slow5;
                 p_sum[kProfMaxRtt - kProfN] = p_maxrtt;
                 p_sum[kProfTorn - kProfN] = p_torn;
+                // relaxed stores only: a release here would write back the
+                // XCD's L2 per request and perturb what it measures
                 uint64_t* pr = rm->prof[blk];
-                pr[kProfSeen] = p_seen;
-                pr[kProfRec] = t_rec;
                 for (int k = 0; k < kProfWords - kProfN; k++)
-                    pr[kProfN + k] = p_sum[k];
-                __hip_atomic_store(&pr[kProfTag], (uint64_t)q, __ATOMIC_RELEASE,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(&pr[kProfN + k], p_sum[k], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+                const u32x4 mk = {(u32)p_seen, (u32)t_rec, q, 0u};
+                asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1"
+                             : : "v"(&pr[kProfMarks]), "v"(mk) : "memory");
             }
             __hip_atomic_store(&pub->prog[r][blk], qend, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
@@ -2448,6 +2548,56 @@ using StreamShip = std::conditional_t<COMPUTE, StreamShape<8, 8192, 7, 4, 32, 2>
 // passes per block region (blockIdx.y): 3 x 8,192 chunks hold 256 packed
 // frames of up to 1,536 B; what a block has beyond them goes per frame
 constexpr int kStreamPasses = 3;
+// GCS_ROOMS_K: frames per group of k_rooms (1, 2 or 4 with their loads issued
+// together; 12 / 14: 2 / 4 with only the descriptors together, SEQ; an A/B
+// knob, read once).
+static int rooms_k()
+{
+    static const int v = [] {
+        const char* e = std::getenv("GCS_ROOMS_K");
+        return e ? std::atoi(e) : 1;
+    }();
+    return v;
+}
+
+template <bool COMPUTE, int K>
+static hipError_t launch_rooms_lds(bool line, uint8_t* frames, uint64_t frames_bytes,
+                                   const uint64_t* off, const uint16_t* len, u32 n, uint8_t* code,
+                                   uint32_t* csums, u32 flags, hipStream_t s)
+{
+    constexpr int G = 32, U = 3, FB = kBlock / G * K;
+    const dim3 rg((n + FB - 1) / FB);
+    if constexpr (COMPUTE) {
+        if (line) {
+            hipLaunchKernelGGL((k_rooms_lds<G, U, COMPUTE, WM_LINE_SC1, K>), rg, dim3(kBlock), 0,
+                               s, frames, frames_bytes, off, len, n, code, csums, flags);
+            return hipGetLastError();
+        }
+    }
+    hipLaunchKernelGGL((k_rooms_lds<G, U, COMPUTE, kWM, K>), rg, dim3(kBlock), 0, s, frames,
+                       frames_bytes, off, len, n, code, csums, flags);
+    return hipGetLastError();
+}
+
+template <bool COMPUTE, int K, bool SEQ = false>
+static hipError_t launch_rooms(bool line, uint8_t* frames, uint64_t frames_bytes,
+                               const uint64_t* off, const uint16_t* len, u32 n, uint8_t* code,
+                               uint32_t* csums, u32 flags, hipStream_t s)
+{
+    constexpr int G = 32, U = 3, FPB = kBlock / G * K;
+    const dim3 rg((n + FPB - 1) / FPB);
+    if constexpr (COMPUTE) {
+        if (line) {
+            hipLaunchKernelGGL((k_rooms<G, U, COMPUTE, WM_LINE_SC1, K, SEQ>), rg, dim3(kBlock), 0,
+                               s, frames, frames_bytes, off, len, n, code, csums, flags);
+            return hipGetLastError();
+        }
+    }
+    hipLaunchKernelGGL((k_rooms<G, U, COMPUTE, kWM, K, SEQ>), rg, dim3(kBlock), 0, s, frames,
+                       frames_bytes, off, len, n, code, csums, flags);
+    return hipGetLastError();
+}
+
 template <bool COMPUTE>
 static hipError_t launch_desc(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
                               const uint16_t* len, u32 n, uint8_t* code, uint32_t* csums,
@@ -2459,19 +2609,26 @@ static hipError_t launch_desc(uint8_t* frames, uint64_t frames_bytes, const uint
         // frames one per room: one 32-lane group per frame, 3 chunks per lane
         // and batch (k_fixed<32, 3>'s shape for MTU frames)
         static_assert(GCS_VF_ROOMS == GCS_CF_ROOMS, "one rooms bit");
-        constexpr int G = 32, U = 3, FPB = kBlock / G;
-        const dim3 rg((n + FPB - 1) / FPB);
-        if constexpr (COMPUTE) {
-            if ((uint64_t)n * 128 <= line_wb_bytes() && !(flags & GCS_CF_SECTOR_WB)) {
-                hipLaunchKernelGGL((k_desc<G, U, COMPUTE, kNT, WM_LINE_SC1, kXCD>), rg,
-                                   dim3(kBlock), 0, s, frames, frames_bytes, off, len, n, code,
-                                   csums, flags);
-                return hipGetLastError();
-            }
+        const bool line = COMPUTE && (uint64_t)n * 128 <= line_wb_bytes() &&
+                          !(flags & GCS_CF_SECTOR_WB);
+        switch (rooms_k()) {
+        case 2: return launch_rooms<COMPUTE, 2>(line, frames, frames_bytes, off, len, n, code,
+                                                csums, flags, s);
+        case 4: return launch_rooms<COMPUTE, 4>(line, frames, frames_bytes, off, len, n, code,
+                                                csums, flags, s);
+        case 12: return launch_rooms<COMPUTE, 2, true>(line, frames, frames_bytes, off, len, n,
+                                                       code, csums, flags, s);
+        case 14: return launch_rooms<COMPUTE, 4, true>(line, frames, frames_bytes, off, len, n,
+                                                       code, csums, flags, s);
+        case 34: return launch_rooms_lds<COMPUTE, 4>(line, frames, frames_bytes, off, len, n,
+                                                     code, csums, flags, s);
+        case 316: return launch_rooms_lds<COMPUTE, 16>(line, frames, frames_bytes, off, len, n,
+                                                       code, csums, flags, s);
+        case 332: return launch_rooms_lds<COMPUTE, 32>(line, frames, frames_bytes, off, len, n,
+                                                       code, csums, flags, s);
+        default: return launch_rooms<COMPUTE, 1>(line, frames, frames_bytes, off, len, n, code,
+                                                 csums, flags, s);
         }
-        hipLaunchKernelGGL((k_desc<G, U, COMPUTE, kNT, kWM, kXCD>), rg, dim3(kBlock), 0, s,
-                           frames, frames_bytes, off, len, n, code, csums, flags);
-        return hipGetLastError();
     }
     const dim3 grid((n + kDescFrames - 1) / kDescFrames);
     static_assert(kDescFrames == kBlock, "one descriptor per thread");

@@ -11,7 +11,9 @@ WRITE_SIZE / duration per configuration -- per kernel AND per launch size,
 which bench.py then looks up for its roofline.traffic.
 
 Labels: <op>_<layout>_<frame_len|imix>_<frames per launch>, e.g.
-compute_fixed_1500_4194304 is the TX fill of a C4 shard.
+compute_fixed_1500_4194304 is the TX fill of a C4 shard; step_* are the two
+launches of the bench step (fill of one batch, then verify of another, back
+to back, as bench.py times them), each with its own label.
 
 --scrub writes, then reads, 1 GiB (four times the Infinity Cache) between
 launches, outside the HIP events, so each launch starts with nothing of its
@@ -30,7 +32,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-ALL = ["C1", "C2", "C2x2", "C4", "C3", "C2ext"]
+ALL = ["C1", "C2", "C2x2", "C4", "C4step", "C3", "C2ext", "C2rooms"]
 
 
 def main():
@@ -105,6 +107,48 @@ def main():
             fixed(1500, 2 << 20)
         elif c == "C4":
             fixed(1500, 4 << 20)
+        elif c == "C4step":
+            n, L = 4 << 20, 1500
+            tx, stride = synth.fixed_frames_device(n, L, seed=0x5E9 ^ n)
+            rx = tx.clone()
+            setup(ctx.compute_fixed, rx, stride, L, n)
+            v = torch.empty(n, dtype=torch.uint8, device="cuda")
+            for _ in range(3):
+                manifest.extend(["setup", "setup"])
+                ctx.compute_fixed(tx, stride, L, n, stream=stream)
+                ctx.verify_fixed(rx, stride, L, n, v, stream=stream)
+            ms = []
+            for _ in range(a.reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                manifest.extend([f"step_compute_fixed_{L}_{n}", f"step_verify_fixed_{L}_{n}"])
+                ctx.compute_fixed(tx, stride, L, n, stream=stream)
+                ctx.verify_fixed(rx, stride, L, n, v, stream=stream)
+                e1.record()
+                torch.cuda.synchronize()
+                ms.append(e0.elapsed_time(e1))
+            med = float(np.median(ms))
+            timings[f"step_fixed_{L}_{n}"] = {"median_us": med * 1e3,
+                                              "bytes_algorithmic": n * (2 * L + 5)}
+            print(f"step_fixed_{L}_{n:<22d} {med * 1e3:9.1f} us", file=sys.stderr, flush=True)
+            assert int((v != 0).sum()) == 0
+            del tx, rx
+        elif c == "C2rooms":
+            n, L, room = 1 << 20, 1500, 2048
+            buf, _ = synth.fixed_frames_device(n, L, stride=room, seed=0x800F)
+            off = torch.arange(n, device="cuda", dtype=torch.int64) * room
+            ln = torch.full((n,), L, dtype=torch.int16, device="cuda")
+            hint = gpucsum.K["GCS_VF_ROOMS"]
+            rx = buf.clone()
+            setup(ctx.compute, rx, off, ln, n, flags=hint)
+            v = torch.empty(n, dtype=torch.uint8, device="cuda")
+            measure(f"compute_rooms_{L}_{n}",
+                    lambda: ctx.compute(buf, off, ln, n, flags=hint, stream=stream), n * (L + 4))
+            measure(f"verify_rooms_{L}_{n}",
+                    lambda: ctx.verify(rx, off, ln, n, v, flags=hint, stream=stream), n * (L + 1))
+            torch.cuda.synchronize()
+            assert int((v != 0).sum()) == 0
+            del buf, rx
         elif c == "C3":
             n = 4 << 20
             lens = synth.imix_lengths(n, seed=0x494D)

@@ -237,8 +237,10 @@ def test_async_tx_fill_wire_identical(H, P, monkeypatch, group, registered):
     """Fill as you go (GPUCSUM_TX_GROUP): completed frames go to the burst
     server in groups while the mTCP-shaped loop builds the rest; send_pkts
     posts the tail and waits.  The wire equals the software folds' for every
-    group size, with the synthetic NIC's TX rooms pageable (staged) or
-    registered (filled in place over PCIe)."""
+    group size, with the synthetic NIC's TX rooms pageable or registered
+    (both staged into device memory by default since round 4, gcs_api.cpp
+    async_reg_stage; GCS_ASYNC_REGISTERED=inplace reads registered rooms in
+    place over PCIe)."""
     import torch
     if not torch.cuda.is_available():
         pytest.fail("plugin GPU tests need a GPU (no CPU fallback exists)")

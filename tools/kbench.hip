@@ -5,7 +5,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../include tools/kbench.hip -o tools/kbench
 //   tools/kbench [frame_len=1500] [n=1048576] [rounds=15]
 #include "../mtcp_amd/csrc/gcs_kernels.hip"
-#include "gro_pipe.hip"
+#include "attic/gro_pipe.hip"   // measured, not shipped
 
 #include <algorithm>
 #include <cstdio>
@@ -173,6 +173,31 @@ __global__ void __launch_bounds__(256) k_sector_writes(uint8_t* __restrict__ buf
     if (f >= n || 16 * c >= lens[f])
         return;
     stg16<WM>(buf + off[f] + 16ull * c, make_uint4((u32)f, c, 0x5EC7u, 0u));
+}
+
+// the same set of 128 B lines as k_sector_writes touches
+// (the line holding each frame's sector 0), each written WHOLE, once (a frame
+// whose line its predecessor already starts in skips it).  8 lanes per frame.
+template <int WM>
+__global__ void __launch_bounds__(256) k_line_writes(uint8_t* __restrict__ buf, uint64_t total,
+                                                     const uint64_t* __restrict__ off, u32 n)
+{
+    const uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x, f = q >> 3;
+    const u32 c = (u32)(q & 7);
+    if (f >= n)
+        return;
+    const uint64_t line = off[f] & ~127ull;
+    if ((f > 0 && (off[f - 1] & ~127ull) == line) || line + 128 > total)
+        return;
+    stg16<WM>(buf + line + 16ull * c, make_uint4((u32)f, c, 0x1173u, 0u));
+}
+// (c): as many bytes as k_sector_writes stores (64 B per frame), contiguous.
+template <int WM>
+__global__ void __launch_bounds__(256) k_contig_writes(uint8_t* __restrict__ buf, uint64_t chunks)
+{
+    const uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (q < chunks)
+        stg16<WM>(buf + 16 * q, make_uint4((u32)q, 0x0C0Du, 0u, 0u));
 }
 
 __global__ void k_hdr_desc(uint8_t* buf, const uint64_t* off, const uint16_t* lens, uint64_t n)
@@ -1925,6 +1950,34 @@ int imix_main(uint64_t n, int rounds)
         hipLaunchKernelGGL((k_sector_writes<WM_SECTOR_NT>), dim3((4ull * n + 255) / 256),
                            dim3(256), 0, st, wbuf, doff, dlen, (u32)n);
     }});
+    {
+        // the C3 write-back's line set written three ways
+        const std::vector<uint64_t>& ho = off;
+        uint64_t nlines = 0;
+        for (size_t i = 0; i < n; i++)
+            nlines += (i == 0 || (ho[i - 1] & ~127ull) != (ho[i] & ~127ull)) &&
+                      (ho[i] & ~127ull) + 128 <= total;
+        std::printf("C3 write set: %zu sectors (%.1f MB), %llu distinct lines (%.1f MB)\n", n,
+                    64.0 * n / 1e6, (unsigned long long)nlines, 128.0 * nlines / 1e6);
+        vs.push_back({"write lines: the sectors' 128 B lines whole, sc1 (no reads)", 128.0 * nlines,
+                      [&](hipStream_t st) {
+            hipLaunchKernelGGL((k_line_writes<WM_SECTOR_SC1>), dim3((8ull * n + 255) / 256),
+                               dim3(256), 0, st, wbuf, total, doff, (u32)n);
+        }});
+        vs.push_back({"write lines: the sectors' 128 B lines whole, nt (no reads)", 128.0 * nlines,
+                      [&](hipStream_t st) {
+            hipLaunchKernelGGL((k_line_writes<WM_SECTOR_NT>), dim3((8ull * n + 255) / 256),
+                               dim3(256), 0, st, wbuf, total, doff, (u32)n);
+        }});
+        vs.push_back({"write contiguous: 64 B x frames, sc1", 64.0 * n, [&](hipStream_t st) {
+            hipLaunchKernelGGL((k_contig_writes<WM_SECTOR_SC1>), dim3((4ull * n + 255) / 256),
+                               dim3(256), 0, st, wbuf, 4ull * n);
+        }});
+        vs.push_back({"write contiguous: 64 B x frames, nt", 64.0 * n, [&](hipStream_t st) {
+            hipLaunchKernelGGL((k_contig_writes<WM_SECTOR_NT>), dim3((4ull * n + 255) / 256),
+                               dim3(256), 0, st, wbuf, 4ull * n);
+        }});
+    }
     vs.push_back({"read-ceiling uint4 NT (whole packed buffer)", (double)total,
                   [&](hipStream_t st) {
         hipLaunchKernelGGL((k_read<true>), dim3(cus * 8), dim3(256), 0, st, (const uint4*)rx,

@@ -7,7 +7,8 @@ mTCP's ProcessPacket (eth_in.c, ip_in.c, tcp_in.c; accepted segments stop at
 StreamHTSearch).  The synthetic NIC's RX rooms (2 KiB each, as mbufs) sit in pageable memory (staged by
 the library into pinned or, GCS_ASYNC_STAGE=device, device memory) or are
 registered with gcs_host_register, as an mbuf pool would be (read in place).  The software path -- the module alone,
-mTCP folding every frame on the CPU -- is timed the same way.  Prints one JSON
+mTCP folding every frame on the CPU -- is timed the same way, over pageable
+and over registered rooms (software_path_registered).  Prints one JSON
 object (tools/, not product)."""
 import ctypes as C
 import json
@@ -118,6 +119,9 @@ out = {"workload": f"{BURSTS} bursts of {BURST} x {L}B TCP frames ({len(bad)} co
        "blocked": "time the mTCP thread spends inside recv_pkts + get_rptr per burst"}
 ctx = C.create_string_buffer(64)
 out["software_path"] = run(vtab(H, "synth_module_func"), C.addressof(ctx), False)
+# the same software path over REGISTERED rooms: the host memory the fastest
+# GPU rows use (compare GPU and CPU bursts on matched rooms)
+out["software_path_registered"] = run(vtab(H, "synth_module_func"), C.addressof(ctx), True)
 MODES = [(False, g, "host") for g in ("0", "8", "16", "32", "64")] + \
         [(False, g, "device") for g in ("8", "16", "32")] + \
         [(True, g, "host") for g in ("0", "8", "16", "32")]

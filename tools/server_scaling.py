@@ -15,7 +15,10 @@ import json
 import os
 import sys
 
-os.environ.setdefault("GCS_SERVER_PROF", "1")
+if os.environ.get("SS_PROF", "1") == "1":
+    os.environ.setdefault("GCS_SERVER_PROF", "1")
+else:
+    os.environ.pop("GCS_SERVER_PROF", None)   # the shipped grid: host-side figures only
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from mtcp_amd import gpucsum  # noqa: E402

@@ -4,7 +4,8 @@ plugin's fill-as-you-go (GPUCSUM_TX_GROUP), through the mTCP-shaped TX loop
 PKT_TX_TCPIP_CSUM, send_pkts every 64 frames, core.c:846-848) over the
 synthetic NIC module, whose TX rooms are pageable or registered (in place).
 The software path (the module alone, mTCP folding on the CPU) is timed the
-same way.  Prints one JSON object (tools/, not product)."""
+same way, over pageable and over registered rooms (software_path_registered:
+the same host memory as the registered GPU rows).  Prints one JSON object (tools/, not product)."""
 import ctypes as C
 import json
 import os
@@ -69,6 +70,9 @@ out = {"workload": f"{BURSTS} bursts of {BURST} x {L}B TCP frames through mini_t
        "timer": "C clock_gettime around each send_pkts and each burst"}
 ctx = C.create_string_buffer(64)
 out["software_path"] = run(vtab(H, "synth_module_func"), C.addressof(ctx), False)
+# the same software path over REGISTERED rooms: the host memory the fastest
+# GPU rows use (compare GPU and CPU bursts on matched rooms)
+out["software_path_registered"] = run(vtab(H, "synth_module_func"), C.addressof(ctx), True)
 MODES = [(False, g, "host") for g in ("0", "8", "16")] + [(False, "8", "device"), (False, "16", "device")] + \
         [(True, g, "host") for g in ("0", "8", "16")] + [(True, None, "host"), (False, None, "host")] + \
         [(True, "16", "regstage")]
