@@ -49,7 +49,7 @@ def parse():
     p.add_argument("--settle-s", type=float, default=1.0,
                    help="untimed seconds of the same kernels before the W warmup steps: "
                         "the HBM/GPU clocks take ~10 ms of load to reach steady state "
-                        "(DESIGN.md §5); reported in the JSON line")
+                        "(DESIGN.md App. A); reported in the JSON line")
     p.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                    help="process group for the timing barrier / max-over-ranks only (nccl = "
                         "RCCL; gloo: rehearsing N>1 ranks on one GPU with GCS_BENCH_DEVICE)")
@@ -117,7 +117,7 @@ def time_steps(ctx, tx, rx, stride, frame_len, n, steps, warmup, world, torch, s
             ev[2].record()
 
     if settle_s > 0:
-        # bring HBM/GPU clocks to their loaded state (DESIGN.md §5): untimed
+        # bring HBM/GPU clocks to their loaded state (DESIGN.md App. A): untimed
         # passes of the same kernels, before and separate from the W warmups
         t_end = time.perf_counter() + settle_s
         while time.perf_counter() < t_end:
@@ -315,7 +315,7 @@ def c1_small_frames(ctx, torch, n=1 << 20, steps=20):
 def _settle(torch, fn, seconds=0.25):
     """Untimed launches of `fn` for `seconds`: the side measurements follow the
     CPU baseline, during which the GPU idles and its clocks drop; the first
-    ~10 ms of load then run 20-25 % slow (DESIGN.md §5, settle phase)."""
+    ~10 ms of load then run 20-25 % slow (DESIGN.md App. A, settle phase)."""
     t_end = time.perf_counter() + seconds
     while time.perf_counter() < t_end:
         for _ in range(20):
@@ -767,16 +767,26 @@ def plugin_bursts(gcs, reps=300):
 
 
 def plugin_threads():
-    """Bursts from several mTCP-like threads per GPU (tools/mt_probe.py), in a
-    child process with HIP's default hardware queues, as the plugin runs."""
+    """Bursts from several mTCP-like threads per GPU (tools/server_scaling.py,
+    child processes with HIP's default hardware queues, as the plugin runs):
+    one thread per ring (64-frame IMIX fill + verify per iteration) at 1 / 8 /
+    12 / 16 threads, and T threads each driving R rings with async posts
+    (rings_TxR: up to 24 hot rings with only 4 CPUs busy, so the CPU quota
+    does not confound the GPU side).  `unprofiled`: the shipped grid, per call
+    and post -> done; `profiled`: the same under GCS_SERVER_PROF, with the
+    GPU serving time (gpu_span_us: first serving block saw the request -> last
+    one's records stored) and its per-block phases."""
     import subprocess
-    env = dict(os.environ, MTP_LIGHT_THREADS="1,16,24")
-    try:
-        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "mt_probe.py")],
-                           capture_output=True, text=True, timeout=300, env=env)
-        return json.loads(r.stdout.strip().splitlines()[-1])
-    except Exception as e:   # a side measurement: report, never fail the bench line
-        return {"error": repr(e)[:200]}
+    out = {}
+    for name, prof in (("unprofiled", "0"), ("profiled", "1")):
+        env = dict(os.environ, SS_PROF=prof, SS_THREADS="1,8,12,16", SS_RINGS="4x2,4x4,4x6")
+        try:
+            r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "server_scaling.py")],
+                               capture_output=True, text=True, timeout=240, env=env)
+            out[name] = json.loads(r.stdout.strip().splitlines()[-1])
+        except Exception as e:   # a side measurement: report, never fail the bench line
+            out[name] = {"error": repr(e)[:200]}
+    return out
 
 
 def plugin_rx_async():

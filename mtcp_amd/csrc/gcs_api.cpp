@@ -80,7 +80,7 @@ constexpr int kSlots = 2;
 constexpr uint64_t kSlotAlign = 64;   // pslib packing, io_engine/lib/pslib.c:146
 // Host batches staged in at most this many bytes run in direct mode (the
 // kernel reads pinned staging over PCIe; run_host_batch).  Per-call latency,
-// DMA copies vs direct (tools/burst_lat.py, DESIGN.md §5): 64 x 1500 B verify
+// DMA copies vs direct (tools/burst_lat.py, DESIGN.md App. A): 64 x 1500 B verify
 // 42 -> 21 us, 256 x 1500 B 87 -> 29 us, 1024 x 1500 B 136 -> 96 us.  The env
 // variable GCS_DIRECT_MAX_BYTES overrides it (0 disables direct mode).
 constexpr uint64_t kDirectMaxBytes = 2u << 20;

@@ -22,7 +22,7 @@ struct Ext {
 // takes host batches from the request rings of up to kHubRings contexts (one
 // per mTCP thread) in pinned fine-grained memory, instead of one kernel
 // launch per batch -- and instead of one resident grid per context, each
-// holding a hardware queue of its own (DESIGN.md §5: 12 per-context grids
+// holding a hardware queue of its own (DESIGN.md App. A: 12 per-context grids
 // cost the pinned verify 6-15%).  The grid has kServerBlocks blocks per ring
 // in use (a ring's group); ring ids of the groups travel in the launch.
 //

@@ -11,7 +11,7 @@ namespace gcs {
 
 constexpr int kBlock = 256;
 
-// Launch-time choices, fixed by the A/B runs recorded in DESIGN.md §5
+// Launch-time choices, fixed by the A/B runs recorded in DESIGN.md App. A
 // (tools/kbench.hip): non-temporal loads for the once-read frame stream
 // (verify 250 -> 236 us per 1M x 1500 B), and check fields written back as
 // whole 64 B sectors with sc1 stores (no partial-line writes; the TX+RX step
@@ -125,7 +125,7 @@ k_fixed_x(uint8_t* __restrict__ frames, uint64_t stride, u32 frame_len, u32 n,
 // ihl == 5 word masks are compile-time constants per register, and the 64
 // verdict bytes of a wave are one coalesced 64 B store.  (The G-lane kernels
 // spend most of their instructions on reductions and a per-group epilogue at
-// this size: tools/kbench.hip)
+// this size: tools/kbench.hip, DESIGN.md App. A.)
 __device__ __forceinline__ XFrame small_xframe(const Ext& x, uint64_t i, const u32* nib)
 {
     XFrame f = xframe(x, i);
@@ -655,7 +655,7 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
             t_claim = t_last;
             // 3 x the gap when that is within hot_max (gaps <= hot_max / 3),
             // else the fixed window: a ring kept alive by one burst every
-            // 200 us still goes cold between them (the idle-poll cost)
+            // 200 us still goes cold between them (the idle-poll cost, DESIGN App. A)
             win = 3 * gap <= hot_max_ticks ? (3 * gap < hot_ticks ? hot_ticks : 3 * gap)
                                            : hot_ticks;
         }
@@ -726,7 +726,7 @@ struct DescShape {
     static constexpr int T0 = 16 * G0 * U0, T1 = 16 * G1 * U1;
 };
 
-// The shipped shapes (A/B in tools/kbench.hip imix, DESIGN.md §5).  The fill
+// The shipped shapes (A/B in tools/kbench.hip imix, DESIGN.md App. A).  The fill
 // stages each frame's sector 0 in LDS and stores the block's sectors together
 // at its end, in frame order, non-temporal: 4M IMIX 390 -> 377-379 us (in the
 // epilogues: sc1 390, nt 411; staged: sc1 409, sc0 sc1 410;

@@ -43,11 +43,25 @@ def server_stats():
     return {k: round(a[i], 3) for i, k in enumerate(KEYS)}
 
 
+def cpu_quota():
+    """CPUs this process may use: affinity, and the cgroup v2 quota if any."""
+    q = None
+    try:
+        a, b = open("/sys/fs/cgroup/cpu.max").read().split()
+        if a != "max":
+            q = int(a) / int(b)
+    except (OSError, ValueError):
+        pass
+    return {"affinity": len(os.sched_getaffinity(0)), "cgroup_quota": q}
+
+
 def main():
     os.environ["MT_CHECK_EVERY"] = os.environ.get("MT_CHECK_EVERY", "16")
     out = {"config": {k: os.environ.get(k, "default") for k in
                       ("GCS_SERVER_MAILBOX", "GCS_SERVER_ACQUIRE", "GCS_SERVER_PROF",
-                       "GCS_DIRECT_STAGE", "GCS_SERVER_HOT_NAPS", "GCS_SERVER_HOT_US")}}
+                       "GCS_DIRECT_STAGE", "GCS_SERVER_HOT_NAPS", "GCS_SERVER_HOT_US")},
+           "cpus": cpu_quota(),
+           "cpu_frac": "thread CPU time / wall time inside the calls (below 1: descheduled)"}
     iters = int(os.environ.get("SS_ITERS", "600"))
     for threads in [int(x) for x in os.environ.get("SS_THREADS", "1,4,8,12,16").split(",") if x]:
         mis, fr, us = C.c_uint64(), C.c_uint64(), C.c_double()
