@@ -561,8 +561,17 @@ def rows_8f(ctx, torch, n=1 << 20, L=1500):
     out["lro_ms"] = ms
     out["lro_merged_frames"] = heads
     out["lro_gbs_algorithmic"] = 2 * n * L / (ms * 1e-3) / 1e9
+    out["lro_frac_peak"] = 2 * n * L / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+    # windows of 256 frames (an ENABLELRO DPDK build's larger bursts,
+    # dpdk_module.c:44-48): the run-per-wave k_gro<2, 256>
+    ms = _launch_ms(torch, lambda: ctx.gro(sb, off, lens, v, n, 256, 16384, o, oo, ol, hd,
+                                           stream=stream))
+    assert int((ol != 0).sum()) == n // 8
+    out["lro_w256_ms"] = ms
+    out["lro_w256_frac_peak"] = 2 * n * L / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS
     out["workload"] = (f"{n} x {L} B frames; RSS 16 queues; copy+fill {pl} B payloads from a "
-                       "contiguous send buffer; LRO 16 flows in runs of 8, windows of 64")
+                       "contiguous send buffer; LRO 16 flows in runs of 8, windows of 64 "
+                       "(lro_w256: windows of 256)")
     return out
 
 

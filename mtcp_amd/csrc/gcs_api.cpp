@@ -407,6 +407,9 @@ class ServerHub {
                 : std::strcmp(acq, "agent") == 0 ? gcs::kServerAcqAgent
                 : std::strcmp(acq, "none") == 0  ? gcs::kServerAcqNone
                                                  : 0u;
+        const char* pol = std::getenv("GCS_SERVER_POLL");
+        if (pol && std::strcmp(pol, "leader") == 0)
+            opts_ |= gcs::kServerLeaderPoll;
         HIP_TRY(hipMalloc((void**)&dpub_, sizeof(gcs::HubPub)));
         HIP_TRY(hipMemset(dpub_, 0, sizeof(gcs::HubPub)));
         // the highest priority: a queue pool of its own, so the resident grid

@@ -195,6 +195,10 @@ hipError_t launch_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, int gro
 // no acquire for device frames.
 constexpr uint32_t kServerAcqAgent = 1u;
 constexpr uint32_t kServerAcqNone = 2u;
+// opts, an A/B knob (GCS_SERVER_POLL=leader): only each group's leader polls
+// the request lines; the other blocks follow its device-memory entry (as cold
+// rings do) and read their lines once it names a request with frames for them.
+constexpr uint32_t kServerLeaderPoll = 4u;
 constexpr uint32_t kModeDevFrames = 1u << 31;
 
 hipError_t launch_verify_fixed(uint8_t* frames, uint64_t stride, uint32_t frame_len, uint32_t n,

@@ -375,6 +375,10 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
     uint64_t p_issue = 0, p_seen = 0, p_rtt = 0, p_sum[kProfWords - kProfN] = {};
     uint64_t p_polls0 = 0, p_rtt0 = 0, p_slow2 = 0, p_slow5 = 0, p_maxrtt = 0, p_torn = 0;
     bool p_cold = false;                     // a cold poll since the last request
+    // kServerLeaderPoll: a follower polls the leader's entry until it names a
+    // request with frames here (armed), then reads that request's lines
+    const bool lead_poll = (opts & kServerLeaderPoll) && !leader;
+    bool armed = false;
     // ack[blk] must stay within 2^31 of the ring's requests (the host reads
     // it as a 32-bit serial number): a block acks each request that wrote
     // frames in place, and otherwise refreshes it at the start and every 2^30
@@ -406,7 +410,7 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
         if (wave == 0) {
             for (;;) {
                 const uint64_t now = __builtin_amdgcn_s_memrealtime();
-                const bool hot = now - t_last <= win;
+                const bool hot = lead_poll ? armed : now - t_last <= win;
                 // ONE load per lane, all in flight together: the lines of q
                 // when hot (the leader reads line A when cold too), the
                 // leader's entry for q's slot for a cold follower (the 16 B
@@ -487,10 +491,12 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
                 } else {
                     // the leader's entry for q's slot: q itself (skip it unless
                     // it has frames here), a newer request (q is done), or older
-                    if (x0 == q && first < z0)
+                    if (x0 == q && first < z0) {
                         t_last = now;
-                    else if ((int32_t)(x0 - q) >= 0)
+                        armed = true;
+                    } else if ((int32_t)(x0 - q) >= 0) {
                         act = SKIP;
+                    }
                 }
                 if (__shfl(v.x, 63) != 0 || now - t_start > life_ticks || ++polls >= max_polls ||
                     (act == IDLE && now - t_last > idle_ticks))
@@ -647,6 +653,7 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
             s_claim = IDLE;
         }
         last = qend;
+        armed = false;
         if (PROF && act == WORK)
             p_cold = false;
         t_last = __builtin_amdgcn_s_memrealtime();

@@ -11,3 +11,5 @@ run() {   # name, env...
 run dev_auto SS_THREADS=1,8,12,16 SS_RINGS=4x1,4x4,4x6 || exit 1
 run dev_noprof SS_PROF=0 SS_THREADS=1,8,12,16 SS_RINGS=4x1,4x4,4x6 || exit 1
 run host_noprof SS_PROF=0 GCS_SERVER_MAILBOX=host SS_THREADS=1,8,12,16 SS_RINGS=4x4 || exit 1
+run dev_leader GCS_SERVER_POLL=leader SS_THREADS=1,8,12,16 SS_RINGS=4x1,4x4,4x6 || exit 1
+run dev_leader_noprof SS_PROF=0 GCS_SERVER_POLL=leader SS_THREADS=1,8,12,16 SS_RINGS=4x1,4x4,4x6 || exit 1
