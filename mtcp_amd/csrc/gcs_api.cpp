@@ -285,6 +285,7 @@ class ServerHub {
         read_knobs();
         std::memset(&mb_->ring[k], 0, sizeof(gcs::ServerMailbox));
         std::memset(&rq_->req[k], 0, sizeof rq_->req[k]);
+        std::memset(&rq_->prof[k], 0, sizeof rq_->prof[k]);
         // every slot reads as holding `start` (done): a slot left at 0 would
         // read as NEWER than the next request near the 32-bit wrap, and be
         // skipped as done
@@ -361,6 +362,7 @@ class ServerHub {
 
     gcs::ServerMailbox* ring(int r) { return &mb_->ring[r]; }
     gcs::ServerReq* reqs(int r) { return rq_->req[r]; }
+    const uint64_t (*prof_sums(int r) const)[gcs::kProfWords] { return rq_->prof[r]; }
     bool dev_mailbox() const { return dev_mailbox_; }
     bool prof() const { return prof_; }
     double ticks_per_us() const { return ticks_per_us_; }
@@ -407,9 +409,7 @@ class ServerHub {
                 : std::strcmp(acq, "agent") == 0 ? gcs::kServerAcqAgent
                 : std::strcmp(acq, "none") == 0  ? gcs::kServerAcqNone
                                                  : 0u;
-        const char* pol = std::getenv("GCS_SERVER_POLL");
-        if (pol && std::strcmp(pol, "leader") == 0)
-            opts_ |= gcs::kServerLeaderPoll;
+
         HIP_TRY(hipMalloc((void**)&dpub_, sizeof(gcs::HubPub)));
         HIP_TRY(hipMemset(dpub_, 0, sizeof(gcs::HubPub)));
         // the highest priority: a queue pool of its own, so the resident grid
@@ -467,7 +467,9 @@ class ServerHub {
     {
         if (!launched_.load(std::memory_order_relaxed))
             return GCS_OK;
-        __atomic_store_n(&mb_->cmd.v, 1u, __ATOMIC_RELEASE);
+        __atomic_store_n(&rq_->cmd.v, 1u, __ATOMIC_RELEASE);
+        if (dev_mailbox_)
+            _mm_sfence();                 // write-combined over the BAR: out now
         HIP_TRY(hipStreamSynchronize(stream_));
         launched_.store(false, std::memory_order_release);
         return GCS_OK;
@@ -486,7 +488,9 @@ class ServerHub {
                 __atomic_store_n(&st.v, 0u, __ATOMIC_RELAXED);
             ring_of_[groups++] = (uint32_t)k;
         }
-        __atomic_store_n(&mb_->cmd.v, 0u, __ATOMIC_RELEASE);
+        __atomic_store_n(&rq_->cmd.v, 0u, __ATOMIC_RELEASE);
+        if (dev_mailbox_)
+            _mm_sfence();
         HIP_TRY(hipMemsetAsync(dpub_->exit, 0, sizeof dpub_->exit, stream_));
         // ring_of_ is only rewritten under mu_ after the previous grid left and
         // this copy completed (stop_locked synchronises the stream)
@@ -738,7 +742,7 @@ class BurstServer {
             const auto tp = std::chrono::steady_clock::now();
             for (int k = 0; k < nb; k++) {
                 const int b = gcs::server_block(r.q, (uint32_t)k * gcs::kServerFPB);
-                const __m128i* mp = reinterpret_cast<const __m128i*>(&mb_->prof[b][gcs::kProfMarks]);
+                const __m128i* mp = reinterpret_cast<const __m128i*>(&mb_->mark[b][0]);
                 alignas(16) uint32_t mk[4];
                 int32_t d;
                 for (;;) {
@@ -794,10 +798,13 @@ class BurstServer {
         st->gpu_span_us = prof_n_ ? prof_span_ / prof_n_ : 0.0;
         st->seen_skew_us = prof_n_ ? prof_skew_ / prof_n_ : 0.0;
         st->block_serve_us = prof_n_ ? prof_serve_ / prof_n_ : 0.0;
+        // the sums live beside the request lines (device memory by default:
+        // read over the BAR, a few hundred slow loads, only here)
         uint64_t sum[gcs::kProfWords] = {};
+        const uint64_t (*pr)[gcs::kProfWords] = hub_->prof_sums(r_);
         for (int b = 0; b < gcs::kServerBlocks; b++)
-            for (int k = gcs::kProfN; k < gcs::kProfWords; k++)
-                sum[k] += __atomic_load_n(&mb_->prof[b][k], __ATOMIC_RELAXED);
+            for (int k = 0; k < gcs::kProfWords; k++)
+                sum[k] += k == gcs::kProfMaxRtt ? 0 : __atomic_load_n(&pr[b][k], __ATOMIC_RELAXED);
         const double tu = hub_->ticks_per_us();
         const double nreq = sum[gcs::kProfN] ? (double)sum[gcs::kProfN] : 1.0;
         st->block_requests = sum[gcs::kProfN];
@@ -815,7 +822,7 @@ class BurstServer {
         st->torn_polls = sum[gcs::kProfTorn];
         uint64_t mx = 0;
         for (int b = 0; b < gcs::kServerBlocks; b++)
-            mx = std::max<uint64_t>(mx, __atomic_load_n(&mb_->prof[b][gcs::kProfMaxRtt],
+            mx = std::max<uint64_t>(mx, __atomic_load_n(&pr[b][gcs::kProfMaxRtt],
                                                         __ATOMIC_RELAXED));
         st->max_poll_us = mx / tu;
         for (int b = 0; b < gcs::kServerBlocks; b++)

@@ -78,9 +78,9 @@ struct alignas(64) ServerLine {
     uint32_t pad[15];
 };
 // A request slot's lines: written by the host, read by the grid.  They live
-// in HubReqs, which is pinned host memory (the grid polls it over PCIe) or,
-// with GCS_SERVER_MAILBOX=device, uncached device memory the host writes over
-// the BAR (the grid polls HBM: no PCIe read per poll).
+// in HubReqs: uncached device memory the host writes over the BAR (default;
+// the grid polls HBM: no PCIe read per poll) or, with
+// GCS_SERVER_MAILBOX=host, pinned host memory the grid polls over PCIe.
 struct alignas(64) ServerReq {
     ServerReqA a;
     ServerReqB b;
@@ -95,43 +95,47 @@ struct alignas(64) ServerReq {
 struct alignas(64) ServerRes {
     uint64_t rec[kSlotFrames];
 };
-// GCS_SERVER_PROF (the k_burst_server<PROF> instantiation): per block, the
-// marks of the last request it served frames of (GPU wall clock, 100 MHz),
-// tagged with its number (written last), and running sums over its requests.
+// GCS_SERVER_PROF (the k_burst_server<PROF> instantiation): per block,
+// running sums over the requests it served (HubReqs::prof, next to the
+// request lines: in device memory they cost the PCIe link nothing), and the
+// marks of its last request (ServerMailbox::mark, host memory: the host waits
+// for them per request).
 enum ServerProf {
-    kProfMarks = 0,     // words 0-1: ONE 16 B store {seen, rec, q, 0} (u32 each):
-                        // the low 32 bits of the clock when the poll that saw
-                        // request q returned and when its records were stored
-                        // (acknowledged); one store, so no fence orders the
-                        // marks before their tag
-    kProfN = 8,         // requests with frames in this block
-    kProfSeenRtt = 9,   // sum: issue -> return of the poll that saw a request
-    kProfAcq = 10,      // sum: the acquire after the poll
-    kProfFrames = 11,   // sum: frame loads, folds, record stores issued
-    kProfRecs = 12,     // sum: the record stores' acknowledgement
-    kProfPolls = 13,    // sum: polls (all)
-    kProfPollRtt = 14,  // sum: issue -> return, all polls
-    kProfRel = 15,      // sum: release fence + ack (requests that wrote frames)
-    kProfCold = 16,     // sum: requests the block was cold for when they came
-    kProfSlow2 = 17,    // polls whose round trip took over 2 us
-    kProfSlow5 = 18,    // ... over 5 us
-    kProfMaxRtt = 19,   // the longest poll round trip (ticks)
-    kProfTorn = 20,     // polls that saw line A of the request but not all its lines
-    kProfWords = 24
+    kProfN = 0,         // requests with frames in this block
+    kProfSeenRtt = 1,   // sum: issue -> return of the poll that saw a request
+    kProfAcq = 2,       // sum: the acquire after the poll
+    kProfFrames = 3,    // sum: frame loads, folds, record stores issued
+    kProfRecs = 4,      // sum: the record stores' acknowledgement
+    kProfPolls = 5,     // sum: polls (all)
+    kProfPollRtt = 6,   // sum: issue -> return, all polls
+    kProfRel = 7,       // sum: release fence + ack (requests that wrote frames)
+    kProfCold = 8,      // sum: requests the block was cold for when they came
+    kProfSlow2 = 9,     // polls whose round trip took over 2 us
+    kProfSlow5 = 10,    // ... over 5 us
+    kProfMaxRtt = 11,   // the longest poll round trip (ticks)
+    kProfTorn = 12,     // polls that saw line A of the request but not all its lines
+    kProfWords = 16
 };
 // One context's ring (pinned host memory).
 struct ServerMailbox {
     ServerLine ack[kServerBlocks];       // device: the last request each block served frames of
     ServerLine state[kServerBlocks];     // device: 1 serving, 2 exited (this launch's group)
-    uint64_t prof[kServerBlocks][kProfWords];   // device, GCS_SERVER_PROF (ServerProf)
+    // device, GCS_SERVER_PROF: ONE 16 B store per request {seen, rec, q, 0}
+    // (u32 each): the low 32 bits of the clock when the poll that saw request
+    // q returned and when its records were stored (acknowledged) -- one
+    // store, so no fence orders the marks before their tag
+    uint64_t mark[kServerBlocks][2];
     ServerRes res[kServerSlots];
 };
 struct HubMailbox {
-    ServerLine cmd;                      // host: 1 = leave now (the group leaders poll it)
     ServerMailbox ring[kHubRings];
 };
+// Written by the host, read by the grid (and the profile sums the other way):
+// uncached device memory over the BAR by default, else pinned host memory.
 struct HubReqs {
+    ServerLine cmd;                      // host: 1 = leave now (the group leaders poll it)
     ServerReq req[kHubRings][kServerSlots];
+    uint64_t prof[kHubRings][kServerBlocks][kProfWords];   // device, GCS_SERVER_PROF sums
 };
 
 // Device memory.  ent[r][q % kServerSlots] = q << 32 | n for each request q
@@ -195,10 +199,7 @@ hipError_t launch_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, int gro
 // no acquire for device frames.
 constexpr uint32_t kServerAcqAgent = 1u;
 constexpr uint32_t kServerAcqNone = 2u;
-// opts, an A/B knob (GCS_SERVER_POLL=leader): only each group's leader polls
-// the request lines; the other blocks follow its device-memory entry (as cold
-// rings do) and read their lines once it names a request with frames for them.
-constexpr uint32_t kServerLeaderPoll = 4u;
+
 constexpr uint32_t kModeDevFrames = 1u << 31;
 
 hipError_t launch_verify_fixed(uint8_t* frames, uint64_t stride, uint32_t frame_len, uint32_t n,

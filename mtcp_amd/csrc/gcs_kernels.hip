@@ -220,104 +220,6 @@ k_desc(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __re
                                                 out_csum ? out_csum + i : nullptr);
 }
 
-// Descriptor batch with the rooms hint (GCS_VF_ROOMS / GCS_CF_ROOMS: frames
-// one per mbuf room): one G-lane group per frame as k_desc, XCD-contiguous
-// blocks, K frames per group, FPB apart: the K descriptors are loaded
-// together, then all K frames' first batches, before the first is folded --
-// so a wave waits on one descriptor trip per K frames instead of one per
-// frame (k_fixed has no descriptor trip at all).
-// SEQ: the K frames' loads are not issued together; only their descriptors
-// are (fewer VGPRs: K = 2 unrolled takes 92-102, 4-5 waves per SIMD).
-template <int G, int U, bool COMPUTE, int WM, int K, bool SEQ = false>
-__global__ void __launch_bounds__(kBlock)
-k_rooms(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __restrict__ off,
-        const uint16_t* __restrict__ lens, u32 n, uint8_t* __restrict__ out_code,
-        uint32_t* __restrict__ out_csum, u32 flags)
-{
-    constexpr int FPB = kBlock / G;
-    const int sub = threadIdx.x & (G - 1);
-    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);
-    const uint64_t i0 = (uint64_t)blk * FPB * K + threadIdx.x / G;
-    if (i0 >= n)
-        return;                                        // whole group leaves together
-    uint64_t o[K];
-    u32 len[K];
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        const uint64_t i = i0 + (uint64_t)k * FPB;
-        o[k] = i < n ? off[i] : 0;
-        len[k] = i < n ? lens[i] : 0;
-    }
-    if constexpr (SEQ) {
-#pragma unroll 1
-        for (int k = 0; k < K; k++) {
-            const uint64_t i = i0 + (uint64_t)k * FPB;
-            if (i >= n)
-                break;
-            const bool ok = (o[k] & 15) == 0 && o[k] <= frames_bytes &&
-                            len[k] <= frames_bytes - o[k];
-            do_frame<G, U, COMPUTE, true, true, kNT, WM>(
-                frames + (ok ? o[k] : 0), len[k], ok ? (int64_t)(frames_bytes - o[k]) : 0, ok,
-                sub, flags, out_code ? out_code + i : nullptr, out_csum ? out_csum + i : nullptr);
-        }
-        return;
-    }
-    uint4 v[K][U];
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        const bool ok = (o[k] & 15) == 0 && o[k] <= frames_bytes && len[k] <= frames_bytes - o[k];
-        const int nch = ok ? (int)((len[k] + 15) >> 4) : 0;
-        load_first<G, U, true, kNT>(frames + (ok ? o[k] : 0), nch,
-                                    ok ? (int64_t)(frames_bytes - o[k]) : 0, sub, v[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        const uint64_t i = i0 + (uint64_t)k * FPB;
-        if (i >= n)
-            break;                                     // group-uniform, and so are later k
-        const bool ok = (o[k] & 15) == 0 && o[k] <= frames_bytes && len[k] <= frames_bytes - o[k];
-        uint8_t* f = frames + (ok ? o[k] : 0);
-        frame_body<G, U, COMPUTE, true, true, kNT, WM>(
-            v[k], f, f, len[k], ok ? (int64_t)(frames_bytes - o[k]) : 0, ok, sub, flags,
-            out_code ? out_code + i : nullptr, out_csum ? out_csum + i : nullptr, true);
-    }
-}
-
-// k_rooms with the block's K * 256 / G descriptors loaded into LDS first (one
-// coalesced trip), then each group walks its K frames from LDS.
-template <int G, int U, bool COMPUTE, int WM, int K>
-__global__ void __launch_bounds__(kBlock, COMPUTE ? 7 : 8)
-k_rooms_lds(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __restrict__ off,
-            const uint16_t* __restrict__ lens, u32 n, uint8_t* __restrict__ out_code,
-            uint32_t* __restrict__ out_csum, u32 flags)
-{
-    constexpr int FPB = kBlock / G, FB = FPB * K;
-    static_assert(FB <= kBlock, "one descriptor per thread");
-    __shared__ uint64_t s_off[FB];
-    __shared__ uint16_t s_len[FB];
-    const int t = threadIdx.x, sub = t & (G - 1), g = t / G;
-    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);
-    const uint64_t base = (uint64_t)blk * FB;
-    if (t < FB && base + t < n) {
-        s_off[t] = off[base + t];
-        s_len[t] = lens[base + t];
-    }
-    __syncthreads();
-#pragma unroll 1
-    for (int k = 0; k < K; k++) {
-        const int l = k * FPB + g;
-        const uint64_t i = base + l;
-        if (i >= n)
-            break;                                     // group-uniform
-        const uint64_t o = s_off[l];
-        const u32 len = s_len[l];
-        const bool ok = (o & 15) == 0 && o <= frames_bytes && len <= frames_bytes - o;
-        do_frame<G, U, COMPUTE, true, true, kNT, WM>(
-            frames + (ok ? o : 0), len, ok ? (int64_t)(frames_bytes - o) : 0, ok, sub, flags,
-            out_code ? out_code + i : nullptr, out_csum ? out_csum + i : nullptr);
-    }
-}
-
 // Burst server: a grid of kServerBlocks blocks per ring in use that stays
 // resident for at most life_ticks (wall clock) and serves the host batches
 // posted in the contexts' request rings (gcs_internal.h HubMailbox) -- each
@@ -372,13 +274,10 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
     // requests when that is <= hot_max_ticks, at least hot_ticks
     uint64_t win = hot_ticks, t_claim = t_start;
     // GCS_SERVER_PROF (thread 0): this launch's additions to the block's sums
-    uint64_t p_issue = 0, p_seen = 0, p_rtt = 0, p_sum[kProfWords - kProfN] = {};
+    uint64_t p_issue = 0, p_seen = 0, p_rtt = 0, p_sum[kProfWords] = {};
+    uint64_t* const psum = rq->prof[r][blk];
     uint64_t p_polls0 = 0, p_rtt0 = 0, p_slow2 = 0, p_slow5 = 0, p_maxrtt = 0, p_torn = 0;
     bool p_cold = false;                     // a cold poll since the last request
-    // kServerLeaderPoll: a follower polls the leader's entry until it names a
-    // request with frames here (armed), then reads that request's lines
-    const bool lead_poll = (opts & kServerLeaderPoll) && !leader;
-    bool armed = false;
     // ack[blk] must stay within 2^31 of the ring's requests (the host reads
     // it as a 32-bit serial number): a block acks each request that wrote
     // frames in place, and otherwise refreshes it at the start and every 2^30
@@ -389,18 +288,18 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
     if (t == 0) {
         s_claim = IDLE;
         if (PROF)                            // the sums go on from the block's last launch
-            for (int k = 0; k < kProfWords - kProfN; k++)
-                p_sum[k] = __hip_atomic_load(&rm->prof[blk][kProfN + k], __ATOMIC_RELAXED,
+            for (int k = 0; k < kProfWords; k++)
+                p_sum[k] = __hip_atomic_load(&psum[k], __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&rm->ack[blk].v, last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&rm->state[blk].v, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    p_polls0 = p_sum[kProfPolls - kProfN];
-    p_rtt0 = p_sum[kProfPollRtt - kProfN];
-    p_slow2 = p_sum[kProfSlow2 - kProfN];
-    p_slow5 = p_sum[kProfSlow5 - kProfN];
-    p_maxrtt = p_sum[kProfMaxRtt - kProfN];
-    p_torn = p_sum[kProfTorn - kProfN];
+    p_polls0 = p_sum[kProfPolls];
+    p_rtt0 = p_sum[kProfPollRtt];
+    p_slow2 = p_sum[kProfSlow2];
+    p_slow5 = p_sum[kProfSlow5];
+    p_maxrtt = p_sum[kProfMaxRtt];
+    p_torn = p_sum[kProfTorn];
     __syncthreads();
     for (;;) {
         const uint32_t q = server_next(last);            // the request this block serves next
@@ -410,7 +309,7 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
         if (wave == 0) {
             for (;;) {
                 const uint64_t now = __builtin_amdgcn_s_memrealtime();
-                const bool hot = lead_poll ? armed : now - t_last <= win;
+                const bool hot = now - t_last <= win;
                 // ONE load per lane, all in flight together: the lines of q
                 // when hot (the leader reads line A when cold too), the
                 // leader's entry for q's slot for a cold follower (the 16 B
@@ -437,7 +336,7 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
                     src = reinterpret_cast<const volatile u32x4*>(
                         &pub->ent[r][(q % kServerSlots) & ~1u]);
                 else if (lane == 63 && (leader || (polls & 7) == 0))
-                    src = leader ? reinterpret_cast<const volatile u32x4*>(&mb->cmd.v)
+                    src = leader ? reinterpret_cast<const volatile u32x4*>(&rq->cmd.v)
                                  : reinterpret_cast<const volatile u32x4*>(&pub->exit[r].v);
                 u32x4 v = {0, 0, 0, 0};
                 if (src)
@@ -491,12 +390,10 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
                 } else {
                     // the leader's entry for q's slot: q itself (skip it unless
                     // it has frames here), a newer request (q is done), or older
-                    if (x0 == q && first < z0) {
+                    if (x0 == q && first < z0)
                         t_last = now;
-                        armed = true;
-                    } else if ((int32_t)(x0 - q) >= 0) {
+                    else if ((int32_t)(x0 - q) >= 0)
                         act = SKIP;
-                    }
                 }
                 if (__shfl(v.x, 63) != 0 || now - t_start > life_ticks || ++polls >= max_polls ||
                     (act == IDLE && now - t_last > idle_ticks))
@@ -625,35 +522,34 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
             }
             if (PROF && mine) {
                 const uint64_t t_rel = clock_after_vmem();
-                p_sum[kProfN - kProfN] += 1;
-                p_sum[kProfSeenRtt - kProfN] += p_seen - p_issue;
-                p_sum[kProfAcq - kProfN] += t_acq - p_seen;
-                p_sum[kProfFrames - kProfN] += t_frames - t_acq;
-                p_sum[kProfRecs - kProfN] += t_rec - t_frames;
-                p_sum[kProfRel - kProfN] += writes ? t_rel - t_rec : 0;
-                p_sum[kProfPolls - kProfN] = p_polls0 + polls;
-                p_sum[kProfPollRtt - kProfN] = p_rtt0 + p_rtt;
-                p_sum[kProfCold - kProfN] += p_cold ? 1 : 0;
-                p_sum[kProfSlow2 - kProfN] = p_slow2;
-                p_sum[kProfSlow5 - kProfN] = p_slow5;
-                p_sum[kProfMaxRtt - kProfN] = p_maxrtt;
-                p_sum[kProfTorn - kProfN] = p_torn;
-                // relaxed stores only: a release here would write back the
-                // XCD's L2 per request and perturb what it measures
-                uint64_t* pr = rm->prof[blk];
-                for (int k = 0; k < kProfWords - kProfN; k++)
-                    __hip_atomic_store(&pr[kProfN + k], p_sum[k], __ATOMIC_RELAXED,
+                p_sum[kProfN] += 1;
+                p_sum[kProfSeenRtt] += p_seen - p_issue;
+                p_sum[kProfAcq] += t_acq - p_seen;
+                p_sum[kProfFrames] += t_frames - t_acq;
+                p_sum[kProfRecs] += t_rec - t_frames;
+                p_sum[kProfRel] += writes ? t_rel - t_rec : 0;
+                p_sum[kProfPolls] = p_polls0 + polls;
+                p_sum[kProfPollRtt] = p_rtt0 + p_rtt;
+                p_sum[kProfCold] += p_cold ? 1 : 0;
+                p_sum[kProfSlow2] = p_slow2;
+                p_sum[kProfSlow5] = p_slow5;
+                p_sum[kProfMaxRtt] = p_maxrtt;
+                p_sum[kProfTorn] = p_torn;
+                // relaxed stores only (a release here would write back the
+                // XCD's L2 per request and perturb what it measures), the sums
+                // next to the request lines (device memory: no PCIe traffic)
+                for (int k = 0; k < kProfWords; k++)
+                    __hip_atomic_store(&psum[k], p_sum[k], __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_SYSTEM);
                 const u32x4 mk = {(u32)p_seen, (u32)t_rec, q, 0u};
                 asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1"
-                             : : "v"(&pr[kProfMarks]), "v"(mk) : "memory");
+                             : : "v"(&rm->mark[blk][0]), "v"(mk) : "memory");
             }
             __hip_atomic_store(&pub->prog[r][blk], qend, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
             s_claim = IDLE;
         }
         last = qend;
-        armed = false;
         if (PROF && act == WORK)
             p_cold = false;
         t_last = __builtin_amdgcn_s_memrealtime();
@@ -682,13 +578,28 @@ hipError_t launch_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, int gro
     if (groups < 1 || groups > kHubRings)
         return hipErrorInvalidValue;
     const dim3 grid(kServerBlocks * groups);
+    // ONE server block per CU: 96 KiB of dynamic LDS per block (unused; a CU
+    // has 160 KiB), so the dispatcher cannot stack up to four of them (117
+    // VGPRs, four waves) on a CU whose memory pipeline they then share.  With
+    // 8-24 rings, per-call times varied 1.5x from grid to grid without it
+    // (DESIGN.md §5).  GCS_SERVER_LDS_KB overrides (0: none).
+    static const size_t lds = [] {
+        const char* e = std::getenv("GCS_SERVER_LDS_KB");
+        return (e ? (size_t)std::strtoul(e, nullptr, 10) : (size_t)96) << 10;
+    }();
+    if (lds > 65536) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_burst_server<32, 3, true>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_burst_server<32, 3, false>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    }
     if (prof)
-        hipLaunchKernelGGL((k_burst_server<32, 3, true>), grid, dim3(kBlock), 0, s, mb, rq, pub,
+        hipLaunchKernelGGL((k_burst_server<32, 3, true>), grid, dim3(kBlock), lds, s, mb, rq, pub,
                            idle_ticks, life_ticks, hot_ticks, hot_max_ticks, max_polls, naps,
                            opts);
     else
-        hipLaunchKernelGGL((k_burst_server<32, 3, false>), grid, dim3(kBlock), 0, s, mb, rq, pub,
-                           idle_ticks, life_ticks, hot_ticks, hot_max_ticks, max_polls, naps,
+        hipLaunchKernelGGL((k_burst_server<32, 3, false>), grid, dim3(kBlock), lds, s, mb, rq,
+                           pub, idle_ticks, life_ticks, hot_ticks, hot_max_ticks, max_polls, naps,
                            opts);
     return hipGetLastError();
 }
@@ -2555,52 +2466,28 @@ using StreamShip = std::conditional_t<COMPUTE, StreamShape<8, 8192, 7, 4, 32, 2>
 // passes per block region (blockIdx.y): 3 x 8,192 chunks hold 256 packed
 // frames of up to 1,536 B; what a block has beyond them goes per frame
 constexpr int kStreamPasses = 3;
-// GCS_ROOMS_K: frames per group of k_rooms (1, 2 or 4 with their loads issued
-// together; 12 / 14: 2 / 4 with only the descriptors together, SEQ; an A/B
-// knob, read once).
-static int rooms_k()
+// Frames one per room (GCS_VF_ROOMS / GCS_CF_ROOMS): k_desc<32, 3>, one group
+// per frame, XCD-contiguous blocks, line write-back for fills of lines that fit
+// the Infinity Cache.  1M x 1500 B in 2 KiB rooms: verify 240-243 us, fill
+// 291-294 us against 278-281 / 363 us on the stream kernel's per-frame path;
+// 2 or 4 frames per group (descriptors, or descriptors and loads, together;
+// 92-140 VGPRs) and descriptors staged in LDS measured 257-340 / 301-388 us
+// (profiles/r05/c2_rooms_k.jsonl).
+template <bool COMPUTE>
+static hipError_t launch_rooms(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
+                               const uint16_t* len, u32 n, uint8_t* code, uint32_t* csums,
+                               u32 flags, hipStream_t s)
 {
-    static const int v = [] {
-        const char* e = std::getenv("GCS_ROOMS_K");
-        return e ? std::atoi(e) : 1;
-    }();
-    return v;
-}
-
-template <bool COMPUTE, int K>
-static hipError_t launch_rooms_lds(bool line, uint8_t* frames, uint64_t frames_bytes,
-                                   const uint64_t* off, const uint16_t* len, u32 n, uint8_t* code,
-                                   uint32_t* csums, u32 flags, hipStream_t s)
-{
-    constexpr int G = 32, U = 3, FB = kBlock / G * K;
-    const dim3 rg((n + FB - 1) / FB);
-    if constexpr (COMPUTE) {
-        if (line) {
-            hipLaunchKernelGGL((k_rooms_lds<G, U, COMPUTE, WM_LINE_SC1, K>), rg, dim3(kBlock), 0,
-                               s, frames, frames_bytes, off, len, n, code, csums, flags);
-            return hipGetLastError();
-        }
-    }
-    hipLaunchKernelGGL((k_rooms_lds<G, U, COMPUTE, kWM, K>), rg, dim3(kBlock), 0, s, frames,
-                       frames_bytes, off, len, n, code, csums, flags);
-    return hipGetLastError();
-}
-
-template <bool COMPUTE, int K, bool SEQ = false>
-static hipError_t launch_rooms(bool line, uint8_t* frames, uint64_t frames_bytes,
-                               const uint64_t* off, const uint16_t* len, u32 n, uint8_t* code,
-                               uint32_t* csums, u32 flags, hipStream_t s)
-{
-    constexpr int G = 32, U = 3, FPB = kBlock / G * K;
+    constexpr int G = 32, U = 3, FPB = kBlock / G;
     const dim3 rg((n + FPB - 1) / FPB);
     if constexpr (COMPUTE) {
-        if (line) {
-            hipLaunchKernelGGL((k_rooms<G, U, COMPUTE, WM_LINE_SC1, K, SEQ>), rg, dim3(kBlock), 0,
-                               s, frames, frames_bytes, off, len, n, code, csums, flags);
+        if ((uint64_t)n * 128 <= line_wb_bytes() && !(flags & GCS_CF_SECTOR_WB)) {
+            hipLaunchKernelGGL((k_desc<G, U, COMPUTE, kNT, WM_LINE_SC1, kXCD>), rg, dim3(kBlock),
+                               0, s, frames, frames_bytes, off, len, n, code, csums, flags);
             return hipGetLastError();
         }
     }
-    hipLaunchKernelGGL((k_rooms<G, U, COMPUTE, kWM, K, SEQ>), rg, dim3(kBlock), 0, s, frames,
+    hipLaunchKernelGGL((k_desc<G, U, COMPUTE, kNT, kWM, kXCD>), rg, dim3(kBlock), 0, s, frames,
                        frames_bytes, off, len, n, code, csums, flags);
     return hipGetLastError();
 }
@@ -2613,29 +2500,8 @@ static hipError_t launch_desc(uint8_t* frames, uint64_t frames_bytes, const uint
     if (n == 0)
         return hipSuccess;
     if (!ext_on && (flags & GCS_VF_ROOMS)) {
-        // frames one per room: one 32-lane group per frame, 3 chunks per lane
-        // and batch (k_fixed<32, 3>'s shape for MTU frames)
         static_assert(GCS_VF_ROOMS == GCS_CF_ROOMS, "one rooms bit");
-        const bool line = COMPUTE && (uint64_t)n * 128 <= line_wb_bytes() &&
-                          !(flags & GCS_CF_SECTOR_WB);
-        switch (rooms_k()) {
-        case 2: return launch_rooms<COMPUTE, 2>(line, frames, frames_bytes, off, len, n, code,
-                                                csums, flags, s);
-        case 4: return launch_rooms<COMPUTE, 4>(line, frames, frames_bytes, off, len, n, code,
-                                                csums, flags, s);
-        case 12: return launch_rooms<COMPUTE, 2, true>(line, frames, frames_bytes, off, len, n,
-                                                       code, csums, flags, s);
-        case 14: return launch_rooms<COMPUTE, 4, true>(line, frames, frames_bytes, off, len, n,
-                                                       code, csums, flags, s);
-        case 34: return launch_rooms_lds<COMPUTE, 4>(line, frames, frames_bytes, off, len, n,
-                                                     code, csums, flags, s);
-        case 316: return launch_rooms_lds<COMPUTE, 16>(line, frames, frames_bytes, off, len, n,
-                                                       code, csums, flags, s);
-        case 332: return launch_rooms_lds<COMPUTE, 32>(line, frames, frames_bytes, off, len, n,
-                                                       code, csums, flags, s);
-        default: return launch_rooms<COMPUTE, 1>(line, frames, frames_bytes, off, len, n, code,
-                                                 csums, flags, s);
-        }
+        return launch_rooms<COMPUTE>(frames, frames_bytes, off, len, n, code, csums, flags, s);
     }
     const dim3 grid((n + kDescFrames - 1) / kDescFrames);
     static_assert(kDescFrames == kBlock, "one descriptor per thread");

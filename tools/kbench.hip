@@ -1909,6 +1909,18 @@ int imix_main(uint64_t n, int rounds)
                            (u32)n, nullptr, nullptr, 0u);
     }});
     vs.back().prep = zero_prep;
+    // round 5: the staged sector's store policy again (the raw write-back of the
+    // C3 sectors alone: nt 67-79 us against sc1 107-113 us, r05c)
+#define STREAMWM(WM_, TAG)                                                                   \
+    vs.push_back({"compute stream 7 waves FRESH, sector " TAG, cb, [&](hipStream_t st) {     \
+        hipLaunchKernelGGL((k_desc_stream<StreamShape<8, 8192, 7, 4, 32, 2>, true, WM_, true>), \
+                           dim3((n + 255) / 256, 3), dim3(256), 0, st, tx, total, doff, dlen, \
+                           (u32)n, nullptr, nullptr, 0u);                                     \
+    }});                                                                                      \
+    vs.back().prep = zero_prep;
+    STREAMWM(WM_SECTOR_NT, "nt")
+    STREAMWM(WM_SECTOR, "plain")
+    STREAMWM(WM_SECTOR_SC01, "sc0 sc1")
     // the verify's shape against round 3's (7 waves, 12K-chunk regions)
     STREAM4(false, "U8 R12K occ8", 8, 12288, 8, WM_SECTOR_SC1, 3)
     STREAM4(false, "U8 R8K occ7", 8, 8192, 7, WM_SECTOR_SC1, 3)
