@@ -781,13 +781,14 @@ def plugin_threads():
     one thread per ring (64-frame IMIX fill + verify per iteration) at 1 / 8 /
     12 / 16 threads, and T threads each driving R rings with async posts
     (rings_TxR: up to 24 hot rings with only 4 CPUs busy, so the CPU quota
-    does not confound the GPU side).  `unprofiled`: the shipped grid, per call
-    and post -> done; `profiled`: the same under GCS_SERVER_PROF, with the
-    GPU serving time (gpu_span_us: first serving block saw the request -> last
-    one's records stored) and its per-block phases."""
+    does not confound the GPU side).  `shipped`: the grid as it ships, per call,
+    post -> done and, from its phase counters, the GPU serving time
+    (gpu_span_us: first serving block saw the request -> last one's records
+    stored) and its per-block phases; `plain`: the grid built without the
+    counters (GCS_SERVER_COUNTERS=0), for comparison."""
     import subprocess
     out = {}
-    for name, prof in (("unprofiled", "0"), ("profiled", "1")):
+    for name, prof in (("shipped", "1"), ("plain", "0")):
         env = dict(os.environ, SS_PROF=prof, SS_THREADS="1,8,12,16", SS_RINGS="4x2,4x4,4x6")
         try:
             r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "server_scaling.py")],

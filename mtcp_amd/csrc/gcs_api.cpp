@@ -365,6 +365,7 @@ class ServerHub {
     const uint64_t (*prof_sums(int r) const)[gcs::kProfWords] { return rq_->prof[r]; }
     bool dev_mailbox() const { return dev_mailbox_; }
     bool prof() const { return prof_; }
+    bool print() const { return print_; }
     double ticks_per_us() const { return ticks_per_us_; }
 
   private:
@@ -404,6 +405,8 @@ class ServerHub {
         // then be read from a stale L2 line); none = no acquire for frames in
         // device staging.  Default: agent scope for device frames, system
         // scope for host frames.
+        if (const char* ab = std::getenv("GCS_SERVER_AB"))     // temporary A/B bits
+            opts_ |= (uint32_t)std::strtoul(ab, nullptr, 0);
         const char* acq = std::getenv("GCS_SERVER_ACQUIRE");
         opts_ = !acq                         ? 0u
                 : std::strcmp(acq, "agent") == 0 ? gcs::kServerAcqAgent
@@ -420,7 +423,14 @@ class ServerHub {
         int khz = 0;
         HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
         ticks_per_us_ = khz > 0 ? khz / 1000.0 : 100.0;
-        prof_ = std::getenv("GCS_SERVER_PROF") != nullptr;   // process-wide
+        // The grid keeps its phase counters always (gcs_server_stats_get):
+        // the counting build served bursts 10-30 % faster than the plain one
+        // at 8-24 rings in every pairing measured, and as fast at 1 (DESIGN.md
+        // §5).  GCS_SERVER_COUNTERS=0 launches the plain build (an A/B knob);
+        // GCS_SERVER_PROF prints each ring's figures at exit.
+        const char* ctr = std::getenv("GCS_SERVER_COUNTERS");
+        prof_ = !(ctr && std::strcmp(ctr, "0") == 0);         // process-wide
+        print_ = std::getenv("GCS_SERVER_PROF") != nullptr;
         read_knobs();
         return GCS_OK;
     }
@@ -518,7 +528,7 @@ class ServerHub {
     uint64_t idle_ticks_ = 0, life_ticks_ = 0, hot_ticks_ = 0, hot_max_ticks_ = 0;
     uint32_t ring_of_[gcs::kHubRings] = {};
     uint32_t naps_ = 0;                   // cold naps | hot naps << 16
-    bool prof_ = false;
+    bool prof_ = true, print_ = false;
     double ticks_per_us_ = 100.0;
 };
 
@@ -529,7 +539,7 @@ class BurstServer {
   public:
     ~BurstServer()
     {
-        if (prof_n_) {
+        if (prof_n_ && hub_->print()) {
             gcs_server_stats st;
             stats(&st);
             std::fprintf(stderr,
@@ -728,7 +738,7 @@ class BurstServer {
         n_done_++;
         total_us_ += total;
         if (hub_->prof() && r.n) {
-            // GCS_SERVER_PROF: the request's GPU span, from the first serving
+            // phase counters: the request's GPU span, from the first serving
             // block's poll that saw it to the last one's records stored (GPU
             // wall clock).  A block writes its marks after its records, so
             // wait briefly for each serving block's tag; a block that has
@@ -787,7 +797,7 @@ class BurstServer {
 
   public:
     // gcs_server_stats_get: this ring's figures so far (GPU parts with
-    // GCS_SERVER_PROF only).
+    // the counting build only, the default).
     void stats(gcs_server_stats* st) const
     {
         std::memset(st, 0, sizeof *st);

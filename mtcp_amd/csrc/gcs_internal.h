@@ -95,7 +95,8 @@ struct alignas(64) ServerReq {
 struct alignas(64) ServerRes {
     uint64_t rec[kSlotFrames];
 };
-// GCS_SERVER_PROF (the k_burst_server<PROF> instantiation): per block,
+// Phase counters (the k_burst_server<PROF = true> build, the default; the
+// plain build with GCS_SERVER_COUNTERS=0): per block,
 // running sums over the requests it served (HubReqs::prof, next to the
 // request lines: in device memory they cost the PCIe link nothing), and the
 // marks of its last request (ServerMailbox::mark, host memory: the host waits
@@ -120,7 +121,7 @@ enum ServerProf {
 struct ServerMailbox {
     ServerLine ack[kServerBlocks];       // device: the last request each block served frames of
     ServerLine state[kServerBlocks];     // device: 1 serving, 2 exited (this launch's group)
-    // device, GCS_SERVER_PROF: ONE 16 B store per request {seen, rec, q, 0}
+    // device, counters: ONE 16 B store per request {seen, rec, q, 0}
     // (u32 each): the low 32 bits of the clock when the poll that saw request
     // q returned and when its records were stored (acknowledged) -- one
     // store, so no fence orders the marks before their tag
@@ -135,7 +136,7 @@ struct HubMailbox {
 struct HubReqs {
     ServerLine cmd;                      // host: 1 = leave now (the group leaders poll it)
     ServerReq req[kHubRings][kServerSlots];
-    uint64_t prof[kHubRings][kServerBlocks][kProfWords];   // device, GCS_SERVER_PROF sums
+    uint64_t prof[kHubRings][kServerBlocks][kProfWords];   // device: phase counter sums
 };
 
 // Device memory.  ent[r][q % kServerSlots] = q << 32 | n for each request q

@@ -236,7 +236,7 @@ k_desc(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __re
 // always drains.  All decisions are taken by wave 0 from the poll's lines
 // and broadcast through LDS (block-uniform control flow: no wave leaves the
 // loop while another waits at a barrier).
-// GCS_SERVER_PROF: the wall clock once every vector-memory access of this
+// Phase counters (PROF): the wall clock once every vector-memory access of this
 // wave issued so far has completed (loads returned, stores acknowledged).
 __device__ __forceinline__ uint64_t clock_after_vmem()
 {
@@ -273,7 +273,7 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
     // adaptive hot window: 3 x the gap between this block's last two
     // requests when that is <= hot_max_ticks, at least hot_ticks
     uint64_t win = hot_ticks, t_claim = t_start;
-    // GCS_SERVER_PROF (thread 0): this launch's additions to the block's sums
+    // PROF (thread 0): this launch's additions to the block's sums
     uint64_t p_issue = 0, p_seen = 0, p_rtt = 0, p_sum[kProfWords] = {};
     uint64_t* const psum = rq->prof[r][blk];
     uint64_t p_polls0 = 0, p_rtt0 = 0, p_slow2 = 0, p_slow5 = 0, p_maxrtt = 0, p_torn = 0;
@@ -341,6 +341,8 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
                 u32x4 v = {0, 0, 0, 0};
                 if (src)
                     v = *src;
+                if (!PROF && (opts & 0x2000u))      // A/B: the profiled poll's wait
+                    p_rtt += clock_after_vmem() - now;
                 if (PROF) {
                     const uint64_t back = clock_after_vmem();
                     p_issue = now;
@@ -519,6 +521,14 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
                 __hip_atomic_store(&rm->ack[blk].v, qend, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
                 acked = qend;
+            }
+            if (!PROF && mine && (opts & 0x1000u)) {   // A/B: the profiled block's stores
+                for (int k = 0; k < 13; k++)
+                    __hip_atomic_store(&psum[k], p_sum[k] + q, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+                const u32x4 mk = {q, q, q, 0u};
+                asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1"
+                             : : "v"(&rm->mark[blk][0]), "v"(mk) : "memory");
             }
             if (PROF && mine) {
                 const uint64_t t_rel = clock_after_vmem();

@@ -1,7 +1,7 @@
 """Burst-server scaling with the number of rings, phase by phase (tools/, not
 product).  One configuration per process (the hub reads GCS_SERVER_MAILBOX /
-GCS_SERVER_ACQUIRE once); GCS_SERVER_PROF is set here so every ring reports
-gcs_server_stats' GPU-side phases.
+GCS_SERVER_ACQUIRE / GCS_SERVER_COUNTERS once); every ring reports
+gcs_server_stats' GPU-side phases from the grid's counters.
 
 Two drivers (tests/plugin/mt_bursts.c):
   threads   one mTCP-like thread per ring, synchronous 64-frame IMIX fill +
@@ -15,10 +15,10 @@ import json
 import os
 import sys
 
-if os.environ.get("SS_PROF", "1") == "1":
-    os.environ.setdefault("GCS_SERVER_PROF", "1")
-else:
-    os.environ.pop("GCS_SERVER_PROF", None)   # the shipped grid: host-side figures only
+# SS_PROF=0: the plain grid without phase counters (GCS_SERVER_COUNTERS=0;
+# host-side figures only); default: the shipped grid, which keeps them
+if os.environ.get("SS_PROF", "1") == "0":
+    os.environ["GCS_SERVER_COUNTERS"] = "0"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from mtcp_amd import gpucsum  # noqa: E402
@@ -58,7 +58,7 @@ def cpu_quota():
 def main():
     os.environ["MT_CHECK_EVERY"] = os.environ.get("MT_CHECK_EVERY", "16")
     out = {"config": {k: os.environ.get(k, "default") for k in
-                      ("GCS_SERVER_MAILBOX", "GCS_SERVER_ACQUIRE", "GCS_SERVER_PROF",
+                      ("GCS_SERVER_MAILBOX", "GCS_SERVER_ACQUIRE", "GCS_SERVER_COUNTERS",
                        "GCS_DIRECT_STAGE", "GCS_SERVER_HOT_NAPS", "GCS_SERVER_HOT_US")},
            "cpus": cpu_quota(),
            "cpu_frac": "thread CPU time / wall time inside the calls (below 1: descheduled)"}
