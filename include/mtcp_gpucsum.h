@@ -196,6 +196,12 @@ typedef struct gcs_server_stats {
     double max_poll_us;       /* the longest poll round trip                          */
     double late_us[8];        /* mean per request: how long after the first serving
                                  block each of the ring's blocks saw it (block index) */
+    double seen_wait_us;      /* mean per request: how much longer than the ring's
+                                 fastest request it took from the post until the first
+                                 block saw it (host and GPU clocks compared)          */
+    double after_gpu_us;      /* mean per request: the fastest post -> seen, plus from
+                                 the last records stored until the host completed it;
+                                 post_to_done = seen_wait + gpu_span + after_gpu      */
 } gcs_server_stats;
 int gcs_server_stats_get(gcs_ctx *ctx, gcs_server_stats *out);
 

@@ -405,8 +405,6 @@ class ServerHub {
         // then be read from a stale L2 line); none = no acquire for frames in
         // device staging.  Default: agent scope for device frames, system
         // scope for host frames.
-        if (const char* ab = std::getenv("GCS_SERVER_AB"))     // temporary A/B bits
-            opts_ |= (uint32_t)std::strtoul(ab, nullptr, 0);
         const char* acq = std::getenv("GCS_SERVER_ACQUIRE");
         opts_ = !acq                         ? 0u
                 : std::strcmp(acq, "agent") == 0 ? gcs::kServerAcqAgent
@@ -743,11 +741,9 @@ class BurstServer {
             // wall clock).  A block writes its marks after its records, so
             // wait briefly for each serving block's tag; a block that has
             // already moved on to a later request is left out.
-            // (marks are the low 32 bits of the 100 MHz clock: differences
-            // within one request are taken modulo 2^32)
             bool first = true;
-            uint32_t seen = 0, seen_max = 0, rec = 0, serve = 0;
-            uint32_t seen_b[gcs::kServerBlocks] = {};
+            uint64_t seen = 0, seen_max = 0, rec = 0, serve = 0;
+            uint64_t seen_b[gcs::kServerBlocks] = {};
             bool have_b[gcs::kServerBlocks] = {};
             const auto tp = std::chrono::steady_clock::now();
             for (int k = 0; k < nb; k++) {
@@ -758,7 +754,7 @@ class BurstServer {
                 for (;;) {
                     asm volatile("" ::: "memory");   // the grid writes it: reload
                     _mm_store_si128(reinterpret_cast<__m128i*>(mk), _mm_load_si128(mp));
-                    d = (int32_t)(mk[2] - r.q);
+                    d = (int32_t)(mk[3] - r.q);
                     if (d >= 0 || std::chrono::steady_clock::now() - tp >
                                       std::chrono::microseconds(200))
                         break;
@@ -766,20 +762,20 @@ class BurstServer {
                 }
                 if (d != 0)
                     continue;
-                const uint32_t s0 = mk[0], r0 = mk[1];
+                const uint64_t s0 = (uint64_t)mk[0] | ((uint64_t)mk[1] << 32), r0 = s0 + mk[2];
                 if (first) {
                     seen = seen_max = s0;
                     rec = r0;
                     first = false;
                 }
-                if ((int32_t)(s0 - seen) < 0) seen = s0;
-                if ((int32_t)(s0 - seen_max) > 0) seen_max = s0;
-                if ((int32_t)(r0 - rec) > 0) rec = r0;
-                if ((int32_t)(r0 - s0) > (int32_t)serve) serve = r0 - s0;
+                seen = std::min(seen, s0);
+                seen_max = std::max(seen_max, s0);
+                rec = std::max(rec, r0);
+                serve = std::max<uint64_t>(serve, mk[2]);
                 seen_b[b] = s0;
                 have_b[b] = true;
             }
-            if (!first && (int32_t)(rec - seen) > 0) {
+            if (!first && rec > seen) {
                 const double tu = hub_->ticks_per_us();
                 prof_n_++;
                 prof_span_ += (double)(rec - seen) / tu;
@@ -787,9 +783,19 @@ class BurstServer {
                 prof_serve_ += (double)serve / tu;
                 for (int b = 0; b < gcs::kServerBlocks; b++)
                     if (have_b[b]) {
-                        late_[b] += (double)(int32_t)(seen_b[b] - seen) / tu;
+                        late_[b] += (double)(seen_b[b] - seen) / tu;
                         late_n_[b]++;
                     }
+                // host clock vs GPU clock: d1 = seen - post and d2 = done -
+                // rec each carry the clocks' unknown offset with opposite
+                // signs; the smallest d1 stands for the fastest post -> seen
+                const double post_us = std::chrono::duration<double, std::micro>(
+                                           r.t0.time_since_epoch()).count();
+                const double done_us = post_us + total;
+                const double d1 = seen / tu - post_us, d2 = done_us - rec / tu;
+                d1_sum_ += d1;
+                d2_sum_ += d2;
+                d1_min_ = prof_n_ == 1 ? d1 : std::min(d1_min_, d1);
             }
         }
         return GCS_OK;
@@ -806,6 +812,8 @@ class BurstServer {
         if (!hub_->prof())
             return;
         st->gpu_span_us = prof_n_ ? prof_span_ / prof_n_ : 0.0;
+        st->seen_wait_us = prof_n_ ? d1_sum_ / prof_n_ - d1_min_ : 0.0;
+        st->after_gpu_us = prof_n_ ? d2_sum_ / prof_n_ + d1_min_ : 0.0;
         st->seen_skew_us = prof_n_ ? prof_skew_ / prof_n_ : 0.0;
         st->block_serve_us = prof_n_ ? prof_serve_ / prof_n_ : 0.0;
         // the sums live beside the request lines (device memory by default:
@@ -852,6 +860,7 @@ class BurstServer {
     uint64_t n_done_ = 0, prof_n_ = 0;
     double total_us_ = 0, prof_span_ = 0, prof_skew_ = 0, prof_serve_ = 0, prof_write_ = 0;
     double late_[gcs::kServerBlocks] = {};
+    double d1_sum_ = 0, d2_sum_ = 0, d1_min_ = 0;
     uint64_t late_n_[gcs::kServerBlocks] = {};
 };
 

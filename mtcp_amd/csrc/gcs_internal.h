@@ -121,10 +121,10 @@ enum ServerProf {
 struct ServerMailbox {
     ServerLine ack[kServerBlocks];       // device: the last request each block served frames of
     ServerLine state[kServerBlocks];     // device: 1 serving, 2 exited (this launch's group)
-    // device, counters: ONE 16 B store per request {seen, rec, q, 0}
-    // (u32 each): the low 32 bits of the clock when the poll that saw request
-    // q returned and when its records were stored (acknowledged) -- one
-    // store, so no fence orders the marks before their tag
+    // device, counters: ONE 16 B store per request {seen lo, seen hi, rec -
+    // seen, q} (u32 each): the clock when the poll that saw request q
+    // returned, and how long after that its records were stored
+    // (acknowledged) -- one store, so no fence orders the marks before their tag
     uint64_t mark[kServerBlocks][2];
     ServerRes res[kServerSlots];
 };

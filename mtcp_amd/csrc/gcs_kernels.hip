@@ -341,8 +341,6 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
                 u32x4 v = {0, 0, 0, 0};
                 if (src)
                     v = *src;
-                if (!PROF && (opts & 0x2000u))      // A/B: the profiled poll's wait
-                    p_rtt += clock_after_vmem() - now;
                 if (PROF) {
                     const uint64_t back = clock_after_vmem();
                     p_issue = now;
@@ -473,9 +471,17 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
             const uint4 d0 = s_line[2 + grp];
             uint64_t* rec = rm->res[q % kServerSlots].rec;
             mine = first < n;                            // block-uniform: frames of q here
-            for (uint32_t i = first + grp, pass = 0; i < n; i += kPass, pass++) {
+            // the block's frames of q in passes of FPB (one per group); each
+            // pass's records leave as ONE 64 B line (four lanes x 16 B), not
+            // as eight 8 B writes: every partial-line write to host memory is
+            // a fabric write of its own, and at 8-16 rings the records' way
+            // back grew from 1.6 to 10-24 us
+            const uint32_t npass = mine ? (n - first + kPass - 1) / kPass : 0;   // block-uniform
+            for (uint32_t pass = 0; pass < npass; pass++) {
+                const uint32_t base = first + pass * kPass, i = base + grp;
+                const bool here = i < n;                 // group-uniform
                 uint4 d = d0;
-                if (pass != 0) {
+                if (pass != 0 && here) {
                     const u32x4 w = *reinterpret_cast<const volatile u32x4*>(&sl->desc[i]);
                     d = make_uint4(w.x, w.y, w.z, w.w);
                 }
@@ -484,18 +490,32 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
                 const bool ok = (o & 15) == 0 && o <= bytes && len <= bytes - o;
                 uint8_t* f = frames + (ok ? o : 0);
                 const int64_t avail = ok ? (int64_t)(bytes - o) : 0;
-                s_csum[grp] = 0;
+                if (sub == 0)
+                    s_csum[grp] = 0;
                 if (compute)
                     do_frame<G, U, true, true, true, kNT, kWM>(f, len, avail, ok, sub, flags,
-                                                               s_code + grp, s_csum + grp);
+                                                               s_code + grp, s_csum + grp, here);
                 else
                     do_frame<G, U, false, true, true, kNT, kWM>(f, len, avail, ok, sub, flags,
-                                                                s_code + grp, nullptr);
-                if (sub == 0) {                  // the group's results, in one 8 B store
-                    const uint64_t rv = (uint64_t)s_csum[grp] | ((uint64_t)s_code[grp] << 32) |
-                                        ((uint64_t)(q & 0xFFFFu) << 48);
-                    __hip_atomic_store(&rec[i], rv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                                                                s_code + grp, nullptr, here);
+                __syncthreads();                         // the pass's results in LDS
+                if (t < FPB / 2) {
+                    const uint32_t j = base + 2 * t;
+                    const uint64_t tag = (uint64_t)(q & 0xFFFFu) << 48;
+                    const uint64_t r0 = (uint64_t)s_csum[2 * t] |
+                                        ((uint64_t)s_code[2 * t] << 32) | tag;
+                    const uint64_t r1 = (uint64_t)s_csum[2 * t + 1] |
+                                        ((uint64_t)s_code[2 * t + 1] << 32) | tag;
+                    if (j + 1 < n) {
+                        const u32x4 w = {(u32)r0, (u32)(r0 >> 32), (u32)r1, (u32)(r1 >> 32)};
+                        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1"
+                                     : : "v"(&rec[j]), "v"(w) : "memory");
+                    } else if (j < n) {
+                        __hip_atomic_store(&rec[j], r0, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
                 }
+                __syncthreads();                         // s_code / s_csum free again
             }
             if (PROF && mine) {
                 __syncthreads();
@@ -522,14 +542,6 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
                                    __HIP_MEMORY_SCOPE_SYSTEM);
                 acked = qend;
             }
-            if (!PROF && mine && (opts & 0x1000u)) {   // A/B: the profiled block's stores
-                for (int k = 0; k < 13; k++)
-                    __hip_atomic_store(&psum[k], p_sum[k] + q, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_SYSTEM);
-                const u32x4 mk = {q, q, q, 0u};
-                asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1"
-                             : : "v"(&rm->mark[blk][0]), "v"(mk) : "memory");
-            }
             if (PROF && mine) {
                 const uint64_t t_rel = clock_after_vmem();
                 p_sum[kProfN] += 1;
@@ -551,7 +563,7 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
                 for (int k = 0; k < kProfWords; k++)
                     __hip_atomic_store(&psum[k], p_sum[k], __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_SYSTEM);
-                const u32x4 mk = {(u32)p_seen, (u32)t_rec, q, 0u};
+                const u32x4 mk = {(u32)p_seen, (u32)(p_seen >> 32), (u32)(t_rec - p_seen), q};
                 asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1"
                              : : "v"(&rm->mark[blk][0]), "v"(mk) : "memory");
             }

@@ -32,8 +32,9 @@ struct job {
  * poll us, [5] acquire us, [6] frames us, [7] records us, [8] release us,
  * [9] polls per block request, [10] seen skew us, [11] slowest block us,
  * [12] cold fraction, [13] polls over 2 us, [14] over 5 us, [15] torn polls,
- * [16] longest poll us, [17..24] mean lateness of blocks 0..7 us. */
-#define NSST 25
+ * [16] longest poll us, [17..24] mean lateness of blocks 0..7 us, [25] wait
+ * before the GPU saw a request (over the fastest) us, [26] after the GPU us. */
+#define NSST 27
 static double g_sst[NSST];
 int mt_last_server_stats(double *out, int n)
 {
@@ -56,6 +57,8 @@ static void sst_add(gcs_server_stats *acc, const gcs_server_stats *s)
 		acc->block_serve_us = (acc->block_serve_us * w0 + s->block_serve_us * w1) / (w0 + w1);
 		for (int b = 0; b < 8; b++)
 			acc->late_us[b] = (acc->late_us[b] * w0 + s->late_us[b] * w1) / (w0 + w1);
+		acc->seen_wait_us = (acc->seen_wait_us * w0 + s->seen_wait_us * w1) / (w0 + w1);
+		acc->after_gpu_us = (acc->after_gpu_us * w0 + s->after_gpu_us * w1) / (w0 + w1);
 	}
 	if (b0 + b1 > 0) {
 		acc->seen_poll_us = (acc->seen_poll_us * b0 + s->seen_poll_us * b1) / (b0 + b1);
@@ -103,6 +106,8 @@ static void sst_publish(struct job *jobs, int threads)
 	g_sst[16] = acc.max_poll_us;
 	for (t = 0; t < 8; t++)
 		g_sst[17 + t] = acc.late_us[t];
+	g_sst[25] = acc.seen_wait_us;
+	g_sst[26] = acc.after_gpu_us;
 }
 
 /* Thread CPU time inside the gcs calls over wall time inside them, averaged

@@ -34,7 +34,7 @@ M.mt_last_server_stats.argtypes = [C.POINTER(C.c_double), C.c_int]
 KEYS = ["requests", "post_to_done_us", "gpu_span_us", "poll_us", "seen_poll_us", "acquire_us",
         "frames_us", "records_us", "release_us", "polls_per_block_request", "seen_skew_us",
         "block_serve_us", "cold_frac", "slow_polls_2us", "slow_polls_5us", "torn_polls",
-        "max_poll_us"] + [f"late_us_b{b}" for b in range(8)]
+        "max_poll_us"] + [f"late_us_b{b}" for b in range(8)] + ["seen_wait_us", "after_gpu_us"]
 
 
 def server_stats():
