@@ -781,14 +781,15 @@ def plugin_threads():
     one thread per ring (64-frame IMIX fill + verify per iteration) at 1 / 8 /
     12 / 16 threads, and T threads each driving R rings with async posts
     (rings_TxR: up to 24 hot rings with only 4 CPUs busy, so the CPU quota
-    does not confound the GPU side).  `shipped`: the grid as it ships, per call,
-    post -> done and, from its phase counters, the GPU serving time
-    (gpu_span_us: first serving block saw the request -> last one's records
-    stored) and its per-block phases; `plain`: the grid built without the
-    counters (GCS_SERVER_COUNTERS=0), for comparison."""
+    does not confound the GPU side).  `shipped`: the grid as it ships, per call
+    and post -> done; `counters`: the build with phase counters
+    (GCS_SERVER_COUNTERS=1), which adds the GPU serving time (gpu_span_us:
+    first serving block saw the request -> last one's records stored), its
+    per-block phases, and post -> done split into the wait before the GPU saw
+    the request, that span, and the way back."""
     import subprocess
     out = {}
-    for name, prof in (("shipped", "1"), ("plain", "0")):
+    for name, prof in (("shipped", "0"), ("counters", "1")):
         env = dict(os.environ, SS_PROF=prof, SS_THREADS="1,8,12,16", SS_RINGS="4x2,4x4,4x6")
         try:
             r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "server_scaling.py")],

@@ -166,11 +166,11 @@ int gcs_sync(gcs_ctx *ctx);                               /* wait for ctx stream
 int gcs_ctx_set_burst_server(gcs_ctx *ctx, int on);
 
 /* The burst server's figures for this context's ring since it was turned on
- * (like mTCP's per-thread NETSTAT, core.c:189-218): requests, post -> done, and
- * the GPU side from the grid's phase counters (always kept; 0 when the
- * process ran with GCS_SERVER_COUNTERS=0).  Per-block figures are means over
- * the (block, request) pairs that served frames.  GCS_SERVER_PROF prints them
- * at exit.  GCS_EINVAL without the server. */
+ * (like mTCP's per-thread NETSTAT, core.c:189-218): requests and post -> done
+ * always; the GPU side only when the process ran with GCS_SERVER_COUNTERS=1 or
+ * GCS_SERVER_PROF (the grid build with phase counters), else 0.  Per-block
+ * figures are means over the (block, request) pairs that served frames.
+ * GCS_SERVER_PROF also prints them at exit.  GCS_EINVAL without the server. */
 typedef struct gcs_server_stats {
     uint64_t requests;        /* requests completed on this ring                      */
     uint64_t block_requests;  /* (block, request) pairs that served frames            */

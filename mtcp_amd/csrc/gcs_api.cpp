@@ -421,14 +421,14 @@ class ServerHub {
         int khz = 0;
         HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
         ticks_per_us_ = khz > 0 ? khz / 1000.0 : 100.0;
-        // The grid keeps its phase counters always (gcs_server_stats_get):
-        // the counting build served bursts 10-30 % faster than the plain one
-        // at 8-24 rings in every pairing measured, and as fast at 1 (DESIGN.md
-        // §5).  GCS_SERVER_COUNTERS=0 launches the plain build (an A/B knob);
-        // GCS_SERVER_PROF prints each ring's figures at exit.
+        // GCS_SERVER_COUNTERS=1 (or GCS_SERVER_PROF): the grid build with
+        // per-block phase counters (a clock read and a wait per phase,
+        // gcs_server_stats_get's GPU figures), 1-3 us slower per burst than the
+        // plain build.  GCS_SERVER_PROF also prints each ring's
+        // figures at exit.  Process-wide.
         const char* ctr = std::getenv("GCS_SERVER_COUNTERS");
-        prof_ = !(ctr && std::strcmp(ctr, "0") == 0);         // process-wide
         print_ = std::getenv("GCS_SERVER_PROF") != nullptr;
+        prof_ = (ctr && std::strcmp(ctr, "0") != 0) || print_;
         read_knobs();
         return GCS_OK;
     }
@@ -526,7 +526,7 @@ class ServerHub {
     uint64_t idle_ticks_ = 0, life_ticks_ = 0, hot_ticks_ = 0, hot_max_ticks_ = 0;
     uint32_t ring_of_[gcs::kHubRings] = {};
     uint32_t naps_ = 0;                   // cold naps | hot naps << 16
-    bool prof_ = true, print_ = false;
+    bool prof_ = false, print_ = false;
     double ticks_per_us_ = 100.0;
 };
 
@@ -803,7 +803,7 @@ class BurstServer {
 
   public:
     // gcs_server_stats_get: this ring's figures so far (GPU parts with
-    // the counting build only, the default).
+    // the counting build only, GCS_SERVER_COUNTERS).
     void stats(gcs_server_stats* st) const
     {
         std::memset(st, 0, sizeof *st);

@@ -95,8 +95,8 @@ struct alignas(64) ServerReq {
 struct alignas(64) ServerRes {
     uint64_t rec[kSlotFrames];
 };
-// Phase counters (the k_burst_server<PROF = true> build, the default; the
-// plain build with GCS_SERVER_COUNTERS=0): per block,
+// Phase counters (the k_burst_server<PROF = true> build, GCS_SERVER_COUNTERS=1
+// or GCS_SERVER_PROF; the plain build by default): per block,
 // running sums over the requests it served (HubReqs::prof, next to the
 // request lines: in device memory they cost the PCIe link nothing), and the
 // marks of its last request (ServerMailbox::mark, host memory: the host waits

@@ -15,10 +15,9 @@ import json
 import os
 import sys
 
-# SS_PROF=0: the plain grid without phase counters (GCS_SERVER_COUNTERS=0;
-# host-side figures only); default: the shipped grid, which keeps them
-if os.environ.get("SS_PROF", "1") == "0":
-    os.environ["GCS_SERVER_COUNTERS"] = "0"
+# SS_PROF=1: the grid build with phase counters (GPU serving time and its
+# phases); 0: the shipped plain build (host-side figures only)
+os.environ["GCS_SERVER_COUNTERS"] = "1" if os.environ.get("SS_PROF", "1") == "1" else "0"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from mtcp_amd import gpucsum  # noqa: E402
