@@ -501,6 +501,15 @@ def c2_rooms(ctx, torch, n=1 << 20, L=1500, room=2048):
             / HBM_PEAK_GBS
         out[f"{name}_compute_frac_peak"] = n * (L + 4) / (out[f"{name}_compute_ms"] * 1e-3) \
             / 1e9 / HBM_PEAK_GBS
+    # the fixed-stride kernels over the same rooms (stride = room): what the
+    # layout itself costs, without descriptors
+    ctx.compute_fixed(buf, room, L, n, stream=stream)
+    out["fixed_stride_verify_ms"] = _launch_ms(
+        torch, lambda: ctx.verify_fixed(buf, room, L, n, v, stream=stream))
+    assert int((v != 0).sum()) == 0
+    out["fixed_stride_compute_ms"] = _launch_ms_fresh(
+        torch, lambda: ctx.compute_fixed(buf, room, L, n, st, stream=stream), zero_checks)
+    assert int((st != 0).sum()) == 0
     del buf
     return out
 

@@ -2602,12 +2602,29 @@ int lro_main(uint64_t n, int rounds)
                            in, n * stride, off, lens, vd, (u32)n, 64u, 16384u, out,         \
                            n * stride, oo, ol, hd);                                         \
     }});
-    GROPIPE(2, 5, 5) GROPIPE(3, 5, 5) GROPIPE(4, 5, 5) GROPIPE(3, 5, 4) GROPIPE(3, 5, 10)
+    if (std::getenv("KB_PIPE")) {
+        GROPIPE(2, 5, 5) GROPIPE(3, 5, 5) GROPIPE(4, 5, 5) GROPIPE(3, 5, 4) GROPIPE(3, 5, 10)
+    }
     vs.push_back({"k_gro<2,64,8,FLAT> ACX nt PF8 (shipped r03)", bytes, [&](hipStream_t st) {
         hipLaunchKernelGGL((k_gro<2, 64, 8, true, WM_SECTOR_NT, true, 8>), dim3((n + 63) / 64),
                            dim3(256), 0, st, in, n * stride, off, lens, vd, (u32)n, 64u, 16384u,
                            out, n * stride, oo, ol, hd);
     }});
+    // round 5 diagnostic: descriptors synthesized, not loaded (the descriptor
+    // trip's cost; same output on this batch)
+    vs.push_back({"k_gro ... DIAG 1 (no descriptor loads)", bytes, [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_gro<2, 64, 8, true, WM_SECTOR_NT, true, 8, 1>), dim3((n + 63) / 64),
+                           dim3(256), 0, st, in, n * stride, off, lens, vd, (u32)n, 64u, 16384u,
+                           out, n * stride, oo, ol, hd);
+    }});
+#define GRONXP(NX_)                                                                          \
+    vs.push_back({"k_gro ... NXP " #NX_ " (next windows' trips prefetched)", bytes,            \
+                  [&](hipStream_t st) {                                                      \
+        hipLaunchKernelGGL((k_gro<2, 64, 8, true, WM_SECTOR_NT, true, 8, 0, NX_>),             \
+                           dim3((n + 63) / 64), dim3(256), 0, st, in, n * stride, off, lens, vd, \
+                           (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd);                \
+    }});
+    GRONXP(512) GRONXP(1024) GRONXP(2048)
     // (round 3's k_gro PROBE = 1, phases A-C + D1 alone: 69-91 us for this batch,
     // profiles/r03/kbench_lro_*.log; the knob left the product kernel in round 4)
     // the same frames in 2 KiB rooms (sparse descriptors: no block streams)
@@ -2623,6 +2640,25 @@ int lro_main(uint64_t n, int rounds)
         for (uint64_t i = 0; i < n; i++) h[i] = i * sstride;
         CK(hipMemcpy(sp_off, h.data(), 8 * n, hipMemcpyHostToDevice));
     }
+    // round 5: the rooms kernel (launch_rooms' k_desc<32,3> XCD) with the next
+    // generation's descriptors prefetched DPF logical blocks ahead
+#define ROOMS(DPF_)                                                                          \
+    vs.push_back({"rooms verify k_desc<32,3> XCD DPF " #DPF_, (double)n * (L + 1),           \
+                  [&](hipStream_t st) {                                                      \
+        hipLaunchKernelGGL((k_desc<32, 3, false, kNT, kWM, kXCD, DPF_>), dim3((n + 7) / 8),   \
+                           dim3(256), 0, st, sp, n * sstride, sp_off, lens, (u32)n, vd2,      \
+                           nullptr, 0u);                                                     \
+    }});                                                                                     \
+    vs.push_back({"rooms fill k_desc<32,3> XCD line DPF " #DPF_, (double)n * (L + 4),         \
+                  [&](hipStream_t st) {                                                      \
+        hipLaunchKernelGGL((k_desc<32, 3, true, kNT, WM_LINE_SC1, kXCD, DPF_>),               \
+                           dim3((n + 7) / 8), dim3(256), 0, st, sp, n * sstride, sp_off, lens, \
+                           (u32)n, nullptr, nullptr, 0u);                                    \
+    }});
+    ROOMS(0) ROOMS(224) ROOMS(448) ROOMS(896)
+    vs.push_back({"fixed stride 2048 verify (same rooms)", (double)n * (L + 1), [&](hipStream_t st) {
+        CK(launch_verify_fixed(sp, sstride, L, (u32)n, vd2, 0u, st));
+    }});
     vs.push_back({"verify sparse 2 KiB rooms (launch_verify_desc: 7 waves, 32x3)", (double)n * (L + 1),
                   [&](hipStream_t st) {
         CK(launch_verify_desc(sp, n * sstride, sp_off, lens, (u32)n, vd, 0u, st));
