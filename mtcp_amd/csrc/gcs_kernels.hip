@@ -198,10 +198,7 @@ k_small_x(uint8_t* __restrict__ frames, uint64_t stride, u32 frame_len, u32 n,
 // (GCS_VF_ROOMS / GCS_CF_ROOMS: frames one per mbuf room, which the packed
 // stream cannot stream; XCD-contiguous blocks, and for a fill of lines that
 // fit the Infinity Cache the whole-line write-back of k_fixed).
-// DPF > 0: lanes 0..FPB-1 also read the descriptors of logical block blk + DPF
-// (the same XCD's range, about one generation of resident blocks later) with
-// the cached policy, so that block's descriptor trip hits L2.
-template <int G, int U, bool COMPUTE, bool NT, int WM, bool XCD = false, int DPF = 0>
+template <int G, int U, bool COMPUTE, bool NT, int WM, bool XCD = false>
 __global__ void __launch_bounds__(kBlock)
 k_desc(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __restrict__ off,
        const uint16_t* __restrict__ lens, u32 n, uint8_t* __restrict__ out_code,
@@ -215,22 +212,12 @@ k_desc(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __re
         return;
     const uint64_t o = off[i];
     const u32 len = lens[i];
-    u32 pfx = 0;
-    if constexpr (DPF > 0) {
-        const uint64_t j = ((uint64_t)blk + DPF) * FPB + threadIdx.x;
-        if (threadIdx.x < FPB && j < n)
-            pfx = (u32)off[j] ^ (u32)lens[j];
-    }
     const bool ok = (o & 15) == 0 && o <= frames_bytes && len <= frames_bytes - o;
     uint8_t* f = frames + (ok ? o : 0);
     do_frame<G, U, COMPUTE, true, true, NT, WM>(f, len, ok ? (int64_t)(frames_bytes - o) : 0,
                                                 ok, sub, flags,
                                                 out_code ? out_code + i : nullptr,
                                                 out_csum ? out_csum + i : nullptr);
-    if constexpr (DPF > 0) {
-        if (pfx == 0x9E3779B9u && len == 0xFFFFu && out_csum)   // never: keeps the loads
-            out_csum[i] = pfx;
-    }
 }
 
 // Burst server: a grid of kServerBlocks blocks per ring in use that stays
@@ -992,7 +979,10 @@ desc_fallback_block(uint8_t* __restrict__ frames, uint64_t frames_bytes,
     }
 }
 
-template <class T, bool COMPUTE, int WM, bool XCD>
+// DPF > 0: after its stream, each block reads the descriptors of logical block
+// blk + DPF (the same XCD's range, blocks that start about then) with the
+// cached policy, so that their phase-0 trip hits L2.
+template <class T, bool COMPUTE, int WM, bool XCD, int DPF = 0>
 __global__ void __launch_bounds__(kBlock, T::OCC)
 k_desc_stream(uint8_t* __restrict__ frames, uint64_t frames_bytes,
               const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens, u32 n,
@@ -1148,6 +1138,12 @@ k_desc_stream(uint8_t* __restrict__ frames, uint64_t frames_bytes,
         if (lane == 0)
             wtot[w] = run;
     }
+    u32 pfx = 0;
+    if constexpr (DPF > 0) {
+        const uint64_t j = ((uint64_t)blk + DPF) * F + t;
+        if (pass == 0 && j < n)
+            pfx = (u32)off[j] ^ (u32)lens[j];
+    }
     __syncthreads();
 
     // phase 3: one lane per frame of the pass
@@ -1235,6 +1231,10 @@ k_desc_stream(uint8_t* __restrict__ frames, uint64_t frames_bytes,
         desc_fallback_block<T::FG, T::FU, COMPUTE>(frames, frames_bytes, off, lens, f0 + p1,
                                                    fb_hi - p1, out_code, out_csum, flags,
                                                    codes + p1);
+    }
+    if constexpr (DPF > 0) {
+        if (pfx == 0x9E3779B9u && nf == 1 && f0 == (uint64_t)-1)
+            out_code[0] = 0;               // never: keeps the loads
     }
 }
 
@@ -1626,8 +1626,8 @@ enum { SEG_HDR = 0, SEG_PAY = 1, SEG_WHOLE = 2 };
 // DIAG (tools/kbench.hip only; 0 in the library): 1 = the descriptors are not
 // loaded but synthesized as kbench's LRO batch lays them out (1500 B frames at a
 // 1536 B stride, all accepted) -- the cost of the descriptor trip.
-// NXP > 0 (A/B): wave 3 first reads window blockIdx + NXP's descriptors and
-// header lines with the cached policy (that window's phase A trips then hit
+// NXP > 0: wave 3 (FLAT; else thread t, frame t) first reads window
+// blockIdx + NXP's descriptors and header lines with the cached policy (that window's phase A trips then hit
 // the caches, if they keep them until it starts).
 template <int U, int W = kGroW, int OCC = 1, bool FLAT = false, int FWM = WM_SECTOR,
           bool ACX = false, int PF = 0, int DIAG = 0, int NXP = 0>
@@ -1683,12 +1683,13 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
     // read the window's input region meanwhile with cached loads, so that D2's
     // payload loads find it in L2 / the Infinity Cache.
     if constexpr (NXP > 0) {
-        const uint64_t j = ((uint64_t)blockIdx.x + NXP) * window + (t - 192);
-        if (t >= 192 && t - 192 < (int)window && j < n) {
+        constexpr int T0 = FLAT ? 192 : 0;             // FLAT: wave 3 (idle until D)
+        const uint64_t j = ((uint64_t)blockIdx.x + NXP) * window + (t - T0);
+        if (t >= T0 && t - T0 < (int)window && j < n) {
             const uint64_t o = off[j];
             const u32 L = lens[j];
             u32 x = L ^ verdict[j];
-            if ((o & 15) == 0 && o + 96 <= in_bytes) {
+            if ((o & 15) == 0 && o <= in_bytes && in_bytes - o >= 96) {
                 const uint4 a = ldg16<false>(in + o), b = ldg16<false>(in + o + 80);
                 x ^= a.x ^ b.w;
             }
@@ -2684,8 +2685,14 @@ hipError_t launch_gro(const uint8_t* in, uint64_t in_bytes, const uint64_t* off,
     // while waves 1-3 stream this one, measured 770-805 us against 650:
     // three streaming waves per block at 5 blocks per CU, 15 per CU, against
     // 32 here -- tools/gro_pipe.hip, kbench lro)
+    // (round 5: phase A's two dependent trips, descriptors then headers, cost
+    // ~25 us: synthesized descriptors 650-655 vs 678-682 us.  NXP = 2048: wave
+    // 3 reads the descriptors and header lines of the window 2048 blocks on,
+    // about one generation of resident blocks later, so that its trips hit the
+    // caches: 653-658 us, the same box; windows of 256 gain nothing from it,
+    // 864 vs 871-876 us -- profiles/r05/kbench_lro_nxp*.log)
     if (window <= 64)
-        hipLaunchKernelGGL((k_gro<2, 64, 8, true, WM_SECTOR_NT, true, 8>),
+        hipLaunchKernelGGL((k_gro<2, 64, 8, true, WM_SECTOR_NT, true, 8, 0, 2048>),
                            dim3((n + window - 1) / window), dim3(kBlock), 0, s, in, in_bytes, off,
                            len, verdict, n, window, max_len, out, out_bytes, out_off, out_len,
                            head);

@@ -6,6 +6,7 @@
 //   tools/kbench [frame_len=1500] [n=1048576] [rounds=15]
 #include "../mtcp_amd/csrc/gcs_kernels.hip"
 #include "attic/gro_pipe.hip"   // measured, not shipped
+#include "attic/rooms_loop.hip" // measured, not shipped
 
 #include <algorithm>
 #include <cstdio>
@@ -1921,6 +1922,23 @@ int imix_main(uint64_t n, int rounds)
     STREAMWM(WM_SECTOR_NT, "nt")
     STREAMWM(WM_SECTOR, "plain")
     STREAMWM(WM_SECTOR_SC01, "sc0 sc1")
+    // round 5: the next generation's descriptors read after the stream (DPF
+    // logical blocks on, the same XCD)
+#define STREAMDPF(DPF_)                                                                        \
+    vs.push_back({"verify  stream shipped DPF " #DPF_, vb, [&](hipStream_t st) {                \
+        hipLaunchKernelGGL((k_desc_stream<StreamShape<8, 8192, 7, 3, 32, 3>, false, WM_SECTOR_SC1, \
+                                          true, DPF_>),                                          \
+                           dim3((n + 255) / 256, 3), dim3(256), 0, st, rx, total, doff, dlen,   \
+                           (u32)n, v1, nullptr, 0u);                                            \
+    }});                                                                                        \
+    vs.push_back({"compute stream shipped DPF " #DPF_ " FRESH", cb, [&](hipStream_t st) {        \
+        hipLaunchKernelGGL((k_desc_stream<StreamShape<8, 8192, 7, 4, 32, 2>, true, WM_SECTOR_SC1, \
+                                          true, DPF_>),                                          \
+                           dim3((n + 255) / 256, 3), dim3(256), 0, st, tx, total, doff, dlen,   \
+                           (u32)n, nullptr, nullptr, 0u);                                       \
+    }});                                                                                        \
+    vs.back().prep = zero_prep;
+    STREAMDPF(128) STREAMDPF(256) STREAMDPF(512)
     // the verify's shape against round 3's (7 waves, 12K-chunk regions)
     STREAM4(false, "U8 R12K occ8", 8, 12288, 8, WM_SECTOR_SC1, 3)
     STREAM4(false, "U8 R8K occ7", 8, 8192, 7, WM_SECTOR_SC1, 3)
@@ -2625,6 +2643,25 @@ int lro_main(uint64_t n, int rounds)
                            (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd);                \
     }});
     GRONXP(512) GRONXP(1024) GRONXP(2048)
+    vs.push_back({"k_gro ... NXP 1024 PF 4", bytes, [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_gro<2, 64, 8, true, WM_SECTOR_NT, true, 4, 0, 1024>),
+                           dim3((n + 63) / 64), dim3(256), 0, st, in, n * stride, off, lens, vd,
+                           (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd);
+    }});
+    vs.push_back({"k_gro ... NXP 1024 PF 16", bytes, [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_gro<2, 64, 8, true, WM_SECTOR_NT, true, 16, 0, 1024>),
+                           dim3((n + 63) / 64), dim3(256), 0, st, in, n * stride, off, lens, vd,
+                           (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd);
+    }});
+    // windows of 256 (run-per-wave k_gro<2, 256>; not compared with launch_gro's
+    // 64-frame windows)
+#define GRO256(NX_)                                                                          \
+    vs.push_back({"w256 k_gro<2,256> NXP " #NX_, bytes, [&](hipStream_t st) {                 \
+        hipLaunchKernelGGL((k_gro<2, 256, 1, false, WM_SECTOR, false, 0, 0, NX_>),             \
+                           dim3((n + 255) / 256), dim3(256), 0, st, in, n * stride, off, lens, vd, \
+                           (u32)n, 256u, 16384u, out, n * stride, oo, ol, hd);               \
+    }});
+    GRO256(0) GRO256(256) GRO256(512) GRO256(1024)
     // (round 3's k_gro PROBE = 1, phases A-C + D1 alone: 69-91 us for this batch,
     // profiles/r03/kbench_lro_*.log; the knob left the product kernel in round 4)
     // the same frames in 2 KiB rooms (sparse descriptors: no block streams)
@@ -2642,20 +2679,34 @@ int lro_main(uint64_t n, int rounds)
     }
     // round 5: the rooms kernel (launch_rooms' k_desc<32,3> XCD) with the next
     // generation's descriptors prefetched DPF logical blocks ahead
-#define ROOMS(DPF_)                                                                          \
-    vs.push_back({"rooms verify k_desc<32,3> XCD DPF " #DPF_, (double)n * (L + 1),           \
-                  [&](hipStream_t st) {                                                      \
-        hipLaunchKernelGGL((k_desc<32, 3, false, kNT, kWM, kXCD, DPF_>), dim3((n + 7) / 8),   \
-                           dim3(256), 0, st, sp, n * sstride, sp_off, lens, (u32)n, vd2,      \
-                           nullptr, 0u);                                                     \
-    }});                                                                                     \
-    vs.push_back({"rooms fill k_desc<32,3> XCD line DPF " #DPF_, (double)n * (L + 4),         \
-                  [&](hipStream_t st) {                                                      \
-        hipLaunchKernelGGL((k_desc<32, 3, true, kNT, WM_LINE_SC1, kXCD, DPF_>),               \
-                           dim3((n + 7) / 8), dim3(256), 0, st, sp, n * sstride, sp_off, lens, \
-                           (u32)n, nullptr, nullptr, 0u);                                    \
+    // (k_desc with the descriptors of the block DPF = 224-896 logical blocks on
+    // read ahead: verify 280-283 vs 243-245 us, fill unchanged -- a short-lived
+    // wave holds its slot until its prefetch returns; kbench_lro_nxp1.log)
+    vs.push_back({"rooms verify k_desc<32,3> XCD (shipped)", (double)n * (L + 1), [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_desc<32, 3, false, kNT, kWM, kXCD>), dim3((n + 7) / 8), dim3(256), 0,
+                           st, sp, n * sstride, sp_off, lens, (u32)n, vd2, nullptr, 0u);
     }});
-    ROOMS(0) ROOMS(224) ROOMS(448) ROOMS(896)
+    vs.push_back({"rooms fill k_desc<32,3> XCD line (shipped)", (double)n * (L + 4), [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_desc<32, 3, true, kNT, WM_LINE_SC1, kXCD>), dim3((n + 7) / 8),
+                           dim3(256), 0, st, sp, n * sstride, sp_off, lens, (u32)n, nullptr,
+                           nullptr, 0u);
+    }});
+    // round 5: k_rooms, a grid of BPC_ blocks per CU walking the frames, the
+    // next descriptor loaded one frame ahead
+#define ROOMSL(BPC_)                                                                         \
+    vs.push_back({"rooms verify k_rooms " #BPC_ " blocks/CU", (double)n * (L + 1),             \
+                  [&](hipStream_t st) {                                                      \
+        const u32 g = (u32)std::min<uint64_t>((n + 7) / 8, (uint64_t)BPC_ * cus);             \
+        hipLaunchKernelGGL((k_rooms<32, 3, false, kNT, kWM>), dim3(g), dim3(256), 0, st, sp,   \
+                           n * sstride, sp_off, lens, (u32)n, vd2, nullptr, 0u);              \
+    }});                                                                                     \
+    vs.push_back({"rooms fill k_rooms line " #BPC_ " blocks/CU", (double)n * (L + 4),         \
+                  [&](hipStream_t st) {                                                      \
+        const u32 g = (u32)std::min<uint64_t>((n + 7) / 8, (uint64_t)BPC_ * cus);             \
+        hipLaunchKernelGGL((k_rooms<32, 3, true, kNT, WM_LINE_SC1>), dim3(g), dim3(256), 0, st, \
+                           sp, n * sstride, sp_off, lens, (u32)n, nullptr, nullptr, 0u);      \
+    }});
+    ROOMSL(8) ROOMSL(16) ROOMSL(32)
     vs.push_back({"fixed stride 2048 verify (same rooms)", (double)n * (L + 1), [&](hipStream_t st) {
         CK(launch_verify_fixed(sp, sstride, L, (u32)n, vd2, 0u, st));
     }});
