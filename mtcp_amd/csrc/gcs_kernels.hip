@@ -979,10 +979,7 @@ desc_fallback_block(uint8_t* __restrict__ frames, uint64_t frames_bytes,
     }
 }
 
-// DPF > 0: after its stream, each block reads the descriptors of logical block
-// blk + DPF (the same XCD's range, blocks that start about then) with the
-// cached policy, so that their phase-0 trip hits L2.
-template <class T, bool COMPUTE, int WM, bool XCD, int DPF = 0>
+template <class T, bool COMPUTE, int WM, bool XCD>
 __global__ void __launch_bounds__(kBlock, T::OCC)
 k_desc_stream(uint8_t* __restrict__ frames, uint64_t frames_bytes,
               const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens, u32 n,
@@ -1138,12 +1135,6 @@ k_desc_stream(uint8_t* __restrict__ frames, uint64_t frames_bytes,
         if (lane == 0)
             wtot[w] = run;
     }
-    u32 pfx = 0;
-    if constexpr (DPF > 0) {
-        const uint64_t j = ((uint64_t)blk + DPF) * F + t;
-        if (pass == 0 && j < n)
-            pfx = (u32)off[j] ^ (u32)lens[j];
-    }
     __syncthreads();
 
     // phase 3: one lane per frame of the pass
@@ -1231,10 +1222,6 @@ k_desc_stream(uint8_t* __restrict__ frames, uint64_t frames_bytes,
         desc_fallback_block<T::FG, T::FU, COMPUTE>(frames, frames_bytes, off, lens, f0 + p1,
                                                    fb_hi - p1, out_code, out_csum, flags,
                                                    codes + p1);
-    }
-    if constexpr (DPF > 0) {
-        if (pfx == 0x9E3779B9u && nf == 1 && f0 == (uint64_t)-1)
-            out_code[0] = 0;               // never: keeps the loads
     }
 }
 
@@ -1623,14 +1610,8 @@ __device__ bool gro_cont32(const uint8_t* p, const uint8_t* c, int pp, int pc)
 // one wave per run -- see the comment at phase D2.
 enum { SEG_HDR = 0, SEG_PAY = 1, SEG_WHOLE = 2 };
 
-// DIAG (tools/kbench.hip only; 0 in the library): 1 = the descriptors are not
-// loaded but synthesized as kbench's LRO batch lays them out (1500 B frames at a
-// 1536 B stride, all accepted) -- the cost of the descriptor trip.
-// NXP > 0: wave 3 (FLAT; else thread t, frame t) first reads window
-// blockIdx + NXP's descriptors and header lines with the cached policy (that window's phase A trips then hit
-// the caches, if they keep them until it starts).
 template <int U, int W = kGroW, int OCC = 1, bool FLAT = false, int FWM = WM_SECTOR,
-          bool ACX = false, int PF = 0, int DIAG = 0, int NXP = 0>
+          bool ACX = false, int PF = 0>
 __global__ void __launch_bounds__(kBlock, OCC)
 k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restrict__ off,
       const uint16_t* __restrict__ lens, const uint8_t* __restrict__ verdict, u32 n, u32 window,
@@ -1672,34 +1653,9 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
     const uint64_t w0 = (uint64_t)blockIdx.x * window;
     const int cnt = (int)min<uint64_t>(window, n - w0);
     const uint4 z = make_uint4(0, 0, 0, 0);
-    auto d_off = [&](uint64_t j) -> uint64_t {
-        if constexpr (DIAG == 1) return j * 1536u; else return off[j];
-    };
-    auto d_len = [&](uint64_t j) -> u32 {
-        if constexpr (DIAG == 1) return 1500u; else return lens[j];
-    };
-
-    // A: parse.  PF (A/B, FLAT windows in wave 0): waves 1-3, idle until D,
-    // read the window's input region meanwhile with cached loads, so that D2's
-    // payload loads find it in L2 / the Infinity Cache.
-    if constexpr (NXP > 0) {
-        constexpr int T0 = FLAT ? 192 : 0;             // FLAT: wave 3 (idle until D)
-        const uint64_t j = ((uint64_t)blockIdx.x + NXP) * window + (t - T0);
-        if (t >= T0 && t - T0 < (int)window && j < n) {
-            const uint64_t o = off[j];
-            const u32 L = lens[j];
-            u32 x = L ^ verdict[j];
-            if ((o & 15) == 0 && o <= in_bytes && in_bytes - o >= 96) {
-                const uint4 a = ldg16<false>(in + o), b = ldg16<false>(in + o + 80);
-                x ^= a.x ^ b.w;
-            }
-            if (x == 0x9E3779B9u && cnt == 1 && w0 == (uint64_t)-1)
-                head[0] = x;                                   // never: keeps the loads alive
-        }
-    }
     if constexpr (PF > 0) {
         if (t >= 64 && cnt > 0) {
-            const uint64_t a = d_off(w0) & ~15ull, l = d_off(w0 + cnt - 1) + d_len(w0 + cnt - 1);
+            const uint64_t a = off[w0] & ~15ull, l = off[w0 + cnt - 1] + lens[w0 + cnt - 1];
             uint64_t b = l < in_bytes ? l : in_bytes;
             if (b > a && b - a > 64ull * 4096)         // not a packed window: no prefetch
                 b = a;
@@ -1720,11 +1676,11 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
         }
     }
     if (t < cnt) {
-        const uint64_t o = d_off(w0 + t);
-        const u32 L = d_len(w0 + t);
+        const uint64_t o = off[w0 + t];
+        const u32 L = lens[w0 + t];
         soff[t] = o;
         const bool ok = (o & 15) == 0 && o <= in_bytes && L <= in_bytes - o;
-        const bool acc = ok && (DIAG == 1 || verdict[w0 + t] == GCS_V_ACCEPT);
+        const bool acc = ok && verdict[w0 + t] == GCS_V_ACCEPT;
         dok[t] = ok;
 #pragma unroll
         for (int c = 0; c < kGroHdr / 16; c++) {
@@ -1787,7 +1743,7 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
     if (walk && t < cnt && (t == 0 || !cont[t])) {
         int cur = t;
         u32 mlen = pay[t] > 0 ? 34 + 4 * (hdr[t][46] >> 4) + (u32)pay[t]
-                              : (dok[t] ? d_len(w0 + t) : 0u);     // a bad descriptor: nothing
+                              : (dok[t] ? (u32)lens[w0 + t] : 0u);     // a bad descriptor: nothing
         pref[t] = 0;
         rhead[t] = (uint16_t)t;
         rn_at[t] = 1;
@@ -2685,14 +2641,13 @@ hipError_t launch_gro(const uint8_t* in, uint64_t in_bytes, const uint64_t* off,
     // while waves 1-3 stream this one, measured 770-805 us against 650:
     // three streaming waves per block at 5 blocks per CU, 15 per CU, against
     // 32 here -- tools/gro_pipe.hip, kbench lro)
-    // (round 5: phase A's two dependent trips, descriptors then headers, cost
-    // ~25 us: synthesized descriptors 650-655 vs 678-682 us.  NXP = 2048: wave
-    // 3 reads the descriptors and header lines of the window 2048 blocks on,
-    // about one generation of resident blocks later, so that its trips hit the
-    // caches: 653-658 us, the same box; windows of 256 gain nothing from it,
-    // 864 vs 871-876 us -- profiles/r05/kbench_lro_nxp*.log)
+    // (round 5, blocked A/B: descriptors synthesized instead of loaded 649 vs
+    // 653 us, and wave 3 reading window blockIdx + 1024's descriptors and
+    // header lines ahead 652 us: phase A's trips are hidden already.  The
+    // interleaved runs' 25 us "gain" was the first variant of each round
+    // running behind the D2D copy's write-back -- profiles/r05/kbench_blocked.log)
     if (window <= 64)
-        hipLaunchKernelGGL((k_gro<2, 64, 8, true, WM_SECTOR_NT, true, 8, 0, 2048>),
+        hipLaunchKernelGGL((k_gro<2, 64, 8, true, WM_SECTOR_NT, true, 8>),
                            dim3((n + window - 1) / window), dim3(kBlock), 0, s, in, in_bytes, off,
                            len, verdict, n, window, max_len, out, out_bytes, out_off, out_len,
                            head);
