@@ -11,8 +11,8 @@ namespace gcs {
 // grid sized to the resident capacity: the descriptor of the group's next frame
 // is loaded with the current frame's chunks (3 VGPRs), so each frame costs one
 // memory trip instead of k_desc's two (descriptor, then chunks).
-template <int G, int U, bool COMPUTE, bool NT, int WM>
-__global__ void __launch_bounds__(kBlock)
+template <int G, int U, bool COMPUTE, bool NT, int WM, int OCC = 1>
+__global__ void __launch_bounds__(kBlock, OCC)
 k_rooms(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __restrict__ off,
         const uint16_t* __restrict__ lens, u32 n, uint8_t* __restrict__ out_code,
         uint32_t* __restrict__ out_csum, u32 flags)
@@ -43,6 +43,75 @@ k_rooms(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __r
         i = nx;
         o = onx;
         len = lnx;
+    }
+}
+
+// The same walk software-pipelined: frame k+1's chunks (and frame k+2's
+// descriptor) are loaded before frame k is folded and written, so the wait for
+// the next frame's data never waits for this frame's stores (vmcnt counts both
+// on CDNA).
+template <int G, int U, bool COMPUTE, bool NT, int WM, int OCC = 1, bool LOOP = true>
+__global__ void __launch_bounds__(kBlock, OCC)
+k_rooms_pipe(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __restrict__ off,
+             const uint16_t* __restrict__ lens, u32 n, uint8_t* __restrict__ out_code,
+             uint32_t* __restrict__ out_csum, u32 flags)
+{
+    constexpr int FPB = kBlock / G;
+    const int sub = threadIdx.x & (G - 1);
+    const uint64_t groups = (uint64_t)gridDim.x * FPB;
+    uint64_t i = (uint64_t)xcd_block(blockIdx.x, gridDim.x) * FPB + threadIdx.x / G;
+    if (i >= n)
+        return;
+    auto valid = [&](uint64_t o, u32 len) {
+        return (o & 15) == 0 && o <= frames_bytes && len <= frames_bytes - o;
+    };
+    uint64_t o = off[i];
+    u32 len = lens[i];
+    bool ok = valid(o, len);
+    uint4 v[U];
+    load_first<G, U, true, NT>(frames + (ok ? o : 0), ok ? (int)((len + 15) >> 4) : 0,
+                               ok ? (int64_t)(frames_bytes - o) : 0, sub, v);
+    uint64_t nx = i + groups, on = 0;
+    u32 ln = 0;
+    if (nx < n) {
+        on = off[nx];
+        ln = lens[nx];
+    }
+    for (;;) {                                         // group-uniform
+        uint4 vn[U];
+#pragma unroll
+        for (int j = 0; j < U; j++)
+            vn[j] = make_uint4(0, 0, 0, 0);
+        bool okn = false;
+        const uint64_t nnx = nx + groups;
+        uint64_t onn = 0;
+        u32 lnn = 0;
+        if (nx < n) {
+            okn = valid(on, ln);
+            load_first<G, U, true, NT>(frames + (okn ? on : 0), okn ? (int)((ln + 15) >> 4) : 0,
+                                       okn ? (int64_t)(frames_bytes - on) : 0, sub, vn);
+            if (nnx < n) {
+                onn = off[nnx];
+                lnn = lens[nnx];
+            }
+        }
+        uint8_t* f = frames + (ok ? o : 0);
+        frame_body<G, U, COMPUTE, LOOP, true, NT, WM>(v, f, f, len,
+                                                      ok ? (int64_t)(frames_bytes - o) : 0, ok,
+                                                      sub, flags, out_code ? out_code + i : nullptr,
+                                                      out_csum ? out_csum + i : nullptr, true);
+        if (nx >= n)
+            break;
+#pragma unroll
+        for (int j = 0; j < U; j++)
+            v[j] = vn[j];
+        i = nx;
+        o = on;
+        len = ln;
+        ok = okn;
+        nx = nnx;
+        on = onn;
+        ln = lnn;
     }
 }
 

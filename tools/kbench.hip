@@ -2663,6 +2663,39 @@ int lro_main(uint64_t n, int rounds)
                            sp, n * sstride, sp_off, lens, (u32)n, nullptr, nullptr, 0u);      \
     }});
     ROOMSL(8) ROOMSL(16) ROOMSL(32)
+#define ROOMSP(BPC_)                                                                         \
+    vs.push_back({"rooms verify k_rooms_pipe " #BPC_ " blocks/CU", (double)n * (L + 1),        \
+                  [&](hipStream_t st) {                                                      \
+        const u32 g = (u32)std::min<uint64_t>((n + 7) / 8, (uint64_t)BPC_ * cus);             \
+        hipLaunchKernelGGL((k_rooms_pipe<32, 3, false, kNT, kWM>), dim3(g), dim3(256), 0, st,  \
+                           sp, n * sstride, sp_off, lens, (u32)n, vd2, nullptr, 0u);          \
+    }});                                                                                     \
+    vs.push_back({"rooms fill k_rooms_pipe line " #BPC_ " blocks/CU", (double)n * (L + 4),    \
+                  [&](hipStream_t st) {                                                      \
+        const u32 g = (u32)std::min<uint64_t>((n + 7) / 8, (uint64_t)BPC_ * cus);             \
+        hipLaunchKernelGGL((k_rooms_pipe<32, 3, true, kNT, WM_LINE_SC1>), dim3(g), dim3(256), 0, \
+                           st, sp, n * sstride, sp_off, lens, (u32)n, nullptr, nullptr, 0u);  \
+    }});
+    ROOMSP(6) ROOMSP(8) ROOMSP(16)
+#define ROOMSX(TAG, KV_, KF_, BPC_)                                                           \
+    vs.push_back({"rooms verify " TAG, (double)n * (L + 1), [&](hipStream_t st) {             \
+        const u32 g = (u32)std::min<uint64_t>((n + 7) / 8, (uint64_t)BPC_ * cus);             \
+        hipLaunchKernelGGL(KV_, dim3(g), dim3(256), 0, st, sp, n * sstride, sp_off, lens,      \
+                           (u32)n, vd2, nullptr, 0u);                                        \
+    }});                                                                                     \
+    vs.push_back({"rooms fill " TAG, (double)n * (L + 4), [&](hipStream_t st) {               \
+        const u32 g = (u32)std::min<uint64_t>((n + 7) / 8, (uint64_t)BPC_ * cus);             \
+        hipLaunchKernelGGL(KF_, dim3(g), dim3(256), 0, st, sp, n * sstride, sp_off, lens,      \
+                           (u32)n, nullptr, nullptr, 0u);                                    \
+    }});
+    ROOMSX("k_rooms occ8, 8 blocks/CU", (k_rooms<32, 3, false, kNT, kWM, 8>),
+           (k_rooms<32, 3, true, kNT, WM_LINE_SC1, 8>), 8)
+    ROOMSX("k_rooms_pipe occ7 noloop, 7 blocks/CU", (k_rooms_pipe<32, 3, false, kNT, kWM, 7, false>),
+           (k_rooms_pipe<32, 3, true, kNT, WM_LINE_SC1, 7, false>), 7)
+    ROOMSX("k_rooms_pipe occ6 noloop, 6 blocks/CU", (k_rooms_pipe<32, 3, false, kNT, kWM, 6, false>),
+           (k_rooms_pipe<32, 3, true, kNT, WM_LINE_SC1, 6, false>), 6)
+    ROOMSX("k_rooms_pipe occ8 noloop, 8 blocks/CU", (k_rooms_pipe<32, 3, false, kNT, kWM, 8, false>),
+           (k_rooms_pipe<32, 3, true, kNT, WM_LINE_SC1, 8, false>), 8)
     vs.push_back({"fixed stride 2048 verify (same rooms)", (double)n * (L + 1), [&](hipStream_t st) {
         CK(launch_verify_fixed(sp, sstride, L, (u32)n, vd2, 0u, st));
     }});
