@@ -2614,6 +2614,10 @@ int lro_main(uint64_t n, int rounds)
                            dim3(256), 0, st, in, n * stride, off, lens, vd, (u32)n, 64u, 16384u,
                            out, n * stride, oo, ol, hd);
     }});
+    // (round 5: phase D2 software-pipelined, trip k+1's loads issued before trip
+    // k is consumed: U = 1 at 8 waves 675 us, U = 2 at 7 waves 664 us, U = 2 at
+    // 8 waves spilled 1,061 us, against 655-659 us shipped; the form was
+    // removed again -- profiles/r05/kbench_gro_pipe_{b,i}.log)
     // windows of 256 (run-per-wave k_gro<2, 256>; not compared with launch_gro's
     // 64-frame windows)
     vs.push_back({"w256 k_gro<2,256>", bytes, [&](hipStream_t st) {
