@@ -538,6 +538,51 @@ def test_desc_sparse_rooms_vs_oracle(torch_dev, ctx, O, rooms):
         assert len(np.unique(rv)) >= 3
 
 
+@pytest.mark.parametrize("sector_wb", [False, True], ids=["line_wb", "sector_wb"])
+def test_rooms_hint_is_only_a_hint(torch_dev, ctx, O, sector_wb):
+    """GCS_VF_ROOMS / GCS_CF_ROOMS change the kernel, never the result: packed
+    IMIX frames in shuffled descriptor order (neighbouring frames share lines,
+    so the line write-back of one frame's group must not clobber another's
+    bytes), ragged n, and bad descriptors (misaligned, past the end, length
+    over the end) -- TX and RX bit-exact against the oracle, with line and
+    with sector write-back (GCS_CF_SECTOR_WB)."""
+    t = torch_dev
+    n = 3 * 256 + 45
+    lens = synth.imix_lengths(n, seed=0x700D)
+    buf, off, lens = synth.packed_frames(lens, seed=0x700E)
+    perm = np.random.default_rng(0x700F).permutation(n)
+    off, lens = off[perm].copy(), lens[perm].copy()
+    nb = len(buf)
+    off[11], lens[11] = off[11] + 8, 64                 # misaligned
+    off[97], lens[97] = (nb + 127) & ~15, 60            # past the end
+    off[300], lens[300] = (nb - 48) & ~15, 1500         # length over the end
+    hint = gpucsum.K["GCS_CF_ROOMS"] | (gpucsum.K["GCS_CF_SECTOR_WB"] if sector_wb else 0)
+    doff, dlen = dev(t, off.view(np.int64)), dev(t, lens.view(np.int16))
+    ref = buf.copy()
+    rst, rcs = O.compute_batch(ref, off, lens)
+    assert (rst == 9).sum() == 3
+    d = dev(t, buf)
+    st = t.full((n,), 0xEE, dtype=t.uint8, device="cuda")
+    cs = t.zeros(n, dtype=t.int32, device="cuda")
+    ctx.compute(d, doff, dlen, n, st, cs, flags=hint)
+    ctx.sync()
+    np.testing.assert_array_equal(host(st), rst)
+    np.testing.assert_array_equal(host(cs).view(np.uint32), rcs)
+    np.testing.assert_array_equal(host(d), ref)
+    good = np.array([i for i in range(n) if i not in (11, 97, 300)])
+    synth.corrupt(ref, off[good], np.maximum(lens[good], 15), frac_log2=3, seed=0x7010)
+    for flags in (0, 1):
+        d = dev(t, ref)
+        v = t.full((n,), 0xEE, dtype=t.uint8, device="cuda")
+        ctx.verify(d, doff, dlen, n, v, flags=flags | gpucsum.K["GCS_VF_ROOMS"])
+        ctx.sync()
+        exp = ref.copy()
+        rv = O.verify_batch(exp, off, lens, flags=flags)
+        np.testing.assert_array_equal(host(v), rv)
+        np.testing.assert_array_equal(host(d), exp)
+        assert len(np.unique(rv)) >= 3
+
+
 def test_desc_stream_region_at_buffer_end(torch_dev, ctx, O):
     """A streaming block whose region ends exactly at frames_bytes (16 B-
     aligned: streamed; not aligned: the block falls back to guarded loads)."""
