@@ -795,11 +795,14 @@ def plugin_threads():
     (GCS_SERVER_COUNTERS=1), which adds the GPU serving time (gpu_span_us:
     first serving block saw the request -> last one's records stored), its
     per-block phases, and post -> done split into the wait before the GPU saw
-    the request, that span, and the way back."""
+    the request, that span, and the way back.  `pinned`: the shipped grid with
+    each thread pinned to one CPU (MT_PIN=1), as mTCP pins its threads
+    (core.c:1153-1245)."""
     import subprocess
     out = {}
-    for name, prof in (("shipped", "0"), ("counters", "1")):
-        env = dict(os.environ, SS_PROF=prof, SS_THREADS="1,8,12,16", SS_RINGS="4x2,4x4,4x6")
+    for name, prof, pin in (("shipped", "0", "0"), ("counters", "1", "0"), ("pinned", "0", "1")):
+        env = dict(os.environ, SS_PROF=prof, SS_THREADS="1,8,12,16", SS_RINGS="4x2,4x4,4x6",
+                   MT_PIN=pin)
         try:
             r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "server_scaling.py")],
                                capture_output=True, text=True, timeout=240, env=env)

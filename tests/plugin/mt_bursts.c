@@ -7,7 +7,11 @@
  * GPU_MAX_HW_QUEUES hardware queues.  Every burst is checked against the
  * oracle (oracle/csum_ref.c) on the thread that made it.
  */
+#ifndef _GNU_SOURCE
+#define _GNU_SOURCE
+#endif
 #include <pthread.h>
+#include <sched.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -146,6 +150,25 @@ static void make_frame(uint8_t *f, uint32_t len, uint64_t *rng)
 	if (len >= 66) { f[54] = 1; f[55] = 1; f[56] = 8; f[57] = 10; }
 }
 
+/* MT_PIN=1: pin worker t to the t-th CPU this process may run on, as mTCP pins
+ * each of its threads to one core (core.c:1153-1245, mtcp_core_affinitize). */
+static void pin_self(int t)
+{
+	const char *e = getenv("MT_PIN");
+	cpu_set_t allowed, one;
+	int c, k = 0;
+
+	if (!e || atoi(e) == 0 || sched_getaffinity(0, sizeof allowed, &allowed) != 0)
+		return;
+	for (c = 0; c < CPU_SETSIZE; c++)
+		if (CPU_ISSET(c, &allowed) && k++ == t % CPU_COUNT(&allowed)) {
+			CPU_ZERO(&one);
+			CPU_SET(c, &one);
+			(void)pthread_setaffinity_np(pthread_self(), sizeof one, &one);
+			return;
+		}
+}
+
 static double now_us(void)
 {
 	struct timespec t;
@@ -156,6 +179,7 @@ static double now_us(void)
 static void *run(void *arg)
 {
 	struct job *j = arg;
+	pin_self(j->id);
 	uint8_t *rooms = malloc((size_t)BURST * ROOM), *ref = malloc((size_t)BURST * ROOM);
 	uint8_t *ptrs[BURST], st[BURST], vd[BURST];
 	uint16_t len[BURST];
@@ -277,6 +301,7 @@ static void *run_rings(void *arg)
 {
 	struct job *j = arg;
 	enum { R = 8 };
+	pin_self(j->id);
 	uint8_t *rooms[R], *ref[R], *ptrs[R][BURST], st[R][BURST], vd[R][BURST];
 	uint16_t len[R][BURST];
 	uint32_t cs[R][BURST];

@@ -58,7 +58,8 @@ def main():
     os.environ["MT_CHECK_EVERY"] = os.environ.get("MT_CHECK_EVERY", "16")
     out = {"config": {k: os.environ.get(k, "default") for k in
                       ("GCS_SERVER_MAILBOX", "GCS_SERVER_ACQUIRE", "GCS_SERVER_COUNTERS",
-                       "GCS_DIRECT_STAGE", "GCS_SERVER_HOT_NAPS", "GCS_SERVER_HOT_US")},
+                       "GCS_DIRECT_STAGE", "GCS_SERVER_HOT_NAPS", "GCS_SERVER_HOT_US",
+                       "MT_PIN")},
            "cpus": cpu_quota(),
            "cpu_frac": "thread CPU time / wall time inside the calls (below 1: descheduled)"}
     iters = int(os.environ.get("SS_ITERS", "600"))
