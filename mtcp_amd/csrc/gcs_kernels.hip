@@ -1653,6 +1653,10 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
     const uint64_t w0 = (uint64_t)blockIdx.x * window;
     const int cnt = (int)min<uint64_t>(window, n - w0);
     const uint4 z = make_uint4(0, 0, 0, 0);
+
+    // A: parse.  PF (A/B, FLAT windows in wave 0): waves 1-3, idle until D,
+    // read the window's input region meanwhile with cached loads, so that D2's
+    // payload loads find it in L2 / the Infinity Cache.
     if constexpr (PF > 0) {
         if (t >= 64 && cnt > 0) {
             const uint64_t a = off[w0] & ~15ull, l = off[w0 + cnt - 1] + lens[w0 + cnt - 1];
