@@ -2644,7 +2644,7 @@ hipError_t launch_gro(const uint8_t* in, uint64_t in_bytes, const uint64_t* off,
     // (round 4's pipelined persistent form, wave 0 planning the next window
     // while waves 1-3 stream this one, measured 770-805 us against 650:
     // three streaming waves per block at 5 blocks per CU, 15 per CU, against
-    // 32 here -- tools/gro_pipe.hip, kbench lro)
+    // 32 here -- tools/attic/gro_pipe.hip, kbench lro)
     // (round 5, blocked A/B: descriptors synthesized instead of loaded 649 vs
     // 653 us, and wave 3 reading window blockIdx + 1024's descriptors and
     // header lines ahead 652 us: phase A's trips are hidden already.  The
