@@ -2646,6 +2646,9 @@ int lro_main(uint64_t n, int rounds)
         hipLaunchKernelGGL((k_desc<32, 3, false, kNT, kWM, kXCD>), dim3((n + 7) / 8), dim3(256), 0,
                            st, sp, n * sstride, sp_off, lens, (u32)n, vd2, nullptr, 0u);
     }});
+    // (round 5: the same kernel without load guards and without the batch
+    // loop, upper bounds for this batch: fill 292-305 vs 297-298 us, verify
+    // within the run-to-run spread -- profiles/r05/kbench_rooms_safe_{b,i}.log)
     vs.push_back({"rooms fill k_desc<32,3> XCD line (shipped)", (double)n * (L + 4), [&](hipStream_t st) {
         hipLaunchKernelGGL((k_desc<32, 3, true, kNT, WM_LINE_SC1, kXCD>), dim3((n + 7) / 8),
                            dim3(256), 0, st, sp, n * sstride, sp_off, lens, (u32)n, nullptr,
