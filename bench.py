@@ -572,7 +572,7 @@ def rows_8f(ctx, torch, n=1 << 20, L=1500):
     out["lro_gbs_algorithmic"] = 2 * n * L / (ms * 1e-3) / 1e9
     out["lro_frac_peak"] = 2 * n * L / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS
     # windows of 256 frames (an ENABLELRO DPDK build's larger bursts,
-    # dpdk_module.c:44-48): the run-per-wave k_gro<2, 256>
+    # dpdk_module.c:44-48): the FLAT form over 1,024-thread blocks (round 5)
     ms = _launch_ms(torch, lambda: ctx.gro(sb, off, lens, v, n, 256, 16384, o, oo, ol, hd,
                                            stream=stream))
     assert int((ol != 0).sum()) == n // 8

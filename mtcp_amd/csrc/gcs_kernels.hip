@@ -1525,6 +1525,7 @@ k_copy_fill(uint8_t* __restrict__ frames, uint64_t frames_bytes,
 //      once and written once.
 
 constexpr int kGroW = 256;      // frames per window (one per thread)
+constexpr int kGroWideThreads = 1024;   // block of the FLAT form for windows > 64
 constexpr int kGroHdr = 96;     // header bytes kept per frame (14 + 20 + 60 + 2)
 
 __device__ __forceinline__ u32 lds_be16(const uint8_t* p) { return ((u32)p[0] << 8) | p[1]; }
@@ -1606,20 +1607,25 @@ __device__ bool gro_cont32(const uint8_t* p, const uint8_t* c, int pp, int pc)
 // W = the largest window the instantiation takes (LDS is sized by it): W = 64
 // needs ~9 KiB of LDS per block instead of ~36 KiB, so a CU holds twice the
 // blocks (8 instead of 4) and twice the run-building waves.
-// FLAT (W <= 64): phase D as one stream over the window's output instead of
-// one wave per run -- see the comment at phase D2.
+// FLAT: phase D as one stream over the window's output instead of one wave
+// per run -- see the comment at phase D2.  W <= 64: the window's frames sit in
+// wave 0.  W > 64 (WIDE, round 5): every wave parses frames; chains and the
+// segment list are block scans, the merged heads' header chunks are read from
+// the input in D2, and the stash of each merged run's first chunks takes the
+// header rows' LDS once D1 is done with them.
 enum { SEG_HDR = 0, SEG_PAY = 1, SEG_WHOLE = 2 };
 
 template <int U, int W = kGroW, int OCC = 1, bool FLAT = false, int FWM = WM_SECTOR,
-          bool ACX = false, int PF = 0>
-__global__ void __launch_bounds__(kBlock, OCC)
+          bool ACX = false, int PF = 0, int BT = kBlock>
+__global__ void __launch_bounds__(BT, OCC)
 k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restrict__ off,
       const uint16_t* __restrict__ lens, const uint8_t* __restrict__ verdict, u32 n, u32 window,
       u32 max_len, uint8_t* __restrict__ out, uint64_t out_bytes, uint64_t* __restrict__ out_off,
       uint16_t* __restrict__ out_len, uint32_t* __restrict__ head)
 {
-    static_assert(W <= kBlock, "one frame per thread");
+    static_assert(W <= BT, "one frame per thread");
     constexpr int G = 64;
+    constexpr bool WIDE = FLAT && W > 64;
     __shared__ __attribute__((aligned(16))) uint8_t hdr[W][kGroHdr];
     __shared__ int pay[W];         // TCP payload bytes of a mergeable frame, else -1
     __shared__ uint8_t cont[W];
@@ -1635,7 +1641,7 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
     __shared__ uint16_t rn_at[W];  // per run head (window index): members, length, run index
     __shared__ uint32_t rl_at[W];
     __shared__ uint16_t ridx[W];
-    __shared__ uint32_t wsum[kBlock / 64][2];
+    __shared__ uint32_t wsum[BT / 64][2];
     __shared__ uint32_t nout_s;     // the window's output bytes (runs at 16 B-aligned offsets)
     constexpr int NS = FLAT ? 2 * W : 1, NRF = FLAT ? W : 1;
     __shared__ uint32_t sg_st[NS];  // FLAT: segments of the output, in output order
@@ -1645,9 +1651,17 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
     __shared__ uint8_t sg_run[NS];
     __shared__ int nseg_s;
     constexpr int NROW = FLAT ? 1024 : 1;   // 64-chunk output rows with a start entry (1 MiB)
-    __shared__ uint8_t sg_row[NROW];   // FLAT: the segment holding each row's first byte
-    __shared__ uint4 rstash[NRF][4];   // FLAT: chunks 0..3 of each merged run
-    __shared__ uint32_t rpf[NRF], rqe[NRF], wtot[kBlock / 64];
+    using SgIdx = std::conditional_t<(NS > 256), uint16_t, uint8_t>;
+    __shared__ SgIdx sg_row[NROW];     // FLAT: the segment holding each row's first byte
+    // FLAT: chunks 0..3 of each merged run (WIDE: in hdr's rows, dead after D1)
+    static_assert(!WIDE || NRF * 64 <= W * kGroHdr, "the stash fits the header rows");
+    __shared__ uint4 rstash_own[WIDE ? 1 : NRF][4];
+    uint4 (*const rstash)[4] = WIDE ? reinterpret_cast<uint4 (*)[4]>(&hdr[0][0]) : rstash_own;
+    __shared__ uint32_t rpf[NRF], rqe[NRF], wtot[BT / 64];
+    constexpr int WW = WIDE ? W : 1;
+    __shared__ uint8_t rpsh[WW];       // WIDE: each merged run's PSH bit (read before D2)
+    __shared__ uint32_t cincl[WW], cexcl[WW], cwt[BT / 64];   // WIDE: block scans
+    __shared__ uint64_t smask[BT / 64];   // WIDE: chain starts, per wave
 
     const int t = threadIdx.x;
     const uint64_t w0 = (uint64_t)blockIdx.x * window;
@@ -1664,11 +1678,11 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
             if (b > a && b - a > 64ull * 4096)         // not a packed window: no prefetch
                 b = a;
             u32 x = 0;
-            for (uint64_t base = a + 16ull * (t - 64); base < b; base += 16ull * 192 * PF) {
+            for (uint64_t base = a + 16ull * (t - 64); base < b; base += 16ull * (BT - 64) * PF) {
                 uint4 v[PF];
 #pragma unroll
                 for (int k = 0; k < PF; k++) {
-                    const uint64_t q = base + 16ull * 192 * k;
+                    const uint64_t q = base + 16ull * (BT - 64) * k;
                     v[k] = q + 16 <= b ? ldg16<false>(in + q) : z;
                 }
 #pragma unroll
@@ -1715,7 +1729,66 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
     uint32_t rl = 0;                                   // this thread's run length if it heads one
     bool rs = false;                                   // ... and whether it does
     bool walk = true;                                  // this chain needs the sequential walk
-    if constexpr (ACX) {
+    if constexpr (ACX && WIDE) {
+        // the same over the block: chain heads and ends from the waves' start
+        // masks, payload prefixes from a block scan
+        const int lane = t & 63, wv = t >> 6;
+        const bool valid = t < cnt, start = !valid || t == 0 || !cont[t];
+        const uint64_t sm = __ballot(start);
+        const u32 pv = valid && pay[t] > 0 ? (u32)pay[t] : 0u;
+        const u32 winc = wave_incl_scan(pv);
+        if (lane == 63) {
+            smask[wv] = sm;
+            cwt[wv] = winc;
+        }
+        __syncthreads();
+        u32 base = 0;
+        for (int q = 0; q < wv; q++)
+            base += cwt[q];
+        const u32 incl = base + winc, excl = incl - pv;
+        if (t < WW) {
+            cincl[t] = incl;
+            cexcl[t] = excl;
+        }
+        const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+        int sh = 0;                                    // the last start at or below t
+        if (sm & upto) {
+            sh = 64 * wv + 63 - __clzll(sm & upto);
+        } else {
+            for (int q = wv - 1; q >= 0; q--)
+                if (smask[q]) {
+                    sh = 64 * q + 63 - __clzll(smask[q]);
+                    break;
+                }
+        }
+        const uint64_t above = sm & ~upto;
+        int se = BT - 1;                           // the frame before the next start
+        if (above) {
+            se = 64 * wv + __ffsll((long long)above) - 2;
+        } else {
+            for (int q = wv + 1; q < BT / 64; q++)
+                if (smask[q]) {
+                    se = 64 * q + __ffsll((long long)smask[q]) - 2;
+                    break;
+                }
+        }
+        __syncthreads();                               // cincl / cexcl complete
+        if (valid) {
+            const u32 hx = cexcl[sh];
+            const u32 tot = cincl[se] - hx;            // the chain's payload
+            const u32 hhl = 34 + 4 * (hdr[sh][46] >> 4);
+            const bool fits = pay[sh] > 0 && hhl + tot <= max_len;
+            walk = !fits;
+            if (fits) {
+                pref[t] = excl - hx;
+                rhead[t] = (uint16_t)sh;
+                if (t == sh) {
+                    rn_at[t] = (uint16_t)(se - sh + 1);
+                    rl_at[t] = hhl + tot;
+                }
+            }
+        }
+    } else if constexpr (ACX) {
         static_assert(W <= 64, "a window's frames sit in wave 0");
         // A chain whose whole payload fits max_len is one run: its members'
         // payload offsets are a segmented scan of the wave, no walk.
@@ -1798,7 +1871,7 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
         }
         xs = bs + is - xs;                             // exclusive
         xl = bl + il - xl;
-        if (t == kBlock - 1) {
+        if (t == BT - 1) {
             nruns = (int)(bs + is);
             nout_s = bl + il;
         }
@@ -1821,10 +1894,18 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
     }
 
     if constexpr (FLAT) {
-        static_assert(W <= 64, "the window's frames sit in wave 0");
-        // D1: the output as segments: a merged run's head headers (from LDS),
-        // each member's payload, or a single frame as it is
-        if (t < 64) {
+        if constexpr (WIDE) {
+            // each merged run's PSH bit for D3, before the stash takes hdr's rows
+            if (t < nruns && run_n[t] > 1) {
+                uint8_t p = 0;
+                for (int k = run_t[t]; k < run_t[t] + run_n[t]; k++)
+                    p |= hdr[k][47] & 0x08;
+                rpsh[t] = p;
+            }
+        }
+        // D1: the output as segments: a merged run's head headers (from LDS;
+        // WIDE: from the input), each member's payload, or a single frame as it is
+        if (WIDE || t < 64) {                        // WIDE: every thread (a block scan)
             int ns = 0, k0 = SEG_HDR;
             u32 st0 = 0, ln0 = 0, ln1 = 0;
             uint64_t sr0 = 0, sr1 = 0;
@@ -1849,7 +1930,7 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
                         k0 = SEG_HDR;
                         st0 = rel;
                         ln0 = hl;
-                        sr0 = (uint64_t)hk;
+                        sr0 = WIDE ? soff[hk] : (uint64_t)hk;
                         ln1 = (u32)pay[t];
                         sr1 = soff[t] + hl;
                     } else {
@@ -1861,7 +1942,16 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
                     }
                 }
             }
-            const u32 incl = wave_incl_scan((u32)ns);
+            const u32 winc = wave_incl_scan((u32)ns);
+            u32 base = 0;
+            if constexpr (WIDE) {
+                if ((t & 63) == 63)
+                    cwt[t >> 6] = winc;
+                __syncthreads();
+                for (int q = 0; q < (t >> 6); q++)
+                    base += cwt[q];
+            }
+            const u32 incl = base + winc;
             const int e = (int)(incl - (u32)ns);
             if (ns >= 1) {
                 sg_st[e] = st0;
@@ -1877,7 +1967,7 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
                 sg_kind[e + 1] = SEG_PAY;
                 sg_run[e + 1] = (uint8_t)rr;
             }
-            if (t == 63)
+            if (t == (WIDE ? BT - 1 : 63))
                 nseg_s = (int)incl;
         }
         __syncthreads();
@@ -1886,14 +1976,14 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
             // (one binary search per row here instead of one per chunk in D2)
             const int nsg = nseg_s;
             const u32 nrow = ((nout_s >> 4) + 63) >> 6;
-            for (u32 rw = t; rw < nrow && rw < (u32)NROW; rw += kBlock) {
+            for (u32 rw = t; rw < nrow && rw < (u32)NROW; rw += BT) {
                 const u32 p = rw << 10;
                 int sgi = 0;
 #pragma unroll
-                for (int step = 64; step > 0; step >>= 1)
+                for (int step = NS / 2; step > 0; step >>= 1)
                     if (sgi + step < nsg && sg_st[sgi + step] <= p)
                         sgi += step;
-                sg_row[rw] = (uint8_t)sgi;
+                sg_row[rw] = (SgIdx)sgi;
             }
         }
         __syncthreads();
@@ -1907,7 +1997,7 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
         // k_desc_stream.  Chunks 0..3 of merged runs wait in LDS for D3.
         const int nseg = nseg_s, wave = t >> 6, lane = t & 63;
         const u32 NOUT = nout_s >> 4;
-        const u32 QW = ((NOUT + 4 * 64 - 1) / (4 * 64)) * 64;
+        const u32 QW = ((NOUT + BT - 1) / BT) * 64;        // BT / 64 waves
         const u32 lo = wave * QW, hi = lo + QW < NOUT ? lo + QW : NOUT;
         uint8_t* ob = out + o0;
         const int64_t wl_all = o0 <= out_bytes ? (int64_t)(out_bytes - o0) : 0;
@@ -1945,10 +2035,10 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
                     const u32 offs = p - ss, rem = sl - offs;
                     const u32 need = rend - p < 16u ? rend - p : 16u;
                     const uint8_t* pa = in + sg_src[sgi] + offs;
-                    if (kd == SEG_HDR && offs + 16 <= (u32)kGroHdr) {
+                    if (!WIDE && kd == SEG_HDR && offs + 16 <= (u32)kGroHdr) {
                         x[j] = *reinterpret_cast<const uint4*>(&hdr[sg_src[sgi]][offs]);
                         plan = AS_ONE;
-                    } else if (kd != SEG_HDR && pa + 16 <= in_end) {
+                    } else if ((WIDE || kd != SEG_HDR) && pa + 16 <= in_end) {
                         x[j] = ldg16u(pa);
                         plan = AS_ONE;
                     } else {
@@ -1989,7 +2079,7 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
                             s2++;
                         if (q < sg_st[s2] || q >= sg_st[s2] + sg_len[s2])
                             continue;
-                        const u32 b = sg_kind[s2] == SEG_HDR
+                        const u32 b = !WIDE && sg_kind[s2] == SEG_HDR
                                           ? (u32)hdr[sg_src[s2]][q - sg_st[s2]]
                                           : (in + sg_src[s2] + (q - sg_st[s2]) < in_end
                                                  ? (u32)in[sg_src[s2] + (q - sg_st[s2])] : 0u);
@@ -2036,8 +2126,12 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
             uint4 sc[4] = {rstash[r][0], rstash[r][1], rstash[r][2], rstash[r][3]};
             const u32 raw = hsum4(sc[0]) + hsum4(sc[1]) + hsum4(sc[2]) + hsum4(sc[3]);
             uint8_t psh = 0;
-            for (int k = k0; k < k0 + nm; k++)
-                psh |= hdr[k][47] & 0x08;
+            if constexpr (WIDE) {
+                psh = rpsh[r];
+            } else {
+                for (int k = k0; k < k0 + nm; k++)
+                    psh |= hdr[k][47] & 0x08;
+            }
             sc[1].x = (sc[1].x & 0xFFFF0000u) | bswap16((mlen - 14) & 0xFFFFu);
             sc[2].w |= (u32)psh << 24;
             Hdr h;
@@ -2054,7 +2148,7 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
                     const u32 q = ch / QW;
                     u32 b = 0;
 #pragma unroll
-                    for (int k = 0; k < kBlock / 64 - 1; k++)
+                    for (int k = 0; k < BT / 64 - 1; k++)
                         b += (u32)k < q ? wtot[k] : 0u;
                     return b;
                 };
@@ -2087,7 +2181,7 @@ k_gro(const uint8_t* __restrict__ in, uint64_t in_bytes, const uint64_t* __restr
     }
 
     // D: build the runs, one wave per run
-    const int wave = t >> 6, sub = t & 63, nwaves = kBlock / 64;
+    const int wave = t >> 6, sub = t & 63, nwaves = BT / 64;
     for (int r = wave; r < nruns; r += nwaves) {       // wave-uniform
         const int k0 = run_t[r], nm = run_n[r];
         const u32 mlen = run_len[r];
@@ -2650,15 +2744,21 @@ hipError_t launch_gro(const uint8_t* in, uint64_t in_bytes, const uint64_t* off,
     // header lines ahead 652 us: phase A's trips are hidden already.  The
     // interleaved runs' 25 us "gain" was the first variant of each round
     // running behind the D2D copy's write-back -- profiles/r05/kbench_blocked.log)
+    // Windows of 65-256 frames (round 5): the FLAT form over the block
+    // (WIDE), 1,024 threads so that two blocks per CU (52 KB of LDS each)
+    // still stream with 32 waves: 1M x 1500 B in windows of 256, 670-672 us
+    // against 860-870 us for round 2's run-per-wave k_gro<2, 256> (695 us at
+    // 512 threads, 891 at 256; tools/kbench lro, profiles/r05/kbench_w256*.log).
     if (window <= 64)
         hipLaunchKernelGGL((k_gro<2, 64, 8, true, WM_SECTOR_NT, true, 8>),
                            dim3((n + window - 1) / window), dim3(kBlock), 0, s, in, in_bytes, off,
                            len, verdict, n, window, max_len, out, out_bytes, out_off, out_len,
                            head);
     else
-        hipLaunchKernelGGL((k_gro<2, kGroW>), dim3((n + window - 1) / window), dim3(kBlock), 0, s,
-                           in, in_bytes, off, len, verdict, n, window, max_len, out, out_bytes,
-                           out_off, out_len, head);
+        hipLaunchKernelGGL((k_gro<2, kGroW, 8, true, WM_SECTOR_NT, true, 0, kGroWideThreads>),
+                           dim3((n + window - 1) / window), dim3(kGroWideThreads), 0, s, in,
+                           in_bytes, off, len, verdict, n, window, max_len, out, out_bytes, out_off,
+                           out_len, head);
     return hipGetLastError();
 }
 

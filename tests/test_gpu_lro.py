@@ -75,7 +75,9 @@ def verdicts(t, ctx, buf, off, lens):
 
 @pytest.mark.parametrize("window,max_len,run_mean", [(64, 16384, 6.0), (256, 65535, 50.0),
                                                      (1, 16384, 6.0), (7, 3000, 6.0),
-                                                     (256, 16384, 3.0)])
+                                                     (256, 16384, 3.0), (65, 16384, 6.0),
+                                                     (100, 3000, 20.0), (200, 16384, 40.0),
+                                                     (256, 3000, 20.0)])
 def test_gro_streams_vs_oracle(torch_dev, ctx, O, window, max_len, run_mean):
     t = torch_dev
     n = 20000
@@ -97,9 +99,11 @@ def test_gro_streams_vs_oracle(torch_dev, ctx, O, window, max_len, run_mean):
         assert (v == 0).all()
 
 
-def test_gro_mixed_traffic_and_bad_descriptors(torch_dev, ctx, O):
+@pytest.mark.parametrize("window", [64, 200, 256])
+def test_gro_mixed_traffic_and_bad_descriptors(torch_dev, ctx, O, window):
     """Streams interleaved with IMIX frames, ICMP, bad descriptors and a
-    cut-short output buffer."""
+    cut-short output buffer; windows of 64 (wave 0 plans) and of more frames
+    (the block plans: chains and segments across waves)."""
     t = torch_dev
     rng = np.random.default_rng(9)
     sb, so, sl = synth.tcp_streams(3000, seed=10)
@@ -118,13 +122,13 @@ def test_gro_mixed_traffic_and_bad_descriptors(torch_dev, ctx, O):
         buf[int(off[k]) + 23] = 1                             # ICMP: not ACCEPT
     off = off.copy()
     off[5] += 8                                               # misaligned descriptor
-    off[128] += 8                                             # ... first of its window: the
+    off[2 * window] += 8                                      # ... first of its window: the
     vd = verdicts(t, ctx, buf, off, lens)                     # window's output base moves too
     for out_bytes in (None, buf.nbytes // 2 + 3):
-        gpu = run_gro(t, ctx, buf, off, lens, vd, 64, 16384, out_bytes=out_bytes)
-        ref = O.gro_batch(buf, off, lens, vd, 64, 16384, out_bytes=out_bytes)
+        gpu = run_gro(t, ctx, buf, off, lens, vd, window, 16384, out_bytes=out_bytes)
+        ref = O.gro_batch(buf, off, lens, vd, window, 16384, out_bytes=out_bytes)
         compare(buf, off, lens, gpu, ref)
-        assert gpu[2][5] == 0 and gpu[2][128] == 0
+        assert gpu[2][5] == 0 and gpu[2][2 * window] == 0
 
 
 def test_gro_rejects_bad_arguments(torch_dev, ctx):

@@ -2620,9 +2620,41 @@ int lro_main(uint64_t n, int rounds)
     // removed again -- profiles/r05/kbench_gro_pipe_{b,i}.log)
     // windows of 256 (run-per-wave k_gro<2, 256>; not compared with launch_gro's
     // 64-frame windows)
-    vs.push_back({"w256 k_gro<2,256>", bytes, [&](hipStream_t st) {
+    vs.push_back({"w256 k_gro<2,256> (run per wave)", bytes, [&](hipStream_t st) {
         hipLaunchKernelGGL((k_gro<2, 256>), dim3((n + 255) / 256), dim3(256), 0, st, in, n * stride,
                            off, lens, vd, (u32)n, 256u, 16384u, out, n * stride, oo, ol, hd);
+    }});
+    // round 5: windows of 256 in the FLAT form (WIDE: block scans)
+#define GROW256(U_, OCC_)                                                                     \
+    vs.push_back({"w256 FLAT U=" #U_ " occ " #OCC_, bytes, [&](hipStream_t st) {               \
+        hipLaunchKernelGGL((k_gro<U_, 256, OCC_, true, WM_SECTOR_NT, true, 0>),                \
+                           dim3((n + 255) / 256), dim3(256), 0, st, in, n * stride, off, lens, vd, \
+                           (u32)n, 256u, 16384u, out, n * stride, oo, ol, hd);               \
+    }});
+    GROW256(4, 3)
+#define GROW256B(U_, OCC_, BT_)                                                               \
+    vs.push_back({"w256 FLAT U=" #U_ " occ " #OCC_ " " #BT_ " threads", bytes, [&](hipStream_t st) { \
+        hipLaunchKernelGGL((k_gro<U_, 256, OCC_, true, WM_SECTOR_NT, true, 0, BT_>),           \
+                           dim3((n + 255) / 256), dim3(BT_), 0, st, in, n * stride, off, lens, vd, \
+                           (u32)n, 256u, 16384u, out, n * stride, oo, ol, hd);               \
+    }});
+    GROW256B(2, 6, 512) GROW256B(2, 8, 1024)
+    // windows of 64 in blocks of 512 threads (wave 0 parses, 7 waves read ahead
+    // and then stream)
+    vs.push_back({"k_gro<2,64,8,FLAT> ACX nt PF8, 512 threads", bytes, [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_gro<2, 64, 8, true, WM_SECTOR_NT, true, 8, 512>), dim3((n + 63) / 64),
+                           dim3(512), 0, st, in, n * stride, off, lens, vd, (u32)n, 64u, 16384u,
+                           out, n * stride, oo, ol, hd);
+    }});
+    vs.push_back({"k_gro<2,64,8,FLAT> ACX nt PF4, 512 threads", bytes, [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_gro<2, 64, 8, true, WM_SECTOR_NT, true, 4, 512>), dim3((n + 63) / 64),
+                           dim3(512), 0, st, in, n * stride, off, lens, vd, (u32)n, 64u, 16384u,
+                           out, n * stride, oo, ol, hd);
+    }});
+    vs.push_back({"k_gro<2,64,8,FLAT> ACX nt PF8 (shipped r03), again", bytes, [&](hipStream_t st) {
+        hipLaunchKernelGGL((k_gro<2, 64, 8, true, WM_SECTOR_NT, true, 8>), dim3((n + 63) / 64),
+                           dim3(256), 0, st, in, n * stride, off, lens, vd, (u32)n, 64u, 16384u,
+                           out, n * stride, oo, ol, hd);
     }});
     // (round 3's k_gro PROBE = 1, phases A-C + D1 alone: 69-91 us for this batch,
     // profiles/r03/kbench_lro_*.log; the knob left the product kernel in round 4)
@@ -2752,6 +2784,35 @@ int lro_main(uint64_t n, int rounds)
             CK(hipMemcpy(got.data(), out, n * stride, hipMemcpyDeviceToHost));
             std::printf("check %-44s output %s launch_gro's\n", v.name.c_str(),
                         ref == got ? "equals" : "DIFFERS FROM");
+        }
+    }
+    // every w256 variant's outputs (frames, offsets, lengths, heads) against
+    // the run-per-wave kernel's
+    {
+        std::vector<uint8_t> ref(n * stride), got(n * stride);
+        std::vector<uint64_t> ro(n), go(n);
+        std::vector<uint16_t> rl(n), gl(n);
+        std::vector<uint32_t> rh(n), gh(n);
+        auto grab = [&](std::vector<uint8_t>& b, std::vector<uint64_t>& o_, std::vector<uint16_t>& l_,
+                        std::vector<uint32_t>& h_) {
+            CK(hipMemcpy(b.data(), out, n * stride, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(o_.data(), oo, 8 * n, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(l_.data(), ol, 2 * n, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(h_.data(), hd, 4 * n, hipMemcpyDeviceToHost));
+        };
+        CK(hipMemsetAsync(out, 0, n * stride, s));
+        hipLaunchKernelGGL((k_gro<2, 256>), dim3((n + 255) / 256), dim3(256), 0, s, in, n * stride,
+                           off, lens, vd, (u32)n, 256u, 16384u, out, n * stride, oo, ol, hd);
+        grab(ref, ro, rl, rh);
+        for (auto& v : vs) {
+            if (v.name.rfind("w256 FLAT", 0) != 0)
+                continue;
+            CK(hipMemsetAsync(out, 0, n * stride, s));
+            CK(hipMemsetAsync(oo, 0xEE, 8 * n, s));
+            v.run(s);
+            grab(got, go, gl, gh);
+            std::printf("check %-44s outputs %s the run-per-wave kernel's\n", v.name.c_str(),
+                        ref == got && ro == go && rl == gl && rh == gh ? "equal" : "DIFFER FROM");
         }
     }
     CK(launch_gro(in, n * stride, off, lens, vd, (u32)n, 64u, 16384u, out, n * stride, oo, ol, hd,

@@ -61,7 +61,7 @@ def desc_case(ctx, O, seed):
 def gro_case(ctx, O, seed):
     rng = np.random.default_rng(seed)
     n = int(rng.integers(1, 6000))
-    window = int(rng.choice([1, 3, 7, 16, 33, 64, 64, 64]))
+    window = int(rng.choice([1, 3, 7, 16, 33, 64, 64, 64, 65, 100, 200, 256, 256]))
     max_len = int(rng.choice([200, 3000, 9000, 16384, 65535]))
     run_mean = float(rng.choice([1.5, 3.0, 6.0, 20.0]))
     buf, off, lens = synth.tcp_streams(n, run_mean=run_mean, seed=seed)
