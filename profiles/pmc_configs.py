@@ -196,6 +196,9 @@ def main():
             measure(f"gro_{L}_{n}",
                     lambda: ctx.gro(sb, off, lens, v, n, 64, 16384, o, oo, ol, hd, stream=stream),
                     2 * n * L)
+            measure(f"gro256_{L}_{n}",      # windows of 256: the FLAT form, 1,024 threads
+                    lambda: ctx.gro(sb, off, lens, v, n, 256, 16384, o, oo, ol, hd, stream=stream),
+                    2 * n * L)
             del sb, o
         else:
             raise SystemExit(f"unknown config {c}")
