@@ -15,7 +15,9 @@ barrier and the max-over-ranks reduction).
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
-Prints ONE JSON line on rank 0.
+Prints ONE compact JSON line on rank 0 (the contract's fields, roofline, CPU
+baseline, per-GPU rates and one scalar per side configuration, < 6 KB); the
+side measurements' full tables go to profiles/bench_extras_last.json.
 """
 from __future__ import annotations
 
@@ -806,9 +808,23 @@ def plugin_threads():
         try:
             r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "server_scaling.py")],
                                capture_output=True, text=True, timeout=240, env=env)
-            out[name] = json.loads(r.stdout.strip().splitlines()[-1])
+            d = json.loads(r.stdout.strip().splitlines()[-1])
+            if prof == "0":
+                d = drop_zero_counters(d)
+            out[name] = d
         except Exception as e:   # a side measurement: report, never fail the bench line
             out[name] = {"error": repr(e)[:200]}
+    return out
+
+
+def drop_zero_counters(series):
+    """A series run without the counting grid reports its GPU-side phase
+    fields as 0: keep only the fields it measured."""
+    out = {}
+    for k, v in series.items():
+        if isinstance(v, dict):
+            v = {kk: vv for kk, vv in v.items() if not (isinstance(vv, float) and vv == 0.0)}
+        out[k] = v
     return out
 
 
@@ -858,6 +874,105 @@ def plugin_tx_async():
         return json.loads(r.stdout.strip().splitlines()[-1])
     except Exception as e:   # a side measurement: report, never fail the bench line
         return {"error": repr(e)[:200]}
+
+
+EXTRAS_PATH = os.path.join(ROOT, "profiles", "bench_extras_last.json")
+LINE_MAX_BYTES = 6144   # the driver parses ONE stdout line; round 5's 29 KB was not parsed
+
+
+def _dig(d, *keys):
+    for k in keys:
+        if not isinstance(d, dict) or k not in d:
+            return None
+        d = d[k]
+    return round(d, 4) if isinstance(d, float) else d
+
+
+def side_scalars(line):
+    """One scalar per side configuration (C1, C3, C4, rooms, SURVEY §8f rows,
+    PCIe-inclusive, plugin bursts) for the compact line; the full tables go
+    to EXTRAS_PATH."""
+    g = lambda *ks: _dig(line, *ks)  # noqa: E731
+    s = {
+        "c1_64B_ms": g("c1_64B", "ms_per_launch"),
+        "c1_64B_cold_ms": g("c1_64B", "cold_ms"),
+        "c1_64B_cold_frac": g("c1_64B", "cold_frac_peak"),
+        "c1_64B_8M_gpkt_per_s": g("c1_64B_8M", "gpkt_per_s"),
+        "c2_sector_wb_frac": g("c2_sector_wb", "sector_frac_peak"),
+        "c2_fresh_cold_compute_frac": g("c2_fresh_cold", "compute_frac_peak"),
+        "c2_fresh_cold_verify_frac": g("c2_fresh_cold", "verify_frac_peak"),
+        "c2_1514B_step_gpkt_per_s": g("c2_1514B", "step_gpkt_per_s"),
+        "c3_fill_ms": g("c3_imix", "compute_ms"),
+        "c3_verify_ms": g("c3_imix", "verify_ms"),
+        "c3_fill_frac": g("c3_imix", "compute_frac_peak"),
+        "c3_verify_frac": g("c3_imix", "verify_frac_peak"),
+        "c3_fill_cold_frac": g("c3_imix", "compute_cold_frac_peak"),
+        "c4_ms_per_step": g("c4_shard", "ms_per_step"),
+        "c4_gpkt_per_s": g("c4_shard", "gpkt_per_s"),
+        "c4_compute_frac": g("c4_shard", "compute_frac"),
+        "c4_verify_frac": g("c4_shard", "verify_frac"),
+        "rooms_verify_ms": g("c2_rooms", "rooms_verify_ms"),
+        "rooms_fill_ms": g("c2_rooms", "rooms_compute_ms"),
+        "lro_w64_ms": g("rows_8f", "lro_ms"),
+        "lro_w256_ms": g("rows_8f", "lro_w256_ms"),
+        "copy_fill_ms": g("rows_8f", "copy_fill_ms"),
+        "classify_ms": g("rows_8f", "classify_ms"),
+        "pcie_pinned_verify_gib_per_s": g("pcie_inclusive", "verify_pinned", "gib_per_s"),
+        "pcie_pinned_fill_gib_per_s": g("pcie_inclusive", "compute_pinned", "gib_per_s"),
+        "pcie_pageable_verify_gib_per_s": g("pcie_inclusive", "verify_pageable", "gib_per_s"),
+        "burst_registered_server_verify_us": g("plugin_bursts", "registered_server", "64x1500B",
+                                               "verify_us"),
+        "burst_pageable_direct_verify_us": g("plugin_bursts", "pageable_direct", "64x1500B",
+                                             "verify_us"),
+        "burst_registered_direct_verify_us": g("plugin_bursts", "registered_direct", "64x1500B",
+                                               "verify_us"),
+        "rx_async_registered_blocked_us": g("plugin_rx_async", "registered_group0",
+                                            "blocked_us_median"),
+        "rx_async_software_blocked_us": g("plugin_rx_async", "software_path_registered",
+                                          "blocked_us_median"),
+        "tx_async_registered_send_pkts_us": g("plugin_tx_async", "registered_groupdefault",
+                                              "send_pkts_us_median"),
+        "threads16_shipped_us": g("plugin_threads", "shipped", "threads_16", "us_per_call"),
+        "threads16_pinned_us": g("plugin_threads", "pinned", "threads_16", "us_per_call"),
+        "threads24_shipped_us": g("plugin_threads", "shipped", "threads_24", "us_per_call"),
+    }
+    return {k: v for k, v in s.items() if v is not None}
+
+
+def compact_line(line, extras_path=None):
+    """The ONE JSON line the driver parses: the contract's fields, the
+    roofline and CPU baseline, per-GPU rates and one scalar per side
+    configuration, well under LINE_MAX_BYTES.  The full side tables are in
+    `extras_path` (written beside it)."""
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+            "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "gib_per_s",
+            "settle_s", "corrupted_frames_detected")
+    out = {k: line[k] for k in keep if k in line}
+    rf = line.get("roofline", {})
+    out["roofline"] = {k: rf[k] for k in ("bound", "kernel", "achieved", "peak", "unit", "frac",
+                                          "traffic", "traffic_source",
+                                          "bytes_per_launch_algorithmic", "avg_launch_ms",
+                                          "tx_write_mode") if k in rf}
+    if "kernels_ms" in line:
+        out["kernels_ms"] = {k: line["kernels_ms"][k] for k in ("compute", "verify")}
+    cb = line.get("cpu_baseline")
+    if cb:
+        out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample",
+                                                  "gib_per_s", "cpu_model") if k in cb}
+        mc = cb.get("multi_core")
+        if mc:
+            out["cpu_baseline"]["multi_core"] = {k: mc[k] for k in ("value", "unit", "cores",
+                                                                    "gib_per_s") if k in mc}
+    out["per_gpu"] = [{k: (round(v, 4) if isinstance(v, float) else v) for k, v in p.items()
+                       if k in ("rank", "device", "gpkt_per_s", "frac_peak",
+                                "bad_frames_detected", "corrupted_frames")}
+                      for p in line.get("per_gpu", [])]
+    side = side_scalars(line)
+    if side:
+        out["side"] = side
+    if extras_path:
+        out["extras_file"] = os.path.relpath(extras_path, ROOT)
+    return out
 
 
 def main():
@@ -981,7 +1096,18 @@ def main():
             line["server_poll_cost"] = server_poll_cost()
     ctx.close()
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        extras = None
+        if any(k not in compact_line(line) for k in line):
+            # the full tables beside the line (never in it: the driver parses
+            # ONE line, and round 5's 29 KB line was left unparsed)
+            extras = EXTRAS_PATH
+            try:
+                with open(extras, "w") as f:
+                    json.dump(line, f)
+            except OSError as e:
+                print(f"warning: extras not written: {e}", file=sys.stderr)
+                extras = None
+        print(json.dumps(compact_line(line, extras)), flush=True)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

@@ -144,10 +144,19 @@ int         gcs_device_count(int *count);
  * max_frames / max_bytes size the staging used by the host-memory entry points
  * (0 = no staging: only the *_dev functions may be used). */
 int gcs_ctx_create(gcs_ctx **out, int device, uint32_t max_frames, uint64_t max_bytes);
+/* Releases everything whatever fails, and returns the first failure (a device
+ * fault that surfaces while the context's work drains is reported here, to
+ * its owner, not to the next caller). */
 int gcs_ctx_destroy(gcs_ctx *ctx);
 int gcs_ctx_device(const gcs_ctx *ctx, int *device);
 int gcs_ctx_stream(const gcs_ctx *ctx, void **stream);   /* hipStream_t */
 int gcs_sync(gcs_ctx *ctx);                               /* wait for ctx stream */
+/* Health check of a device (tests run it after every GPU test; an mTCP
+ * thread may after a failed call): every stream of the process drained with
+ * no fault, twice, 1 ms apart (a fault reaches the process asynchronously);
+ * with no context holding a burst-server ring, no server grid resident.
+ * GCS_EHIP with gcs_last_hip_error() naming what failed. */
+int gcs_device_check(int device);
 
 /* Burst server (on = 1): host batches small enough for direct mode (the
  * kernel reads pinned staging over PCIe: an mTCP burst) are served by a
@@ -374,10 +383,12 @@ int gcs_compute_ptrs_async(gcs_ctx *ctx, uint8_t *const *pkts, const uint16_t *l
  * context's request ring and complete in posting order.
  * A gcs_wait that fails (no answer from the GPU) cancels every pending async
  * request: their outputs and frames are never written.  That failure is the
- * report for every cancelled request of the kind (fill or verify) of the
- * ticket it waited for; a cancelled request of the other kind is reported
- * once, by the first later gcs_wait for a ticket of its kind that covers it
- * (GCS_EHIP).  Requests posted after the failure are never reported for it. */
+ * report for the cancelled requests of the kind (fill or verify) of the
+ * ticket it waited for, up to that ticket; every other cancelled request (a
+ * later one of that kind, or one of the other kind) is reported once, by the
+ * first later gcs_wait for a ticket of its kind that covers it -- its own
+ * ticket included (GCS_EHIP).  Requests posted after the failure are never
+ * reported for it. */
 int gcs_verify_ptrs_async(gcs_ctx *ctx, uint8_t *const *pkts, const uint16_t *len,
                           uint32_t n, uint8_t *verdict, uint32_t flags, uint64_t *ticket);
 int gcs_wait(gcs_ctx *ctx, uint64_t ticket);

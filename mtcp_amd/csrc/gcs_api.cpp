@@ -253,11 +253,10 @@ class ServerHub {
   public:
     static ServerHub* get(int device)
     {
-        static std::mutex mu;
-        static ServerHub* hubs[64] = {};
-        if (device < 0 || device >= 64)
+        if (device < 0 || device >= kMaxDevices)
             return nullptr;
-        std::lock_guard<std::mutex> lk(mu);
+        std::lock_guard<std::mutex> lk(registry_mu());
+        ServerHub** hubs = registry();
         if (!hubs[device]) {
             // process lifetime: never freed (a static destructor would run
             // after the HIP runtime may have gone)
@@ -267,6 +266,37 @@ class ServerHub {
             hubs[device] = h.release();
         }
         return hubs[device];
+    }
+
+    // The device's hub if one was made (gcs_device_check), else nullptr.
+    static ServerHub* peek(int device)
+    {
+        if (device < 0 || device >= kMaxDevices)
+            return nullptr;
+        std::lock_guard<std::mutex> lk(registry_mu());
+        return registry()[device];
+    }
+
+    // gcs_device_check: with no ring joined, no grid may be resident and the
+    // hub's stream must be idle (a grid outliving its contexts would serve
+    // request lines whose frames were freed).
+    int check_idle()
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (mask_ != 0)
+            return GCS_OK;
+        if (launched_.load(std::memory_order_relaxed)) {
+            std::snprintf(g_hip_err, sizeof g_hip_err,
+                          "burst server: a grid is resident with no ring joined");
+            return GCS_EHIP;
+        }
+        const hipError_t e = hipStreamQuery(stream_);
+        if (e == hipErrorNotReady) {
+            std::snprintf(g_hip_err, sizeof g_hip_err,
+                          "burst server: the hub stream is busy with no ring joined");
+            return GCS_EHIP;
+        }
+        return e == hipSuccess ? GCS_OK : hip_fail(e, "burst server stream");
     }
 
     // A context joins: ring index in *r, or GCS_ERANGE when kHubRings
@@ -288,17 +318,20 @@ class ServerHub {
         std::memset(&rq_->prof[k], 0, sizeof rq_->prof[k]);
         // every slot reads as holding `start` (done): a slot left at 0 would
         // read as NEWER than the next request near the 32-bit wrap, and be
-        // skipped as done
-        for (auto& sl : rq_->req[k])
+        // skipped as done (line A whole: its tag half carries start too)
+        for (auto& sl : rq_->req[k]) {
             sl.a.seq = start;
+            sl.a.n = gcs::server_tag(start) << 16;
+        }
         if (dev_mailbox_)
             _mm_sfence();                 // write-combined over the BAR
         // ... and every block's ack reads as `start` (nothing served yet): an
         // ack left at 0 would read as NEWER than a request >= 2^31 past it,
         // and complete an in-place request before its release fence
-        // (test-only GCS_SERVER_ACK_SKEW: join with acks that stale, as after
-        // 2^31 requests that wrote no frame; the grid must refresh them)
-        const char* sk = std::getenv("GCS_SERVER_ACK_SKEW");
+        // (test-only, GCS_FAULT_INJECT=ack_skew with GCS_SERVER_ACK_SKEW: join
+        // with acks that stale, as after 2^31 requests that wrote no frame;
+        // the grid must refresh them)
+        const char* sk = fault("ack_skew") ? std::getenv("GCS_SERVER_ACK_SKEW") : nullptr;
         const uint32_t skew = sk ? (uint32_t)std::strtoul(sk, nullptr, 0) : 0u;
         for (auto& a : mb_->ring[k].ack)
             a.v = start + skew;
@@ -512,6 +545,17 @@ class ServerHub {
     }
 
     static constexpr uint32_t kMaxPolls = 1u << 22;   // hard bound beside the clock
+    static constexpr int kMaxDevices = 64;
+    static std::mutex& registry_mu()
+    {
+        static std::mutex m;
+        return m;
+    }
+    static ServerHub** registry()
+    {
+        static ServerHub* hubs[kMaxDevices] = {};
+        return hubs;
+    }
     std::mutex mu_;
     gcs::HubMailbox* mb_ = nullptr;       // host view
     gcs::HubMailbox* dmb_ = nullptr;      // device view
@@ -535,7 +579,25 @@ class ServerHub {
 // context's).
 class BurstServer {
   public:
-    ~BurstServer()
+    ~BurstServer() { (void)shutdown(); }
+
+    // Complete what is posted, then leave the hub (its grid stops; another
+    // ring's next request starts a fresh one).  The first failure is returned
+    // -- gcs_ctx_destroy and gcs_ctx_set_burst_server(ctx, 0) report it -- so
+    // a device fault at teardown is charged to this context, not to the next
+    // caller that happens to check.
+    int shutdown()
+    {
+        if (!hub_ || r_ < 0)
+            return GCS_OK;
+        print_stats();
+        const int rc = wait(posted_);
+        const int rc2 = hub_->leave(r_);
+        r_ = -1;
+        return rc ? rc : rc2;
+    }
+
+    void print_stats() const
     {
         if (prof_n_ && hub_->print()) {
             gcs_server_stats st;
@@ -550,10 +612,6 @@ class BurstServer {
                          st.poll_us, st.seen_poll_us, st.acquire_us, st.frames_us,
                          st.records_us, st.release_us, st.seen_skew_us, st.block_serve_us,
                          st.cold_frac);
-        }
-        if (hub_ && r_ >= 0) {
-            (void)wait(posted_);
-            (void)hub_->leave(r_);
         }
     }
 
@@ -589,6 +647,12 @@ class BurstServer {
              uint32_t n, bool compute, uint32_t flags, uint8_t* code, uint32_t* csum,
              bool in_place, bool dev_frames, uint32_t* ticket)
     {
+        const uint64_t fa = reinterpret_cast<uint64_t>(frames);
+        if ((fa & ~gcs::kAddrMask) || n > (uint32_t)gcs::kSlotFrames) {
+            std::snprintf(g_hip_err, sizeof g_hip_err,
+                          "burst server: frames above 2^48 or more than one request's frames");
+            return GCS_EINVAL;
+        }
         const uint32_t q = gcs::server_next(posted_);
         Req& r = req_[q % gcs::kServerSlots];
         if (r.pending) {                  // the slot's previous request must be done
@@ -603,37 +667,47 @@ class BurstServer {
                                                                                      // of an older request
         const uint32_t mode = (compute ? 1u : 0u) | (flags << 1) |
                               (dev_frames ? gcs::kModeDevFrames : 0u);
+        // every line carries the request in both 8 B halves (gcs_internal.h):
+        // the tag in the top 16 bits of the address / offset and beside n
+        const uint64_t tag = gcs::server_tag(q);
+        auto tagged = [&](uint64_t a) {
+            // an offset past 2^48 cannot lie inside the frames (a region is
+            // < 64 GiB): it is kept out of bounds, so the kernel flags the frame
+            return (a > gcs::kAddrMask ? gcs::kAddrMask : a) | tag << gcs::kTagShift;
+        };
+        const uint64_t fb = fa | tag << gcs::kTagShift;
+        const uint32_t na = n | (uint32_t)tag << 16;
         if (dev_) {
             // Device memory over the BAR, write-combined: each 16 B line goes
-            // out as ONE aligned 16 B store carrying its seq (a line is read
-            // in one piece), the descriptors and line B first, then (sfence)
-            // line A, then sfence again so the request leaves the
-            // write-combining buffers now.
-            for (uint32_t i = 0; i < n; i++)
+            // out as ONE aligned 16 B store, the descriptors and line B first,
+            // then (sfence) line A, then sfence again so the request leaves
+            // the write-combining buffers now.
+            for (uint32_t i = 0; i < n; i++) {
+                const uint64_t o = tagged(off[i]);
                 _mm_store_si128(reinterpret_cast<__m128i*>(&sl.desc[i]),
-                                _mm_set_epi32((int)q, (int)len[i], (int)(uint32_t)(off[i] >> 32),
-                                              (int)(uint32_t)off[i]));
-            const uint64_t fa = reinterpret_cast<uint64_t>(frames);
+                                _mm_set_epi32((int)q, (int)len[i], (int)(uint32_t)(o >> 32),
+                                              (int)(uint32_t)o));
+            }
             _mm_store_si128(reinterpret_cast<__m128i*>(&sl.b),
                             _mm_set_epi32((int)q, (int)(uint32_t)(bytes / 16),
-                                          (int)(uint32_t)(fa >> 32), (int)(uint32_t)fa));
+                                          (int)(uint32_t)(fb >> 32), (int)(uint32_t)fb));
             _mm_sfence();
             r = Req{q, n, compute, in_place, true, code, csum, 0, std::chrono::steady_clock::now()};
             _mm_store_si128(reinterpret_cast<__m128i*>(&sl.a),
-                            _mm_set_epi32((int)mode, (int)n, 0, (int)q));
+                            _mm_set_epi32((int)mode, (int)na, 0, (int)q));
             _mm_sfence();
         } else {
             // each 16 B line: its fields, then its seq (x86 keeps the order)
             for (uint32_t i = 0; i < n; i++) {
                 gcs::ServerDesc& d = sl.desc[i];
-                d.off = off[i];
+                d.off = tagged(off[i]);
                 d.len = len[i];
                 __atomic_store_n(&d.seq, q, __ATOMIC_RELEASE);
             }
-            sl.b.frames = reinterpret_cast<uint64_t>(frames);
+            sl.b.frames = fb;
             sl.b.bytes16 = (uint32_t)(bytes / 16);
             __atomic_store_n(&sl.b.seq, q, __ATOMIC_RELEASE);
-            sl.a.n = n;
+            sl.a.n = na;
             sl.a.mode = mode;
             sl.a.cmd = 0;
             r = Req{q, n, compute, in_place, true, code, csum, 0, std::chrono::steady_clock::now()};
@@ -705,8 +779,13 @@ class BurstServer {
             bool all = r.have == r.n;
             if (all && r.in_place)
                 for (int k = 0; k < nb; k++) {
+                    // an ack counts only inside [r.q, posted_]: one past the
+                    // last request posted is stale (a ring joined with old
+                    // acks, GCS_FAULT_INJECT=ack_skew) and proves nothing
+                    // about r's writes
                     const int b = gcs::server_block(r.q, (uint32_t)k * gcs::kServerFPB);
-                    if ((int32_t)(__atomic_load_n(&mb_->ack[b].v, __ATOMIC_ACQUIRE) - r.q) < 0)
+                    const uint32_t ak = __atomic_load_n(&mb_->ack[b].v, __ATOMIC_ACQUIRE);
+                    if ((int32_t)(ak - r.q) < 0 || (int32_t)(posted_ - ak) < 0)
                         all = false;
                 }
             if (all)
@@ -962,26 +1041,37 @@ hipStream_t pick_stream(gcs_ctx* ctx, void* stream)
     return stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
 }
 
-void free_slot(Slot& s)
+// Teardown keeps going past a failure (everything is released) and reports
+// the first one: rc stays the first non-OK status.
+void keep_first(int& rc, hipError_t e, const char* what)
 {
-    if (s.h_frames) (void)hipHostFree(s.h_frames);
-    if (s.h_off) (void)hipHostFree(s.h_off);
-    if (s.h_len) (void)hipHostFree(s.h_len);
-    if (s.h_code) (void)hipHostFree(s.h_code);
-    if (s.h_csum) (void)hipHostFree(s.h_csum);
-    if (s.h_hash) (void)hipHostFree(s.h_hash);
-    if (s.h_queue) (void)hipHostFree(s.h_queue);
-    if (s.d_hash) (void)hipFree(s.d_hash);
-    if (s.d_queue) (void)hipFree(s.d_queue);
-    if (s.d_frames) (void)hipFree(s.d_frames);
-    if (s.d_off) (void)hipFree(s.d_off);
-    if (s.d_len) (void)hipFree(s.d_len);
-    if (s.v_frames) (void)hipFree(s.v_frames);
-    if (s.d_code) (void)hipFree(s.d_code);
-    if (s.d_csum) (void)hipFree(s.d_csum);
-    if (s.done) (void)hipEventDestroy(s.done);
-    if (s.stream) (void)hipStreamDestroy(s.stream);
+    if (e != hipSuccess && rc == GCS_OK)
+        rc = hip_fail(e, what);
+}
+
+int free_slot(Slot& s)
+{
+    int rc = GCS_OK;
+    if (s.stream) keep_first(rc, hipStreamSynchronize(s.stream), "slot stream sync");
+    if (s.h_frames) keep_first(rc, hipHostFree(s.h_frames), "hipHostFree");
+    if (s.h_off) keep_first(rc, hipHostFree(s.h_off), "hipHostFree");
+    if (s.h_len) keep_first(rc, hipHostFree(s.h_len), "hipHostFree");
+    if (s.h_code) keep_first(rc, hipHostFree(s.h_code), "hipHostFree");
+    if (s.h_csum) keep_first(rc, hipHostFree(s.h_csum), "hipHostFree");
+    if (s.h_hash) keep_first(rc, hipHostFree(s.h_hash), "hipHostFree");
+    if (s.h_queue) keep_first(rc, hipHostFree(s.h_queue), "hipHostFree");
+    if (s.d_hash) keep_first(rc, hipFree(s.d_hash), "hipFree");
+    if (s.d_queue) keep_first(rc, hipFree(s.d_queue), "hipFree");
+    if (s.d_frames) keep_first(rc, hipFree(s.d_frames), "hipFree");
+    if (s.d_off) keep_first(rc, hipFree(s.d_off), "hipFree");
+    if (s.d_len) keep_first(rc, hipFree(s.d_len), "hipFree");
+    if (s.v_frames) keep_first(rc, hipFree(s.v_frames), "hipFree");
+    if (s.d_code) keep_first(rc, hipFree(s.d_code), "hipFree");
+    if (s.d_csum) keep_first(rc, hipFree(s.d_csum), "hipFree");
+    if (s.done) keep_first(rc, hipEventDestroy(s.done), "hipEventDestroy");
+    if (s.stream) keep_first(rc, hipStreamDestroy(s.stream), "hipStreamDestroy");
     s = Slot();
+    return rc;
 }
 
 int alloc_slot(Slot& s, uint32_t frames, uint64_t bytes)
@@ -1508,27 +1598,57 @@ try {
     return GCS_OK;
 } GCS_CATCH
 
+// Everything is released whatever fails; the first failure is returned (a
+// device fault surfacing at teardown is this context's, not the next
+// caller's).  The ring leaves the grid before any staging it served is freed.
 int gcs_ctx_destroy(gcs_ctx* ctx)
 try {
     if (!ctx)
         return GCS_EINVAL;
+    int rc = GCS_OK;
     {
         DeviceGuard g(ctx->device);
-        ctx->server.reset();   // its requests complete; the ring leaves the grid
+        if (ctx->server) {
+            rc = ctx->server->shutdown();   // its requests complete; the ring leaves the grid
+            ctx->server.reset();
+        }
         for (auto& a : ctx->areq)
-            if (a.h_stage) (void)(a.stage_dev ? hipFree(a.h_stage) : hipHostFree(a.h_stage));
+            if (a.h_stage)
+                keep_first(rc, a.stage_dev ? hipFree(a.h_stage) : hipHostFree(a.h_stage),
+                           "async staging free");
         for (auto& s : ctx->slot) {
-            if (s.stream)
-                (void)hipStreamSynchronize(s.stream);
-            free_slot(s);
+            const int e = free_slot(s);
+            if (rc == GCS_OK) rc = e;
         }
         if (ctx->stream) {
-            (void)hipStreamSynchronize(ctx->stream);
-            (void)hipStreamDestroy(ctx->stream);
+            keep_first(rc, hipStreamSynchronize(ctx->stream), "context stream sync");
+            keep_first(rc, hipStreamDestroy(ctx->stream), "hipStreamDestroy");
         }
-
     }
     delete ctx;
+    return rc;
+} GCS_CATCH
+
+int gcs_device_check(int device)
+try {
+    int count = 0;
+    int rc = gcs_device_count(&count);
+    if (rc)
+        return rc;
+    if (device < 0 || device >= count)
+        return GCS_ENODEV;
+    DeviceGuard g(device);
+    if (ServerHub* h = ServerHub::peek(device)) {
+        rc = h->check_idle();
+        if (rc)
+            return rc;
+    }
+    HIP_TRY(hipDeviceSynchronize());
+    // a fault is reported to the process asynchronously (its interrupt is
+    // handled after the faulting kernel may have completed): look again
+    // after a moment, so it is charged to the work that caused it
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    HIP_TRY(hipDeviceSynchronize());
     return GCS_OK;
 } GCS_CATCH
 
@@ -1767,8 +1887,9 @@ try {
         return GCS_EINVAL;
     DeviceGuard g(ctx->device);
     if (!on) {
+        const int rc = ctx->server ? ctx->server->shutdown() : GCS_OK;
         ctx->server.reset();
-        return GCS_OK;
+        return rc;
     }
     if (ctx->server)
         return GCS_OK;
@@ -1931,19 +2052,22 @@ int async_wait(gcs_ctx* ctx, uint32_t q, bool report = true)
             // addresses here).  The staging slot itself is reused only after
             // its server request completes (BurstServer::post waits for it
             // first).  This failure is the report for every cancelled request
-            // of the waiter's kind (the plugin drops the rest of a burst when
-            // one of its waits fails); one of the other kind is reported
-            // once, to the first later wait of its kind that covers it.
+            // of the waiter's kind up to the ticket it waited for; any other
+            // cancelled request -- a later one of its kind, or one of the
+            // other kind -- is reported once, to the first later wait of its
+            // kind that covers it (a wait for its own ticket included: it
+            // never reads as done).
             const int kind = ticket_kind(ctx, q);
             for (auto& a : ctx->areq) {
-                const bool own = kind < 0 || kind == a.compute;
+                const bool reported = (kind < 0 || kind == a.compute) &&
+                                      (int32_t)(q - a.q) >= 0;
                 if (a.pending) {
                     a.pending = false;
-                    a.cancelled = !own;
+                    a.cancelled = !reported;
                     std::fill(a.ptrs.begin(), a.ptrs.end(), nullptr);
                     a.status = nullptr;
                     a.csums = nullptr;
-                } else if (own) {
+                } else if (reported) {
                     a.cancelled = false;        // reported by this failure
                 }
             }

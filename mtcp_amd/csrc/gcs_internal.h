@@ -56,23 +56,34 @@ constexpr int kServerSlots = 8;
 constexpr int kSlotFrames = 512;         // frames per request
 constexpr int kServerMaxFrames = 4096;   // a larger synchronous batch: several requests
 constexpr int kHubRings = 32;            // contexts one grid serves (mTCP threads per GPU)
+//
+// Each 16 B line goes out as ONE store, but write-combined BAR memory may land
+// a partial line as two 8 B halves in either order (Intel SDM 11.3.1), so a
+// poll may read one half new and the other from the request that used the
+// slot 8 requests earlier.  Every line therefore carries its request in BOTH
+// halves: line A the tag (server_tag) beside n, line B and the descriptors
+// the tag in the top 16 bits of their 48-bit address / offset (kTagShift).
+// A poll takes a line as written only when both halves agree.
 struct alignas(16) ServerReqA {
     uint32_t seq;                       // request number (written last)
     uint32_t cmd;                       // unused (0)
-    uint32_t n;                         // frames
+    uint32_t n;                         // frames | server_tag(seq) << 16
     uint32_t mode;                      // bit 0: compute (TX fill); bits 1..: flags
 };
 struct alignas(16) ServerReqB {
-    uint64_t frames;                    // device address of the frame buffer
+    uint64_t frames;                    // device address of the frame buffer (48 bits)
+                                        // | server_tag(seq) << kTagShift
     uint32_t bytes16;                   // its size / 16
     uint32_t seq;
 };
 struct alignas(16) ServerDesc {
-    uint64_t off;
+    uint64_t off;                       // offset (48 bits) | server_tag(seq) << kTagShift
     uint16_t len;
     uint16_t pad;
     uint32_t seq;
 };
+constexpr int kTagShift = 48;
+constexpr uint64_t kAddrMask = (1ull << kTagShift) - 1;
 struct alignas(64) ServerLine {
     uint32_t v;
     uint32_t pad[15];
@@ -162,6 +173,13 @@ __host__ __device__ inline uint32_t server_next(uint32_t q)
 {
     q += 1;
     return (q & 0xFFFFu) == 0 ? q + 1 : q;
+}
+
+// Request q's 16-bit tag (its records and the second half of each request
+// line carry it; never 0, see server_next).
+__host__ __device__ inline uint32_t server_tag(uint32_t q)
+{
+    return q & 0xFFFFu;
 }
 
 // Request q starts at block 2q mod kServerBlocks and goes out kServerFPB

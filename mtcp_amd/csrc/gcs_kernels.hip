@@ -341,6 +341,22 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
                 u32x4 v = {0, 0, 0, 0};
                 if (src)
                     v = *src;
+                // Whole lines only (gcs_internal.h: the host's 16 B lines may
+                // land as two 8 B halves).  A line A whose halves name
+                // different requests reads as the request before the one
+                // expected (look again); n loses its tag.  Line B and the
+                // descriptors keep their tag for the torn test below, and
+                // lose it from the address / offset.
+                const bool line_a = ahead || (lane == 0 && !follow);
+                const bool line_bd = !ahead && hot && lane >= 1 && lane < kLanes;
+                const bool bd_whole = (v.y >> 16) == server_tag(q);
+                if (line_a) {
+                    if ((v.z >> 16) != server_tag(v.x))
+                        v.x = (ahead ? qk : q) - 1u;
+                    v.z &= 0xFFFFu;
+                } else if (line_bd) {
+                    v.y &= 0xFFFFu;
+                }
                 if (PROF) {
                     const uint64_t back = clock_after_vmem();
                     p_issue = now;
@@ -358,10 +374,11 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
                     dn = (q & 1u) ? v.z : v.x;
                 }
                 const uint32_t x0 = __shfl(dq, 0), z0 = __shfl(dn, 0);
-                // a consistent poll has seq q in line B and in the descriptor
-                // lines of the block's frames: each lane checks its own line
-                const bool torn = hot && lane >= 1 && lane < kLanes &&
-                                  first + (lane >= 2 ? lane - 2 : 0) < z0 && v.w != q;
+                // a consistent poll has request q whole in line B and in the
+                // descriptor lines of the block's frames: each lane checks its
+                // own line, both halves
+                const bool torn = line_bd && first + (lane >= 2 ? lane - 2 : 0) < z0 &&
+                                  (v.w != q || !bd_whole);
                 const bool ok = __ballot(torn) == 0;
                 uint32_t act = IDLE;
                 if (hot) {
@@ -466,7 +483,8 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
             // tcp_in.c:1237 side effect
             writes = compute ? !(flags & GCS_CF_NO_INPLACE)
                              : (flags & GCS_VF_ZERO_BAD_TCP_CHECK) != 0;
-            uint8_t* frames = reinterpret_cast<uint8_t*>((uint64_t)b.x | ((uint64_t)b.y << 32));
+            uint8_t* frames = reinterpret_cast<uint8_t*>((uint64_t)b.x |
+                                                         ((uint64_t)(b.y & 0xFFFFu) << 32));
             const uint64_t bytes = (uint64_t)b.z * 16;
             const uint4 d0 = s_line[2 + grp];
             uint64_t* rec = rm->res[q % kServerSlots].rec;
@@ -482,10 +500,11 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
                 const bool here = i < n;                 // group-uniform
                 uint4 d = d0;
                 if (pass != 0 && here) {
+                    // written before line A's fence: whole once A was seen
                     const u32x4 w = *reinterpret_cast<const volatile u32x4*>(&sl->desc[i]);
                     d = make_uint4(w.x, w.y, w.z, w.w);
                 }
-                const uint64_t o = (uint64_t)d.x | ((uint64_t)d.y << 32);
+                const uint64_t o = (uint64_t)d.x | ((uint64_t)(d.y & 0xFFFFu) << 32);
                 const u32 len = d.z & 0xFFFFu;
                 const bool ok = (o & 15) == 0 && o <= bytes && len <= bytes - o;
                 uint8_t* f = frames + (ok ? o : 0);

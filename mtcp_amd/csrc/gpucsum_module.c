@@ -527,6 +527,11 @@ static void rx_wait(struct gthr *g, struct rx_if *r, int32_t index)
 			break;
 		}
 	hi = (int32_t)((grp + 1) * G) < r->n ? (int32_t)((grp + 1) * G) : r->n;
+	if (rc && r->ngroups > 0 && k + 1 < r->ngroups && r->ticket[r->ngroups - 1])
+		/* the failed wait cancelled the burst's later groups too and left
+		 * them to be reported by a wait that covers them: take that report
+		 * here, so no wait of a later burst inherits it */
+		(void)gcs_wait(g->gcs, r->ticket[r->ngroups - 1]);
 	if (rc)
 		rx_unverified(g, r, (int32_t)r->ready, r->n, rc);   /* the rest of the burst */
 	else

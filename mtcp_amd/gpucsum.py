@@ -73,6 +73,7 @@ def lib() -> C.CDLL:
             "gcs_ctx_device": (i, [vp, C.POINTER(i)]),
             "gcs_ctx_stream": (i, [vp, C.POINTER(vp)]),
             "gcs_sync": (i, [vp]),
+            "gcs_device_check": (i, [i]),
             "gcs_host_alloc": (i, [C.POINTER(vp), u64]),
             "gcs_host_free": (i, [vp]),
             "gcs_host_register": (i, [vp, u64]),
@@ -149,6 +150,12 @@ def check(rc: int, what: str = "") -> None:
         L = lib()
         raise GcsError(f"{what}: {L.gcs_strerror(rc).decode()} ({rc}) "
                        f"{L.gcs_last_hip_error().decode()}", rc)
+
+
+def device_check(device: int = 0) -> None:
+    """gcs_device_check: every stream drained without a fault and no burst
+    server grid resident without a ring; raises GcsError otherwise."""
+    check(lib().gcs_device_check(device), "gcs_device_check")
 
 
 def device_count() -> int:

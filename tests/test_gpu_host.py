@@ -197,6 +197,7 @@ def test_registered_rooms_in_place(torch_dev, monkeypatch, server, start, skew):
     if start is not None:
         monkeypatch.setenv("GCS_SERVER_SEQ_START", str(start))
     if skew is not None:
+        monkeypatch.setenv("GCS_FAULT_INJECT", "ack_skew")      # test-only knob, gated
         monkeypatch.setenv("GCS_SERVER_ACK_SKEW", str(skew))
     L = gpucsum.lib()
     O = Oracle()
@@ -429,6 +430,58 @@ def test_async_fill_without_server_is_synchronous(torch_dev):
     assert t.value == 0                     # done on return
     np.testing.assert_array_equal(st, rst)
     np.testing.assert_array_equal(buf, ref)
+
+
+def test_failed_wait_reports_later_requests_to_their_own_wait(torch_dev, monkeypatch):
+    """A failed gcs_wait reports the cancelled fills up to its ticket; fills
+    posted after that ticket stay cancelled and fail their OWN wait once
+    (GCS_EHIP: their outputs were never written), then read as done; a
+    cancelled verify is reported once to the first verify wait covering it.
+    Nothing reports success for results it never produced."""
+    import ctypes as C
+    L = gpucsum.lib()
+    L.gcs_compute_ptrs_async.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                         C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64)]
+    L.gcs_verify_ptrs_async.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                        C.c_void_p, C.c_uint32, C.POINTER(C.c_uint64)]
+    L.gcs_wait.argtypes = [C.c_void_p, C.c_uint64]
+    EHIP = gpucsum.K["GCS_EHIP"]
+    monkeypatch.setenv("GCS_FAULT_INJECT", "none")        # arms the context's fault hooks
+    buf, off, lens = synth.packed_frames(synth.imix_lengths(80, seed=171), seed=172)
+    ptrs = (C.c_void_p * len(off))(*[buf.ctypes.data + int(o) for o in off])
+    st = np.zeros(len(off), np.uint8)
+    vd = np.zeros(len(off), np.uint8)
+    with gpucsum.Context(0, max_frames=1024, max_bytes=4 << 20) as c:
+        c.set_burst_server(True)
+        tk = []
+        for k in range(5):                    # fills f0..f3 and one verify (k = 2)
+            t = C.c_uint64()
+            p = C.cast(C.byref(ptrs, 8 * 16 * k), C.c_void_p)
+            if k == 2:
+                gpucsum.check(L.gcs_verify_ptrs_async(c.h, p, lens.ctypes.data + 32 * k, 16,
+                                                      vd.ctypes.data + 16 * k, 0, C.byref(t)))
+            else:
+                gpucsum.check(L.gcs_compute_ptrs_async(c.h, p, lens.ctypes.data + 32 * k, 16,
+                                                       st.ctypes.data + 16 * k, None,
+                                                       C.byref(t)))
+            assert t.value != 0
+            tk.append(t.value)
+        monkeypatch.setenv("GCS_FAULT_INJECT", "wait")
+        assert L.gcs_wait(c.h, tk[1]) == EHIP          # reports f0, f1
+        monkeypatch.setenv("GCS_FAULT_INJECT", "none")
+        assert L.gcs_wait(c.h, tk[3]) == EHIP          # f2 (k = 3): its own wait
+        assert L.gcs_wait(c.h, tk[4]) == EHIP          # f3 (k = 4): its own wait
+        assert L.gcs_wait(c.h, tk[4]) == 0             # reported once
+        assert L.gcs_wait(c.h, tk[2]) == EHIP          # the verify, to a verify wait
+        assert L.gcs_wait(c.h, tk[2]) == 0
+        # the ring serves on: a fresh fill completes exactly
+        ref = buf.copy()
+        rst, _ = Oracle().compute_batch(ref, off, lens)
+        t = C.c_uint64()
+        gpucsum.check(L.gcs_compute_ptrs_async(c.h, ptrs, lens.ctypes.data, 16, st.ctypes.data,
+                                               None, C.byref(t)))
+        gpucsum.check(L.gcs_wait(c.h, t.value))
+        np.testing.assert_array_equal(st[:16], rst[:16])
 
 
 @pytest.mark.parametrize("life_us", [2000, 150])
