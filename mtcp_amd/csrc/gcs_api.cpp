@@ -23,6 +23,9 @@
 #include <vector>
 
 #include <emmintrin.h>
+#include <sched.h>
+#include <sys/prctl.h>
+#include <time.h>
 
 #include "gcs_internal.h"
 
@@ -631,6 +634,7 @@ class BurstServer {
         mb_ = hub_->ring(r_);
         rq_ = hub_->reqs(r_);
         dev_ = hub_->dev_mailbox();
+        read_wait_knobs();
         return GCS_OK;
     }
 
@@ -763,6 +767,44 @@ class BurstServer {
         std::chrono::steady_clock::time_point t0;    // posted
     };
 
+    // One step of the host's wait for a request, `waited` into it.  Spin
+    // (pause) first; past GCS_SERVER_SPIN_US, GCS_SERVER_WAIT=yield gives the
+    // CPU to another runnable thread at each step (sched_yield), and =sleep
+    // sleeps GCS_SERVER_SLEEP_NS per step (with the thread's timer slack at
+    // 1 ns, set on first use): a thread that waits long stops burning the
+    // CPU share (cgroup quota) the other mTCP threads of the host need.
+    // Default: spin.
+    void idle(std::chrono::steady_clock::duration waited)
+    {
+        if (wait_mode_ == kWaitSpin || waited < spin_) {
+            __builtin_ia32_pause();
+            return;
+        }
+        if (wait_mode_ == kWaitYield) {
+            sched_yield();
+            return;
+        }
+        if (!slack_set_) {
+            (void)prctl(PR_SET_TIMERSLACK, 1UL, 0UL, 0UL, 0UL);
+            slack_set_ = true;
+        }
+        const struct timespec ts = {0, sleep_ns_};
+        nanosleep(&ts, nullptr);
+    }
+
+    void read_wait_knobs()
+    {
+        const char* e = std::getenv("GCS_SERVER_WAIT");
+        wait_mode_ = !e                            ? kWaitSpin
+                     : std::strcmp(e, "yield") == 0 ? kWaitYield
+                     : std::strcmp(e, "sleep") == 0 ? kWaitSleep
+                                                    : kWaitSpin;
+        e = std::getenv("GCS_SERVER_SPIN_US");
+        spin_ = std::chrono::nanoseconds((long)(1000.0 * (e ? std::max(0.0, std::atof(e)) : 4.0)));
+        e = std::getenv("GCS_SERVER_SLEEP_NS");
+        sleep_ns_ = e ? std::clamp(std::atol(e), 1L, 1000000L) : 1000L;
+    }
+
     // Wait until request r is done (its records, and for an in-place request
     // the serving blocks' acks), starting a grid when the last one left first.
     int complete(Req& r)
@@ -797,12 +839,13 @@ class BurstServer {
                 if (rc) return rc;
                 continue;
             }
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+            const auto now = std::chrono::steady_clock::now();
+            if (now - t0 > std::chrono::seconds(2)) {
                 (void)hub_->stop();
                 std::snprintf(g_hip_err, sizeof g_hip_err, "burst server: no answer in 2 s");
                 return GCS_EHIP;
             }
-            __builtin_ia32_pause();
+            idle(now - t0);
         }
         for (uint32_t i = 0; i < r.n; i++) {
             const uint64_t v = sl.rec[i];
@@ -928,6 +971,11 @@ class BurstServer {
 
   private:
 
+    enum { kWaitSpin = 0, kWaitYield = 1, kWaitSleep = 2 };
+    int wait_mode_ = kWaitSpin;           // GCS_SERVER_WAIT (idle)
+    std::chrono::nanoseconds spin_{4000};
+    long sleep_ns_ = 1000;
+    bool slack_set_ = false;
     ServerHub* hub_ = nullptr;
     int r_ = -1;                          // ring index in the hub
     gcs::ServerMailbox* mb_ = nullptr;    // this ring (host view)
