@@ -105,6 +105,7 @@ struct Slot {
     uint32_t* d_hash = nullptr;
     uint16_t* h_queue = nullptr;
     uint16_t* d_queue = nullptr;
+    uint64_t* h_rec = nullptr;     // direct mode: 8 B records (k_desc_rec), pinned
     // device views of the pinned buffers (direct mode: the kernel reads the
     // staged frames and writes its results over PCIe, no DMA copies)
     uint8_t* m_frames = nullptr;
@@ -114,6 +115,7 @@ struct Slot {
     uint32_t* m_csum = nullptr;
     uint32_t* m_hash = nullptr;
     uint16_t* m_queue = nullptr;
+    uint64_t* m_rec = nullptr;
     // GCS_DIRECT_STAGE=device: a direct-mode batch is gathered into this
     // fine-grained device memory (host writes over the BAR, posted) instead
     // of the pinned staging, so the kernel reads its frames from HBM rather
@@ -122,6 +124,7 @@ struct Slot {
     // bookkeeping of the chunk in flight
     bool busy = false;
     bool served = false;           // results already complete (burst server)
+    bool rec = false;              // results came as records (h_rec): unpack first
     uint32_t first = 0, count = 0;
 };
 
@@ -645,11 +648,13 @@ class BurstServer {
     // in_place: the kernel writes the frames themselves (host memory), so
     // completion also waits for the serving blocks' release + ack; otherwise
     // the tagged result records alone complete it.
-    // dev_frames: the frames are in device memory (device staging), so an
-    // agent-scope acquire makes them visible (gcs_internal.h kModeDevFrames).
+    // where: where the frames live, as line A's mode bits (gcs_internal.h):
+    // kModeDevFrames (device staging: an agent-scope acquire makes them
+    // visible), kModeUncachedFrames (a region registered uncached: no cache
+    // above the GPU's L1 holds its lines), or 0 (pinned host memory).
     int post(uint8_t* frames, uint64_t bytes, const uint64_t* off, const uint16_t* len,
              uint32_t n, bool compute, uint32_t flags, uint8_t* code, uint32_t* csum,
-             bool in_place, bool dev_frames, uint32_t* ticket)
+             bool in_place, uint32_t where, uint32_t* ticket)
     {
         const uint64_t fa = reinterpret_cast<uint64_t>(frames);
         if ((fa & ~gcs::kAddrMask) || n > (uint32_t)gcs::kSlotFrames) {
@@ -670,7 +675,7 @@ class BurstServer {
         std::memset(mb_->res[q % gcs::kServerSlots].rec, 0, n * sizeof(uint64_t));   // no record
                                                                                      // of an older request
         const uint32_t mode = (compute ? 1u : 0u) | (flags << 1) |
-                              (dev_frames ? gcs::kModeDevFrames : 0u);
+                              (where & (gcs::kModeDevFrames | gcs::kModeUncachedFrames));
         // every line carries the request in both 8 B halves (gcs_internal.h):
         // the tag in the top 16 bits of the address / offset and beside n
         const uint64_t tag = gcs::server_tag(q);
@@ -741,14 +746,14 @@ class BurstServer {
     // Serve one batch (n <= gcs::kServerMaxFrames) and return when it is done.
     int serve(uint8_t* frames, uint64_t bytes, const uint64_t* off, const uint16_t* len,
               uint32_t n, bool compute, uint32_t flags, uint8_t* code, uint32_t* csum,
-              bool in_place, bool dev_frames)
+              bool in_place, uint32_t where)
     {
         uint32_t q = done_;
         for (uint32_t k = 0; k < n; k += gcs::kSlotFrames) {
             const uint32_t m = std::min<uint32_t>(gcs::kSlotFrames, n - k);
             int rc = post(frames, bytes, off + k, len + k, m, compute, flags,
                           code ? code + k : nullptr, csum ? csum + k : nullptr, in_place,
-                          dev_frames, &q);
+                          where, &q);
             if (rc) return rc;
         }
         return wait(q);
@@ -1108,6 +1113,7 @@ int free_slot(Slot& s)
     if (s.h_csum) keep_first(rc, hipHostFree(s.h_csum), "hipHostFree");
     if (s.h_hash) keep_first(rc, hipHostFree(s.h_hash), "hipHostFree");
     if (s.h_queue) keep_first(rc, hipHostFree(s.h_queue), "hipHostFree");
+    if (s.h_rec) keep_first(rc, hipHostFree(s.h_rec), "hipHostFree");
     if (s.d_hash) keep_first(rc, hipFree(s.d_hash), "hipFree");
     if (s.d_queue) keep_first(rc, hipFree(s.d_queue), "hipFree");
     if (s.d_frames) keep_first(rc, hipFree(s.d_frames), "hipFree");
@@ -1138,6 +1144,7 @@ int alloc_slot(Slot& s, uint32_t frames, uint64_t bytes)
     HIP_TRY(hipMalloc((void**)&s.d_csum, frames * sizeof(uint32_t)));
     HIP_TRY(hipHostMalloc((void**)&s.h_hash, frames * sizeof(uint32_t), hipHostMallocDefault));
     HIP_TRY(hipHostMalloc((void**)&s.h_queue, frames * sizeof(uint16_t), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&s.h_rec, frames * sizeof(uint64_t), hipHostMallocDefault));
     HIP_TRY(hipMalloc((void**)&s.d_hash, frames * sizeof(uint32_t)));
     HIP_TRY(hipMalloc((void**)&s.d_queue, frames * sizeof(uint16_t)));
     HIP_TRY(hipHostGetDevicePointer((void**)&s.m_frames, s.h_frames, 0));
@@ -1147,6 +1154,7 @@ int alloc_slot(Slot& s, uint32_t frames, uint64_t bytes)
     HIP_TRY(hipHostGetDevicePointer((void**)&s.m_csum, s.h_csum, 0));
     HIP_TRY(hipHostGetDevicePointer((void**)&s.m_hash, s.h_hash, 0));
     HIP_TRY(hipHostGetDevicePointer((void**)&s.m_queue, s.h_queue, 0));
+    HIP_TRY(hipHostGetDevicePointer((void**)&s.m_rec, s.h_rec, 0));
     return GCS_OK;
 }
 
@@ -1208,6 +1216,17 @@ bool is_pinned(const void* p, uint64_t bytes)
     return true;
 }
 
+// Records of a direct-mode batch (k_desc_rec: csum | code << 32 per frame)
+// into the slot's verdict / check arrays.
+void unpack_records(const uint64_t* rec, uint32_t n, uint8_t* code, uint32_t* csum)
+{
+    for (uint32_t i = 0; i < n; i++) {
+        const uint64_t v = rec[i];
+        code[i] = (uint8_t)(v >> 32);
+        csum[i] = (uint32_t)v;
+    }
+}
+
 // tcp_in.c:1237 (tcph->check = 0 on a TCP checksum failure), on the host copy.
 template <class FramePtr>
 void zero_bad_tcp_checks(const uint8_t* code, uint32_t n, FramePtr frame_ptr, const uint16_t* len)
@@ -1228,6 +1247,7 @@ struct RegRegion {
     uint8_t* host;
     uint64_t bytes;
     uint8_t* dev;
+    bool uncached;   // registered with hipExtHostRegisterUncached
 };
 std::mutex g_reg_mu;
 std::vector<RegRegion> g_regions;
@@ -1292,6 +1312,7 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
                         (void)hipEventSynchronize(s.done);
                     s.busy = false;
                     s.served = false;
+                    s.rec = false;
                 }
         }
     } slot_reset{ctx};
@@ -1313,6 +1334,10 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
             HIP_TRY(hipEventSynchronize(s.done));
         s.busy = false;
         s.served = false;
+        if (s.rec) {
+            unpack_records(s.h_rec, s.count, s.h_code, s.h_csum);
+            s.rec = false;
+        }
         if (!compute) {
             std::memcpy(code + s.first, s.h_code, s.count);
             if (hash)
@@ -1370,7 +1395,8 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
             if (ctx->server && n <= (uint32_t)gcs::kServerMaxFrames) {
                 int rc = ctx->server->serve(reg.dev, reg.bytes & ~15ull, s.h_off, s.h_len, n,
                                             compute, 0u, s.h_code, compute ? s.h_csum : nullptr,
-                                            /*in_place=*/compute, /*dev_frames=*/false);
+                                            /*in_place=*/compute,
+                                            reg.uncached ? gcs::kModeUncachedFrames : 0u);
                 if (rc) return rc;
             } else {
                 if (ctx->server) {
@@ -1379,14 +1405,12 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
                     int rc = ctx->server->stop();
                     if (rc) return rc;
                 }
-                if (compute)
-                    HIP_TRY(gcs::launch_compute_desc_spread(reg.dev, reg.bytes, s.m_off, s.m_len,
-                                                            n, s.m_code, s.m_csum, 0u, s.stream));
-                else
-                    HIP_TRY(gcs::launch_verify_desc_spread(reg.dev, reg.bytes, s.m_off, s.m_len,
-                                                           n, s.m_code, 0u, s.stream));
+                // results as whole 64 B lines of records (k_desc_rec)
+                HIP_TRY(gcs::launch_desc_rec(reg.dev, reg.bytes & ~15ull, s.m_off, s.m_len, n,
+                                             s.m_rec, compute, 0u, s.stream));
                 HIP_TRY(hipEventRecord(s.done, s.stream));
                 HIP_TRY(hipEventSynchronize(s.done));
+                unpack_records(s.h_rec, n, s.h_code, s.h_csum);
             }
             if (code)
                 std::memcpy(code, s.h_code, n);
@@ -1494,7 +1518,7 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
             int rc = ctx->server->serve(frames_d, (used + 15) / 16 * 16, s.h_off, s.h_len, cnt,
                                         compute, compute ? GCS_CF_NO_INPLACE : 0u, s.h_code,
                                         compute ? s.h_csum : nullptr, false,
-                                        /*dev_frames=*/gdst != s.h_frames);
+                                        gdst != s.h_frames ? gcs::kModeDevFrames : 0u);
             if (rc) return rc;
             s.busy = true;
             s.served = true;
@@ -1508,9 +1532,12 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
             int rc = ctx->server->stop();
             if (rc) return rc;
         }
-        if (compute && spread) {
-            HIP_TRY(gcs::launch_compute_desc_spread(frames_d, used, off_d, len_d, cnt, code_d,
-                                                    csum_d, GCS_CF_NO_INPLACE, s.stream));
+        if (spread && !classify) {
+            // direct mode: the results come back as whole 64 B lines of
+            // records (k_desc_rec), unpacked by drain()
+            HIP_TRY(gcs::launch_desc_rec(frames_d, used, off_d, len_d, cnt, s.m_rec, compute,
+                                         compute ? (uint32_t)GCS_CF_NO_INPLACE : 0u, s.stream));
+            s.rec = true;
         } else if (compute) {
             HIP_TRY(gcs::launch_compute_desc(frames_d, used, off_d, len_d, cnt, code_d, csum_d,
                                              GCS_CF_NO_INPLACE, s.stream));
@@ -1527,9 +1554,6 @@ int run_host_batch(gcs_ctx* ctx, uint8_t* base, const uint64_t* off, uint8_t* co
             if (queue && !direct)
                 HIP_TRY(hipMemcpyAsync(s.h_queue, s.d_queue, cnt * sizeof(uint16_t),
                                        hipMemcpyDeviceToHost, s.stream));
-        } else if (spread) {
-            HIP_TRY(gcs::launch_verify_desc_spread(frames_d, used, off_d, len_d, cnt, code_d,
-                                                   flags & GCS_VF_ICMP, s.stream));
         } else {
             // the tcp_in.c:1237 side effect is applied on the host copy below
             HIP_TRY(gcs::launch_verify_desc(frames_d, used, off_d, len_d, cnt, code_d,
@@ -1752,14 +1776,27 @@ try {
     for (const auto& r : g_regions)
         if (host < r.host + r.bytes && r.host < host + bytes)
             return GCS_EINVAL;                        // overlaps a registered region
-    HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterMapped));
+    // Uncached (MTYPE UC) by default: the burst server then reads a region's
+    // frames without invalidating the L2 first (the acquire after each poll,
+    // ~1 us per RX burst); GCS_REGISTER_UNCACHED=0, or a runtime without the
+    // flag, registers it cached (then every request takes the acquire).
+    const char* uc = std::getenv("GCS_REGISTER_UNCACHED");
+    bool uncached = !uc || std::strcmp(uc, "0") != 0;
+    if (uncached &&
+        hipHostRegister(p, bytes, hipHostRegisterMapped | hipExtHostRegisterUncached) !=
+            hipSuccess) {
+        (void)hipGetLastError();
+        uncached = false;
+    }
+    if (!uncached)
+        HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterMapped));
     uint8_t* dev = nullptr;
     hipError_t e = hipHostGetDevicePointer((void**)&dev, p, 0);
     if (e != hipSuccess) {
         (void)hipHostUnregister(p);
         return hip_fail(e, "hipHostGetDevicePointer");
     }
-    g_regions.push_back(RegRegion{host, bytes, dev});
+    g_regions.push_back(RegRegion{host, bytes, dev, uncached});
     return GCS_OK;
 } GCS_CATCH
 
@@ -2264,7 +2301,9 @@ int post_async(gcs_ctx* ctx, uint8_t* const* pkts, const uint16_t* len, uint32_t
     int rc = ctx->server->post(frames_d, bytes, a.off.data(), a.dlen.data(), n, compute,
                                compute ? (uint32_t)GCS_CF_NO_INPLACE : 0u, a.st.data(),
                                compute ? a.cs.data() : nullptr, /*in_place=*/false,
-                               /*dev_frames=*/a.staged && a.stage_dev, &got);
+                               a.staged ? (a.stage_dev ? gcs::kModeDevFrames : 0u)
+                                        : (reg.uncached ? gcs::kModeUncachedFrames : 0u),
+                               &got);
     if (rc) return rc;
     a.q = got;
     a.pending = true;

@@ -220,6 +220,12 @@ constexpr uint32_t kServerAcqAgent = 1u;
 constexpr uint32_t kServerAcqNone = 2u;
 
 constexpr uint32_t kModeDevFrames = 1u << 31;
+// ... and a request whose frames are in a region registered uncached
+// (gcs_host_register: hipExtHostRegisterUncached, MTYPE UC) takes only a
+// workgroup-scope invalidate (the CU's L1): no L2 or Infinity Cache line
+// holds that memory, so there is nothing older to miss it in (RX bursts from
+// an mbuf pool: the L2 invalidate was ~1 us of each).
+constexpr uint32_t kModeUncachedFrames = 1u << 30;
 
 hipError_t launch_verify_fixed(uint8_t* frames, uint64_t stride, uint32_t frame_len, uint32_t n,
                                uint8_t* verdict, uint32_t flags, hipStream_t s);
@@ -232,12 +238,11 @@ hipError_t launch_verify_desc(uint8_t* frames, uint64_t frames_bytes, const uint
 hipError_t launch_compute_desc(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
                                const uint16_t* len, uint32_t n, uint8_t* status, uint32_t* csums,
                                uint32_t flags, hipStream_t s);
-hipError_t launch_verify_desc_spread(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
-                                     const uint16_t* len, uint32_t n, uint8_t* verdict,
-                                     uint32_t flags, hipStream_t s);
-hipError_t launch_compute_desc_spread(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
-                                      const uint16_t* len, uint32_t n, uint8_t* status,
-                                      uint32_t* csums, uint32_t flags, hipStream_t s);
+// Direct-mode host batch with its results as 8 B records (csum | code << 32)
+// into pinned host memory, one 64 B line per block of 8 frames (k_desc_rec).
+hipError_t launch_desc_rec(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
+                           const uint16_t* len, uint32_t n, uint64_t* rec, bool compute,
+                           uint32_t flags, hipStream_t s);
 hipError_t launch_classify_fixed(uint8_t* frames, uint64_t stride, uint32_t frame_len,
                                  uint32_t n, uint8_t* verdict, uint32_t flags, const Ext& ext,
                                  hipStream_t s);

@@ -5,6 +5,7 @@
 #include "gcs_internal.h"
 
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 namespace gcs {
@@ -218,6 +219,70 @@ k_desc(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __re
                                                 ok, sub, flags,
                                                 out_code ? out_code + i : nullptr,
                                                 out_csum ? out_csum + i : nullptr);
+}
+
+// Direct-mode host batch (gcs_api.cpp run_host_batch: a small batch whose
+// results go straight into pinned host memory, without the burst server):
+// k_desc's one frame per 32-lane group, 8 frames per block, but each block
+// stages its frames' results in LDS and writes them as ONE 64 B line of 8 B
+// records (csum | code << 32), the burst server's record format: every
+// partial-line write into host memory is a fabric write of its own (round 5:
+// eight 8 B record stores per block made the server's way back grow 1.6 ->
+// 24 us at 16 threads), and the plain k_desc wrote a 1 B verdict and a 4 B
+// check per frame.
+template <int G, int U, bool COMPUTE>
+__global__ void __launch_bounds__(kBlock)
+k_desc_rec(uint8_t* __restrict__ frames, uint64_t frames_bytes, const uint64_t* __restrict__ off,
+           const uint16_t* __restrict__ lens, u32 n, uint64_t* __restrict__ out_rec, u32 flags)
+{
+    constexpr int FPB = kBlock / G;
+    static_assert(FPB == 8, "one 64 B line of records per block");
+    __shared__ uint8_t s_code[FPB];
+    __shared__ uint32_t s_csum[FPB];
+    const int sub = threadIdx.x & (G - 1), grp = threadIdx.x / G;
+    const uint64_t i = (uint64_t)blockIdx.x * FPB + grp;
+    const bool here = i < n;                           // group-uniform
+    if (sub == 0)
+        s_csum[grp] = 0;
+    if (here) {
+        const uint64_t o = off[i];
+        const u32 len = lens[i];
+        const bool ok = (o & 15) == 0 && o <= frames_bytes && len <= frames_bytes - o;
+        uint8_t* f = frames + (ok ? o : 0);
+        do_frame<G, U, COMPUTE, true, true, kNT, kWM>(f, len,
+                                                      ok ? (int64_t)(frames_bytes - o) : 0, ok,
+                                                      sub, flags, s_code + grp,
+                                                      COMPUTE ? s_csum + grp : nullptr);
+    }
+    __syncthreads();                                   // the block's results in LDS
+    if (threadIdx.x < FPB / 2) {
+        const int t = threadIdx.x;
+        const uint64_t j = (uint64_t)blockIdx.x * FPB + 2 * t;
+        const uint64_t r0 = (uint64_t)s_csum[2 * t] | ((uint64_t)s_code[2 * t] << 32);
+        const uint64_t r1 = (uint64_t)s_csum[2 * t + 1] | ((uint64_t)s_code[2 * t + 1] << 32);
+        if (j + 1 < n) {
+            const u32x4 w = {(u32)r0, (u32)(r0 >> 32), (u32)r1, (u32)(r1 >> 32)};
+            asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1"
+                         : : "v"(&out_rec[j]), "v"(w) : "memory");
+        } else if (j < n) {
+            __hip_atomic_store(&out_rec[j], r0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
+hipError_t launch_desc_rec(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
+                           const uint16_t* len, uint32_t n, uint64_t* rec, bool compute,
+                           uint32_t flags, hipStream_t s)
+{
+    constexpr int G = 32, U = 3, FPB = kBlock / G;
+    const dim3 grid((n + FPB - 1) / FPB);
+    if (compute)
+        hipLaunchKernelGGL((k_desc_rec<G, U, true>), grid, dim3(kBlock), 0, s, frames,
+                           frames_bytes, off, len, n, rec, flags);
+    else
+        hipLaunchKernelGGL((k_desc_rec<G, U, false>), grid, dim3(kBlock), 0, s, frames,
+                           frames_bytes, off, len, n, rec, flags);
+    return hipGetLastError();
 }
 
 // Burst server: a grid of kServerBlocks blocks per ring in use that stays
@@ -470,15 +535,18 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
             // after observing it: later loads see everything the host wrote)
             const uint4 a = s_line[0], b = s_line[1];
             const bool dev = (a.w & kModeDevFrames) != 0;   // block-uniform
+            const bool unc = (a.w & kModeUncachedFrames) != 0;
             if (dev && (opts & kServerAcqNone))
                 ;
+            else if (unc && !(opts & kServerAcqAgent))
+                asm volatile("buffer_inv sc0" ::: "memory");   // the CU's L1 only
             else if (dev || (opts & kServerAcqAgent))
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             else
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
             if (PROF)
                 t_acq = clock_after_vmem();
-            const uint32_t n = a.z, compute = a.w & 1u, flags = (a.w & ~kModeDevFrames) >> 1;
+            const uint32_t n = a.z, compute = a.w & 1u, flags = (a.w & ~(kModeDevFrames | kModeUncachedFrames)) >> 1;
             // frames written in place: a fill's check fields, or a verify's
             // tcp_in.c:1237 side effect
             writes = compute ? !(flags & GCS_CF_NO_INPLACE)
@@ -2495,16 +2563,59 @@ static hipError_t launch_fixed_wm(uint8_t* frames, uint64_t stride, u32 frame_le
     return hipGetLastError();
 }
 
+// GCS_TX_HYBRID (A/B knob, read once): a fill too large for whole-line
+// write-back takes lines for its first line_wb_bytes() / 128 frames and
+// sectors for the rest, in two launches -- sc1 (sector sc1 stores) or nt
+// (non-temporal sector stores), line part first; *_linelast puts the line
+// part second.  Unset: sectors for the whole batch.
+static int tx_hybrid()
+{
+    static const int v = [] {
+        const char* e = std::getenv("GCS_TX_HYBRID");
+        if (!e) return 0;
+        if (std::strcmp(e, "sc1") == 0) return 1;
+        if (std::strcmp(e, "nt") == 0) return 2;
+        if (std::strcmp(e, "sc1_linelast") == 0) return 3;
+        if (std::strcmp(e, "nt_linelast") == 0) return 4;
+        return 0;
+    }();
+    return v;
+}
+
 template <int G, int U, bool COMPUTE, bool LOOP, bool EXT, int K = 1>
 static hipError_t launch_fixed(uint8_t* frames, uint64_t stride, u32 frame_len, u32 n,
                                uint8_t* code, uint32_t* csum, u32 flags, const Ext& ext,
                                hipStream_t s)
 {
-    if constexpr (COMPUTE && G >= 8)
+    if constexpr (COMPUTE && G >= 8) {
         if (stride % 128 == 0 && (uint64_t)n * 128 <= line_wb_bytes() &&
             !(flags & GCS_CF_SECTOR_WB))
             return launch_fixed_wm<G, U, COMPUTE, LOOP, EXT, K, WM_LINE_SC1>(
                 frames, stride, frame_len, n, code, csum, flags, ext, s);
+        const int hy = tx_hybrid();
+        constexpr u32 FPB = kBlock / G * K;
+        const u32 m = (u32)(line_wb_bytes() / 128) / FPB * FPB;
+        if (hy && stride % 128 == 0 && !(flags & GCS_CF_SECTOR_WB) && m > 0 && m < n) {
+            auto part = [&](u32 a, u32 b, bool line) -> hipError_t {
+                uint8_t* f = frames + (uint64_t)a * stride;
+                uint8_t* c = code ? code + a : nullptr;
+                uint32_t* k = csum ? csum + a : nullptr;
+                if (line)
+                    return launch_fixed_wm<G, U, COMPUTE, LOOP, EXT, K, WM_LINE_SC1>(
+                        f, stride, frame_len, b - a, c, k, flags, ext, s);
+                if (hy == 2 || hy == 4)
+                    return launch_fixed_wm<G, U, COMPUTE, LOOP, EXT, K, WM_SECTOR_NT>(
+                        f, stride, frame_len, b - a, c, k, flags, ext, s);
+                return launch_fixed_wm<G, U, COMPUTE, LOOP, EXT, K>(f, stride, frame_len, b - a,
+                                                                    c, k, flags, ext, s);
+            };
+            const bool line_last = hy >= 3;
+            hipError_t e = line_last ? part(m, n, false) : part(0, m, true);
+            if (e != hipSuccess)
+                return e;
+            return line_last ? part(0, m, true) : part(m, n, false);
+        }
+    }
     return launch_fixed_wm<G, U, COMPUTE, LOOP, EXT, K>(frames, stride, frame_len, n, code, csum,
                                                         flags, ext, s);
 }
@@ -2666,35 +2777,6 @@ hipError_t launch_compute_desc(uint8_t* frames, uint64_t frames_bytes, const uin
 {
     return launch_desc<true>(frames, frames_bytes, off, len, n, status, csums, flags,
                              (flags & GCS_CF_ICMP) != 0, Ext{}, s);
-}
-
-// Descriptor batch spread thin: one frame per 32-lane group (8 frames per
-// block), so a small batch read over PCIe from pinned host memory (direct
-// mode, gcs_api.cpp) is pulled by many CUs at once instead of one block.
-template <bool COMPUTE>
-static hipError_t launch_desc_spread(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
-                                     const uint16_t* len, u32 n, uint8_t* code, uint32_t* csums,
-                                     u32 flags, hipStream_t s)
-{
-    constexpr int G = 32, U = 3, FPB = kBlock / G;
-    hipLaunchKernelGGL((k_desc<G, U, COMPUTE, kNT, kWM>), dim3((n + FPB - 1) / FPB), dim3(kBlock),
-                       0, s, frames, frames_bytes, off, len, n, code, csums, flags);
-    return hipGetLastError();
-}
-
-hipError_t launch_verify_desc_spread(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
-                                     const uint16_t* len, u32 n, uint8_t* verdict, u32 flags,
-                                     hipStream_t s)
-{
-    return launch_desc_spread<false>(frames, frames_bytes, off, len, n, verdict, nullptr, flags,
-                                     s);
-}
-
-hipError_t launch_compute_desc_spread(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
-                                      const uint16_t* len, u32 n, uint8_t* status,
-                                      uint32_t* csums, u32 flags, hipStream_t s)
-{
-    return launch_desc_spread<true>(frames, frames_bytes, off, len, n, status, csums, flags, s);
 }
 
 hipError_t launch_classify_desc(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,

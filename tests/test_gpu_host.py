@@ -176,13 +176,16 @@ def test_burst_server_yields_to_large_batches(torch_dev):
         np.testing.assert_array_equal(v, O.verify_batch(buf.copy(), off, lens))
 
 
-@pytest.mark.parametrize("server,start,skew", [(False, None, None), (True, None, None),
-                                               (True, 0x80000002, None),
-                                               (True, 0xFFFFFFFF - 4, None),
-                                               (True, 0xFFFF0, 0x7FFFFFF0)],
-                         ids=["direct", "server", "server_seq_2^31", "server_seq_wrap",
-                              "server_stale_ack"])
-def test_registered_rooms_in_place(torch_dev, monkeypatch, server, start, skew):
+@pytest.mark.parametrize("server,start,skew,cached", [(False, None, None, False),
+                                                      (True, None, None, False),
+                                                      (True, None, None, True),
+                                                      (False, None, None, True),
+                                                      (True, 0x80000002, None, False),
+                                                      (True, 0xFFFFFFFF - 4, None, False),
+                                                      (True, 0xFFFF0, 0x7FFFFFF0, False)],
+                         ids=["direct", "server", "server_cached", "direct_cached",
+                              "server_seq_2^31", "server_seq_wrap", "server_stale_ack"])
+def test_registered_rooms_in_place(torch_dev, monkeypatch, server, start, skew, cached):
     """Frames in one registered region (an mbuf pool) are verified and filled
     in place over PCIe -- no gather, no scatter -- with the same results; a
     frame outside the region, or misaligned, sends the batch down the staged
@@ -192,8 +195,14 @@ def test_registered_rooms_in_place(torch_dev, monkeypatch, server, start, skew):
     request and complete it before its release: every result must
     still equal the oracle.  server_stale_ack joins the ring with acks 2^31 + 16
     requests behind it (GCS_SERVER_ACK_SKEW), as after 2^31 requests that
-    wrote no frame: the grid refreshes them before it serves."""
+    wrote no frame: the grid refreshes them before it serves.
+    The region is registered uncached by default (the grid then skips the L2
+    invalidate before reading its frames); *_cached registers it cached.
+    Every burst rewrites the rooms with new frames, as a NIC reuses mbufs: a
+    stale cached line would show as a wrong verdict or check."""
     import ctypes as C
+    if cached:
+        monkeypatch.setenv("GCS_REGISTER_UNCACHED", "0")
     if start is not None:
         monkeypatch.setenv("GCS_SERVER_SEQ_START", str(start))
     if skew is not None:

@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round 6: the C4 4M-frame TX fill with hybrid write-back (GCS_TX_HYBRID):
+# lines for the first 1M frames, sectors (sc1 or nt) for the rest.
+set -o pipefail
+O=gpurun_out/${R06_OUT:-r06d}
+mkdir -p $O
+c4() { local name=$1; shift; env "$@" timeout -k 10 180 python -u -c "
+import json, torch, bench
+from mtcp_amd import gpucsum
+ctx = gpucsum.Context(0)
+torch.cuda.set_stream(torch.cuda.Stream())
+r = bench.c4_shard(ctx, torch, 20, 3, 1.0)
+ctx.close()
+print(json.dumps(r))" > $O/$name.json 2> $O/$name.err || { tail -5 $O/$name.err; exit 1; }
+python -c "
+import json; d=json.load(open('$O/$name.json'))
+print('$name', round(d['ms_per_step'],4), 'fill', round(d['compute_ms'],4), round(d['compute_frac'],4), 'verify', round(d['verify_ms'],4), round(d['verify_frac'],4))"; }
+for r in 1 2; do
+c4 c4_base_$r
+c4 c4_sc1_$r GCS_TX_HYBRID=sc1
+c4 c4_nt_$r GCS_TX_HYBRID=nt
+c4 c4_sc1ll_$r GCS_TX_HYBRID=sc1_linelast
+c4 c4_ntll_$r GCS_TX_HYBRID=nt_linelast
+done

@@ -59,7 +59,7 @@ def main():
     out = {"config": {k: os.environ.get(k, "default") for k in
                       ("GCS_SERVER_MAILBOX", "GCS_SERVER_ACQUIRE", "GCS_SERVER_COUNTERS",
                        "GCS_DIRECT_STAGE", "GCS_SERVER_HOT_NAPS", "GCS_SERVER_HOT_US",
-                       "MT_PIN")},
+                       "GCS_SERVER_WAIT", "GCS_SERVER_SPIN_US", "MT_PIN")},
            "cpus": cpu_quota(),
            "cpu_frac": "thread CPU time / wall time inside the calls (below 1: descheduled)"}
     iters = int(os.environ.get("SS_ITERS", "600"))
