@@ -103,20 +103,26 @@ def make_batches(ctx, n, frame_len, seed, torch):
     return tx, rx, stride, int(pick.numel())
 
 
-def time_steps(ctx, tx, rx, stride, frame_len, n, steps, warmup, world, torch, settle_s=0.0):
+def time_steps(ctx, tx, rx, stride, frame_len, n, steps, warmup, world, torch, settle_s=0.0,
+               fused=True):
+    """W untimed warmup steps, then exactly K timed steps between a barrier +
+    synchronize on both sides.  A step is the TX fill of `tx` and the RX
+    verify of `rx`: ONE launch (gcs_step_fixed_dev, fused=True: mTCP's loop
+    folds RX and TX each iteration) or the two launches (fused=False).  One
+    HIP event per step boundary on the launches' own stream (K + 1 in all,
+    nothing between a step's kernels): the fused launch's duration per step.
+    Returns (wall seconds, per-step event ms, verdicts)."""
     stream = torch.cuda.current_stream().cuda_stream
     assert stream, "kernels must run on the events' stream"
     verdict = torch.empty(n, dtype=torch.uint8, device="cuda")
 
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record()
-        ctx.compute_fixed(tx, stride, frame_len, n, stream=stream)
-        if ev is not None:
-            ev[1].record()
-        ctx.verify_fixed(rx, stride, frame_len, n, verdict, stream=stream)
-        if ev is not None:
-            ev[2].record()
+    def step():
+        if fused:
+            ctx.step_fixed(tx, stride, frame_len, n, rx, stride, frame_len, n, verdict,
+                           stream=stream)
+        else:
+            ctx.compute_fixed(tx, stride, frame_len, n, stream=stream)
+            ctx.verify_fixed(rx, stride, frame_len, n, verdict, stream=stream)
 
     if settle_s > 0:
         # bring HBM/GPU clocks to their loaded state (DESIGN.md App. A): untimed
@@ -128,18 +134,45 @@ def time_steps(ctx, tx, rx, stride, frame_len, n, steps, warmup, world, torch, s
             torch.cuda.synchronize()
     for _ in range(warmup):
         step()
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(steps):
-        step(evs[k])
+        evs[k].record()
+        step()
+    evs[steps].record()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier(world)
-    tx_ms = [e[0].elapsed_time(e[1]) for e in evs]
-    rx_ms = [e[1].elapsed_time(e[2]) for e in evs]
-    return t1 - t0, tx_ms, rx_ms, verdict
+    step_ms = [evs[k].elapsed_time(evs[k + 1]) for k in range(steps)]
+    return t1 - t0, step_ms, verdict
+
+
+def split_kernels_ms(ctx, tx, rx, stride, frame_len, n, torch, reps=20):
+    """After the timed region (untimed for the line): the step's two halves
+    as separate launches -- the TX fill and the RX verify, each timed back to
+    back with HIP events -- so the per-kernel figures stay on record beside
+    the fused step.  The TX fill rewrites the checks it wrote in the step
+    (refills), as the round-5 line's per-kernel figures did."""
+    stream = torch.cuda.current_stream().cuda_stream
+    v = torch.empty(n, dtype=torch.uint8, device="cuda")
+    out = {}
+    for name, fn in (("compute", lambda: ctx.compute_fixed(tx, stride, frame_len, n,
+                                                           stream=stream)),
+                     ("verify", lambda: ctx.verify_fixed(rx, stride, frame_len, n, v,
+                                                         stream=stream))):
+        for _ in range(3):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        out[name] = e0.elapsed_time(e1) / reps
+    return out
 
 
 def pmc_row(label: str):
@@ -154,13 +187,14 @@ def pmc_row(label: str):
         return None
 
 
-def dominant_frac(n, L, compute_ms, verify_ms):
-    """Algorithmic GB/s of the slower of the two kernels / the HBM peak."""
-    if compute_ms >= verify_ms:
-        gbs = n * (L + 4) / (compute_ms * 1e-3) / 1e9
-    else:
-        gbs = n * (L + 1) / (verify_ms * 1e-3) / 1e9
-    return gbs / HBM_PEAK_GBS
+def step_bytes(n, L):
+    """Algorithmic bytes of one step: TX L + 4, RX L + 1 per frame."""
+    return n * (L + 4) + n * (L + 1)
+
+
+def step_frac(n, L, step_ms):
+    """Algorithmic GB/s of the fused step launch / the HBM peak."""
+    return step_bytes(n, L) / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
 
 
 def host_cpus():
@@ -589,10 +623,18 @@ def rows_8f(ctx, torch, n=1 << 20, L=1500):
 def tx_write_mode(n, stride):
     """The TX fill's write-back for a fixed-stride batch, as the library picks
     it (gcs_kernels.hip launch_fixed): whole 128 B lines while n x 128 B fits
-    GCS_TX_LINE_WB_MB (default 128 MiB, inside the Infinity Cache), else the
-    64 B sectors holding the check fields."""
+    GCS_TX_LINE_WB_MB (default 128 MiB, inside the Infinity Cache), else lines
+    for that many frames and non-temporal 64 B sectors holding the check
+    fields for the rest (GCS_TX_HYBRID)."""
     mb = int(os.environ.get("GCS_TX_LINE_WB_MB", "128"))
-    return "line" if stride % 128 == 0 and n * 128 <= (mb << 20) else "sector"
+    if stride % 128:
+        return "sector"
+    if n * 128 <= (mb << 20):
+        return "line"
+    hy = os.environ.get("GCS_TX_HYBRID", "nt")
+    if hy in ("nt", "sc1"):
+        return f"line for the first {(mb << 20) // 128} frames, {hy} sectors after"
+    return "sector"
 
 
 def c2_sector_wb(ctx, torch, tx, stride, L, n):
@@ -644,26 +686,27 @@ def c2_fresh_cold(ctx, torch, tx, stride, L, n):
 
 def c4_shard(ctx, torch, steps, warmup, settle_s, n=4 << 20, L=1500):
     """The N > 1 per-GPU workload on this one GPU: a C4 shard of 4M x 1500 B
-    frames, the same TX + RX step, settle, warmup and timing as the main line
-    (time_steps), so a SCALE curve's per-GPU rate can be read against it."""
+    frames, the same fused TX + RX step, settle, warmup and timing as the main
+    line (time_steps), so a SCALE curve's per-GPU rate can be read against
+    it; the step's two halves as separate launches beside it."""
     tx, rx, stride, nbad = make_batches(ctx, n, L, 0x6D746370, torch)
-    el, txl, rxl, verdict = time_steps(ctx, tx, rx, stride, L, n, steps, warmup, 1, torch,
-                                       settle_s)
+    el, sl, verdict = time_steps(ctx, tx, rx, stride, L, n, steps, warmup, 1, torch, settle_s)
     bad = int((verdict != 0).sum())
     assert bad == nbad, (bad, nbad)
-    tms, rms = float(np.mean(txl)), float(np.mean(rxl))
-    kname, kms, kb = (("compute", tms, n * (L + 4)) if tms >= rms else
-                      ("verify", rms, n * (L + 1)))
-    prow = pmc_row(f"{kname}_fixed_{L}_{n}")
+    sms = float(np.mean(sl))
+    split = split_kernels_ms(ctx, tx, rx, stride, L, n, torch)
+    tms, rms = split["compute"], split["verify"]
+    prow = pmc_row(f"step_fixed_{L}_{n}")
     del tx, rx
-    return {"workload": f"C4 shard: {n} x {L}B frames, TX compute + RX verify per step",
+    return {"workload": f"C4 shard: {n} x {L}B frames, TX fill + RX verify per step (one launch)",
             "gpkt_per_s": 2 * n * steps / el / 1e9, "ms_per_step": el / steps * 1e3,
-            "compute_ms": tms, "verify_ms": rms,
+            "step_kernel_ms": sms, "compute_ms": tms, "verify_ms": rms,
             "tx_write_mode": tx_write_mode(n, stride),
-            "roofline": {"kernel": kname, "achieved": kb / (kms * 1e-3) / 1e9,
-                         "frac": kb / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "roofline": {"kernel": "step (fill + verify, one launch)",
+                         "achieved": step_bytes(n, L) / (sms * 1e-3) / 1e9,
+                         "frac": step_frac(n, L, sms),
                          "traffic": prow["hbm_bytes_per_launch"] if prow else None,
-                         "traffic_source": (f"profiles/pmc_summary.json configs[{kname}_fixed_"
+                         "traffic_source": (f"profiles/pmc_summary.json configs[step_fixed_"
                                             f"{L}_{n}]" if prow else None)},
             "verify_frac": n * (L + 1) / (rms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "compute_frac": n * (L + 4) / (tms * 1e-3) / 1e9 / HBM_PEAK_GBS,
@@ -954,7 +997,8 @@ def compact_line(line, extras_path=None):
                                           "bytes_per_launch_algorithmic", "avg_launch_ms",
                                           "tx_write_mode") if k in rf}
     if "kernels_ms" in line:
-        out["kernels_ms"] = {k: line["kernels_ms"][k] for k in ("compute", "verify")}
+        out["kernels_ms"] = {k: line["kernels_ms"][k] for k in ("step", "compute", "verify")
+                             if k in line["kernels_ms"]}
     cb = line.get("cpu_baseline")
     if cb:
         out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample",
@@ -964,7 +1008,7 @@ def compact_line(line, extras_path=None):
             out["cpu_baseline"]["multi_core"] = {k: mc[k] for k in ("value", "unit", "cores",
                                                                     "gib_per_s") if k in mc}
     out["per_gpu"] = [{k: (round(v, 4) if isinstance(v, float) else v) for k, v in p.items()
-                       if k in ("rank", "device", "gpkt_per_s", "frac_peak",
+                       if k in ("rank", "device", "gpkt_per_s", "frac_peak", "step_us",
                                 "bad_frames_detected", "corrupted_frames")}
                       for p in line.get("per_gpu", [])]
     side = side_scalars(line)
@@ -993,29 +1037,27 @@ def main():
     torch.cuda.set_stream(work)
     tx, rx, stride, nbad = make_batches(ctx, n, L, 0x6D746370 ^ rank, torch)
 
-    elapsed, tx_list, rx_list, verdict = time_steps(ctx, tx, rx, stride, L, n, args.steps,
-                                                    args.warmup, world, torch, args.settle_s)
-    tx_ms, rx_ms = float(np.mean(tx_list)), float(np.mean(rx_list))
+    elapsed, step_list, verdict = time_steps(ctx, tx, rx, stride, L, n, args.steps, args.warmup,
+                                             world, torch, args.settle_s)
+    step_ms = float(np.mean(step_list))
     bad_seen = int((verdict != 0).sum())
     if bad_seen != nbad:
         raise SystemExit(f"rank {rank}: verify flagged {bad_seen} frames, {nbad} corrupted")
+    # after the timed region: the step's halves as separate launches, on record
+    split = split_kernels_ms(ctx, tx, rx, stride, L, n, torch)
     red_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
     t = max_over_ranks(world, elapsed, device=red_dev)
-    per = gather_per_rank(world, [float(rank), float(local), elapsed, tx_ms, rx_ms,
-                                  float(bad_seen), float(nbad)], device=red_dev)
+    per = gather_per_rank(world, [float(rank), float(local), elapsed, step_ms, split["compute"],
+                                  split["verify"], float(bad_seen), float(nbad)], device=red_dev)
 
     rate = aggregate_rate(2 * n, world, args.steps, t)   # TX fills + RX verifies, all ranks
     value = rate / 1e9
     gib = rate * L / 2**30
-    # dominant kernel's roofline (algorithmic bytes)
-    rx_bytes = n * (L + 1)
-    tx_bytes = n * (L + 4)
-    if rx_ms >= tx_ms:
-        kname, kms, kbytes = "verify", rx_ms, rx_bytes
-    else:
-        kname, kms, kbytes = "compute", tx_ms, tx_bytes
-    achieved = kbytes / (kms * 1e-3) / 1e9
-    prow = pmc_row(f"{kname}_fixed_{L}_{n}")
+    # the dominant kernel is the step's one launch (gcs_step_fixed_dev): its
+    # algorithmic bytes over its HIP-event time per step
+    kbytes = step_bytes(n, L)
+    achieved = kbytes / (step_ms * 1e-3) / 1e9
+    prow = pmc_row(f"step_fixed_{L}_{n}")
     line = {
         "metric": METRIC,
         "value": value,
@@ -1030,37 +1072,44 @@ def main():
         "dtype": "u16",
         "data": "synthetic (seeded mTCP-shaped Eth/IPv4/TCP frames generated in HBM)",
         "config": {
-            "workload": ("C2: 1M x 1500B frames, TX compute + RX verify per step" if world == 1
+            "workload": ("C2: 1M x 1500B frames, TX fill + RX verify per step" if world == 1
                          and n == (1 << 20) and L == 1500 else
-                         f"C4 shard: {n} x {L}B frames per GPU, TX compute + RX verify per step"),
+                         f"C4 shard: {n} x {L}B frames per GPU, TX fill + RX verify per step"),
             "frames_per_gpu": n, "frame_len": L, "stride": stride,
+            "step": "one launch per step (gcs_step_fixed_dev: the TX batch's fill and the RX "
+                    "batch's verify)",
             "parallelism": f"frame-shard x{world} (no collective)",
         },
         "gib_per_s": gib,
         "roofline": {
             "bound": "hbm",
-            "kernel": f"{kname} of {n} x {L}B: " + (prow["kernel"] if prow else "see kernels_ms"),
+            "kernel": f"step of {n} + {n} x {L}B: " + (prow["kernel"] if prow else
+                                                       "k_fixed_step (fill + verify)"),
             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             # HBM bytes per launch of THIS configuration (kernel and frames per
             # launch) from rocprofv3 PMC; null when it was not profiled
             "traffic": prow["hbm_bytes_per_launch"] if prow else None,
-            "traffic_source": (f"profiles/pmc_summary.json configs[{kname}_fixed_{L}_{n}]"
+            "traffic_source": (f"profiles/pmc_summary.json configs[step_fixed_{L}_{n}]"
                                if prow else None),
-            "bytes_per_launch_algorithmic": kbytes, "avg_launch_ms": kms,
+            "bytes_per_launch_algorithmic": kbytes, "avg_launch_ms": step_ms,
             "tx_write_mode": tx_write_mode(n, stride),
         },
-        "kernels_ms": {"compute": tx_ms, "verify": rx_ms,
-                       "compute_first_last": [tx_list[0], tx_list[-1]],
-                       "verify_first_last": [rx_list[0], rx_list[-1]]},
+        # the step's halves as separate launches (after the timed region)
+        "kernels_ms": {"step": step_ms, "compute": split["compute"], "verify": split["verify"],
+                       "step_first_last": [step_list[0], step_list[-1]],
+                       "compute_frac": n * (L + 4) / (split["compute"] * 1e-3) / 1e9 /
+                       HBM_PEAK_GBS,
+                       "verify_frac": n * (L + 1) / (split["verify"] * 1e-3) / 1e9 /
+                       HBM_PEAK_GBS},
         # per GPU, like mTCP's per-thread NETSTAT (core.c:189-218): each rank's
-        # own rate, dominant-kernel fraction of peak and bad-frame count
+        # own rate, its step launch's fraction of peak and bad-frame count
         "per_gpu": [{"rank": int(r), "device": int(d), "gpkt_per_s": 2 * n * args.steps / e / 1e9,
                      "gib_per_s": 2 * n * args.steps * L / e / 2**30,
-                     "compute_us": c * 1e3, "verify_us": v * 1e3,
-                     "frac_peak": dominant_frac(n, L, c, v),
+                     "step_us": sm * 1e3, "compute_us": c * 1e3, "verify_us": v * 1e3,
+                     "frac_peak": step_frac(n, L, sm),
                      "bad_frames_detected": int(b), "corrupted_frames": int(nb)}
-                    for r, d, e, c, v, b, nb in per],
+                    for r, d, e, sm, c, v, b, nb in per],
         "settle_s": args.settle_s,
         "corrupted_frames_detected": bad_seen,
     }

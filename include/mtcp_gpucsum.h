@@ -240,6 +240,18 @@ int gcs_verify_fixed_dev(gcs_ctx *ctx, uint8_t *d_frames, uint64_t stride,
 int gcs_compute_fixed_dev(gcs_ctx *ctx, uint8_t *d_frames, uint64_t stride,
                           uint32_t frame_len, uint32_t n, uint8_t *d_status,
                           uint32_t *d_csums, uint32_t flags, void *stream);
+/* One iteration of mTCP's loop over two device-resident fixed-stride batches
+ * (core.c:761-877 folds RX and TX every iteration): the TX fill of d_tx (as
+ * gcs_compute_fixed_dev) and the RX verify of d_rx (as gcs_verify_fixed_dev)
+ * in ONE launch when both frame sizes take the same kernel shape and no
+ * GCS_*_ICMP flag is set -- the verify's first blocks then run in the fill's
+ * tail instead of behind a kernel boundary -- else as those two launches, in
+ * that order.  The batches may not overlap (GCS_EINVAL); n_tx or n_rx may
+ * be 0. */
+int gcs_step_fixed_dev(gcs_ctx *ctx, uint8_t *d_tx, uint64_t tx_stride, uint32_t tx_len,
+                       uint32_t n_tx, uint8_t *d_tx_status, uint32_t *d_tx_csums,
+                       uint32_t tx_flags, uint8_t *d_rx, uint64_t rx_stride, uint32_t rx_len,
+                       uint32_t n_rx, uint8_t *d_rx_verdict, uint32_t rx_flags, void *stream);
 int gcs_verify_dev(gcs_ctx *ctx, uint8_t *d_frames, uint64_t frames_bytes,
                    const uint64_t *d_off, const uint16_t *d_len, uint32_t n,
                    uint8_t *d_verdict, uint32_t flags, void *stream);

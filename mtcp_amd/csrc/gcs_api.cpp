@@ -1863,6 +1863,33 @@ try {
     return GCS_OK;
 } GCS_CATCH
 
+int gcs_step_fixed_dev(gcs_ctx* ctx, uint8_t* d_tx, uint64_t tx_stride, uint32_t tx_len,
+                       uint32_t n_tx, uint8_t* d_tx_status, uint32_t* d_tx_csums,
+                       uint32_t tx_flags, uint8_t* d_rx, uint64_t rx_stride, uint32_t rx_len,
+                       uint32_t n_rx, uint8_t* d_rx_verdict, uint32_t rx_flags, void* stream)
+try {
+    auto bad_shape = [](uint64_t stride, uint32_t len) {
+        return stride % 16 || stride == 0 || (len + 15u) / 16u * 16u > stride;
+    };
+    if (!ctx || (n_tx && (!d_tx || bad_shape(tx_stride, tx_len))) ||
+        (n_rx && (!d_rx || !d_rx_verdict || bad_shape(rx_stride, rx_len))))
+        return GCS_EINVAL;
+    if (n_tx && n_rx) {
+        // the one launch runs both at once: they may not share a byte
+        const uint64_t t0 = reinterpret_cast<uint64_t>(d_tx), t1 = t0 + (uint64_t)n_tx * tx_stride;
+        const uint64_t r0 = reinterpret_cast<uint64_t>(d_rx), r1 = r0 + (uint64_t)n_rx * rx_stride;
+        if (t0 < r1 && r0 < t1)
+            return GCS_EINVAL;
+    }
+    if (n_tx == 0 && n_rx == 0)
+        return GCS_OK;
+    DeviceGuard g(ctx->device);
+    HIP_TRY(gcs::launch_step_fixed(d_tx, tx_stride, tx_len, n_tx, d_tx_status, d_tx_csums,
+                                   tx_flags, d_rx, rx_stride, rx_len, n_rx, d_rx_verdict, rx_flags,
+                                   pick_stream(ctx, stream)));
+    return GCS_OK;
+} GCS_CATCH
+
 int gcs_verify_dev(gcs_ctx* ctx, uint8_t* d_frames, uint64_t frames_bytes, const uint64_t* d_off,
                    const uint16_t* d_len, uint32_t n, uint8_t* d_verdict, uint32_t flags,
                    void* stream)

@@ -231,6 +231,12 @@ hipError_t launch_verify_fixed(uint8_t* frames, uint64_t stride, uint32_t frame_
                                uint8_t* verdict, uint32_t flags, hipStream_t s);
 hipError_t launch_compute_fixed(uint8_t* frames, uint64_t stride, uint32_t frame_len, uint32_t n,
                                 uint8_t* status, uint32_t* csums, uint32_t flags, hipStream_t s);
+// A TX fill and an RX verify of two fixed-stride batches in one launch
+// (k_fixed_step), or the two launches when their kernel shapes differ.
+hipError_t launch_step_fixed(uint8_t* tx, uint64_t tx_stride, uint32_t tx_len, uint32_t ntx,
+                             uint8_t* tx_code, uint32_t* tx_csum, uint32_t tx_flags, uint8_t* rx,
+                             uint64_t rx_stride, uint32_t rx_len, uint32_t nrx, uint8_t* rx_code,
+                             uint32_t rx_flags, hipStream_t s);
 constexpr uint32_t kDescFrames = 256;    // frames per k_desc_stream block
 hipError_t launch_verify_desc(uint8_t* frames, uint64_t frames_bytes, const uint64_t* off,
                               const uint16_t* len, uint32_t n, uint8_t* verdict, uint32_t flags,

@@ -54,15 +54,17 @@ __device__ __forceinline__ XFrame xframe(const Ext& x, uint64_t i)
 // wave still reads one contiguous range), and issues the loads of all K before
 // folding any: small frames give a lane only U*16 bytes each, too few bytes in
 // flight per wave to cover HBM latency.
+// bid / nb: this block's index in, and the size of, the grid (or the part of
+// a grid, k_fixed_step) that takes this batch.
 template <int G, int U, bool COMPUTE, bool LOOP, bool NT, int WM, bool XCD, bool EXT, int K = 1>
 __device__ __forceinline__ void fixed_frame(uint8_t* __restrict__ frames, uint64_t stride,
                                             u32 frame_len, u32 n, uint8_t* __restrict__ out_code,
                                             uint32_t* __restrict__ out_csum, u32 flags,
-                                            const Ext& ext)
+                                            const Ext& ext, uint32_t bid, uint32_t nb)
 {
     constexpr int FPB = kBlock / G;                    // frames per block and batch
     const int sub = threadIdx.x & (G - 1);
-    const uint32_t blk = XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t blk = XCD ? xcd_block(bid, nb) : bid;
     const uint64_t i0 = (uint64_t)blk * FPB * K + threadIdx.x / G;
     if (i0 >= n)
         return;                                        // whole group leaves together
@@ -107,7 +109,41 @@ k_fixed(uint8_t* __restrict__ frames, uint64_t stride, u32 frame_len, u32 n,
         uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags)
 {
     fixed_frame<G, U, COMPUTE, LOOP, NT, WM, XCD, false, K>(frames, stride, frame_len, n,
-                                                            out_code, out_csum, flags, Ext{});
+                                                            out_code, out_csum, flags, Ext{},
+                                                            blockIdx.x, gridDim.x);
+}
+
+// One launch for a TX fill and an RX verify of two fixed-stride batches
+// (gcs_step_fixed_dev: mTCP's loop folds both every iteration, core.c:761-877):
+// blocks [0, tx_blocks) fill the TX batch, the rest verify the RX batch, so
+// the verify's first blocks run in the fill's tail instead of behind a
+// kernel boundary.  tx_blocks is a multiple of 8: both parts keep the
+// XCD-contiguous block order (xcd_block).
+template <int G, int U, bool LOOP, int WMA, int WMB>
+__global__ void __launch_bounds__(kBlock)
+k_fixed_step(uint8_t* __restrict__ tx, uint64_t tx_stride, u32 tx_len, u32 ntx,
+             uint8_t* __restrict__ tx_code, uint32_t* __restrict__ tx_csum, u32 tx_flags,
+             uint8_t* __restrict__ rx, uint64_t rx_stride, u32 rx_len, u32 nrx,
+             uint8_t* __restrict__ rx_code, u32 rx_flags, u32 tx_blocks, u32 tx_split)
+{
+    // the fill's write-back as launch_fixed picks it (k_fixed_tx2): WMA for
+    // its logical blocks [0, tx_split), WMB after
+    if (blockIdx.x < tx_blocks) {
+        const uint32_t blk = xcd_block(blockIdx.x, tx_blocks);
+        if (blk < tx_split)
+            fixed_frame<G, U, true, LOOP, kNT, WMA, false, false>(tx, tx_stride, tx_len, ntx,
+                                                                  tx_code, tx_csum, tx_flags,
+                                                                  Ext{}, blk, tx_blocks);
+        else
+            fixed_frame<G, U, true, LOOP, kNT, WMB, false, false>(tx, tx_stride, tx_len, ntx,
+                                                                  tx_code, tx_csum, tx_flags,
+                                                                  Ext{}, blk, tx_blocks);
+    } else {
+        fixed_frame<G, U, false, LOOP, kNT, kWM, kXCD, false>(rx, rx_stride, rx_len, nrx, rx_code,
+                                                              nullptr, rx_flags, Ext{},
+                                                              blockIdx.x - tx_blocks,
+                                                              gridDim.x - tx_blocks);
+    }
 }
 
 // k_fixed with the extensions (ICMP fold, RSS steering): a separate
@@ -118,7 +154,8 @@ k_fixed_x(uint8_t* __restrict__ frames, uint64_t stride, u32 frame_len, u32 n,
           uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags, Ext ext)
 {
     fixed_frame<G, U, COMPUTE, LOOP, NT, WM, XCD, true, K>(frames, stride, frame_len, n, out_code,
-                                                           out_csum, flags, ext);
+                                                           out_csum, flags, ext, blockIdx.x,
+                                                           gridDim.x);
 }
 
 // Small frames (<= 64 B, C1): ONE LANE PER FRAME.  A lane loads its frame's
@@ -679,6 +716,8 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
         __hip_atomic_store(&rm->state[blk].v, 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+constexpr int kLdsMaxGroups = 24;
+
 hipError_t launch_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, int groups,
                                uint64_t idle_ticks, uint64_t life_ticks, uint64_t hot_ticks,
                                uint64_t hot_max_ticks, uint32_t max_polls, uint32_t naps,
@@ -691,11 +730,20 @@ hipError_t launch_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, int gro
     // has 160 KiB), so the dispatcher cannot stack up to four of them (117
     // VGPRs, four waves) on a CU whose memory pipeline they then share.  With
     // 8-24 rings, per-call times varied 1.5x from grid to grid without it
-    // (DESIGN.md §5).  GCS_SERVER_LDS_KB overrides (0: none).
-    static const size_t lds = [] {
+    // (DESIGN.md §5).  The reservation leaves 64 KiB of those CUs' LDS to
+    // other kernels while the grid lives, so it is made only while the grid
+    // covers at most kLdsMaxGroups x 8 CUs (3/4 of the chip); a larger grid
+    // stacks.  GCS_SERVER_LDS_KB overrides the size (0: none),
+    // GCS_SERVER_LDS_GROUPS the group bound.
+    static const size_t lds_kb = [] {
         const char* e = std::getenv("GCS_SERVER_LDS_KB");
-        return (e ? (size_t)std::strtoul(e, nullptr, 10) : (size_t)96) << 10;
+        return e ? (size_t)std::strtoul(e, nullptr, 10) : (size_t)96;
     }();
+    static const int lds_groups = [] {
+        const char* e = std::getenv("GCS_SERVER_LDS_GROUPS");
+        return e ? std::atoi(e) : kLdsMaxGroups;
+    }();
+    const size_t lds = groups <= lds_groups ? lds_kb << 10 : 0;
     if (lds > 65536) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_burst_server<32, 3, true>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -2563,23 +2611,60 @@ static hipError_t launch_fixed_wm(uint8_t* frames, uint64_t stride, u32 frame_le
     return hipGetLastError();
 }
 
-// GCS_TX_HYBRID (A/B knob, read once): a fill too large for whole-line
-// write-back takes lines for its first line_wb_bytes() / 128 frames and
-// sectors for the rest, in two launches -- sc1 (sector sc1 stores) or nt
-// (non-temporal sector stores), line part first; *_linelast puts the line
-// part second.  Unset: sectors for the whole batch.
+// A fill too large for whole-line write-back (C4: 4M frames) writes whole
+// lines for its first line_wb_bytes() / 128 frames -- their dirty lines fit
+// the Infinity Cache -- and the 64 B sectors with non-temporal stores for the
+// rest, in ONE launch (k_fixed_tx2): 4M x 1500 B fill 1,093-1,096 us (0.719-
+// 0.721 of 8 TB/s) as two launches against 1,104-1,137 us with sc1 sectors
+// for the whole batch, 1,117-1,120 us with nt sectors alone, 1,215-1,223 us
+// with sc1 sectors after the lines (profiles/r06/r06{d,e}).  GCS_TX_HYBRID
+// (read once): nt (default), sc1, off (sc1 sectors for the whole batch, as
+// before round 6).
 static int tx_hybrid()
 {
     static const int v = [] {
         const char* e = std::getenv("GCS_TX_HYBRID");
-        if (!e) return 0;
+        if (!e || std::strcmp(e, "nt") == 0) return 2;
         if (std::strcmp(e, "sc1") == 0) return 1;
-        if (std::strcmp(e, "nt") == 0) return 2;
-        if (std::strcmp(e, "sc1_linelast") == 0) return 3;
-        if (std::strcmp(e, "nt_linelast") == 0) return 4;
         return 0;
     }();
     return v;
+}
+
+// The TX write-back of a plain fixed-stride fill of n frames (G >= 8 lanes
+// per frame): WMA for the frames of logical blocks [0, split), WMB after.
+struct TxWb {
+    int mode;      // 0: kWM whole batch; 1: lines whole batch; 2: lines then nt; 3: lines then sc1
+    u32 split;     // logical blocks written with lines (modes 2, 3)
+};
+
+static TxWb tx_wb(uint64_t stride, u32 n, u32 flags, u32 fpb)
+{
+    if (stride % 128 != 0 || (flags & GCS_CF_SECTOR_WB))
+        return {0, 0};
+    if ((uint64_t)n * 128 <= line_wb_bytes())
+        return {1, 0};
+    const int hy = tx_hybrid();
+    const u32 m = (u32)(line_wb_bytes() / 128) / fpb;
+    if (!hy)
+        return {0, 0};
+    return {hy == 2 ? 2 : 3, m};
+}
+
+template <int G, int U, bool LOOP, int WMA, int WMB>
+__global__ void __launch_bounds__(kBlock)
+k_fixed_tx2(uint8_t* __restrict__ frames, uint64_t stride, u32 frame_len, u32 n,
+            uint8_t* __restrict__ out_code, uint32_t* __restrict__ out_csum, u32 flags, u32 split)
+{
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);    // block-uniform choice below
+    if (blk < split)
+        fixed_frame<G, U, true, LOOP, kNT, WMA, false, false>(frames, stride, frame_len, n,
+                                                              out_code, out_csum, flags, Ext{},
+                                                              blk, gridDim.x);
+    else
+        fixed_frame<G, U, true, LOOP, kNT, WMB, false, false>(frames, stride, frame_len, n,
+                                                              out_code, out_csum, flags, Ext{},
+                                                              blk, gridDim.x);
 }
 
 template <int G, int U, bool COMPUTE, bool LOOP, bool EXT, int K = 1>
@@ -2588,32 +2673,24 @@ static hipError_t launch_fixed(uint8_t* frames, uint64_t stride, u32 frame_len, 
                                hipStream_t s)
 {
     if constexpr (COMPUTE && G >= 8) {
-        if (stride % 128 == 0 && (uint64_t)n * 128 <= line_wb_bytes() &&
-            !(flags & GCS_CF_SECTOR_WB))
+        constexpr u32 FPB = kBlock / G * K;
+        const TxWb wb = tx_wb(stride, n, flags, FPB);
+        if (wb.mode == 1)
             return launch_fixed_wm<G, U, COMPUTE, LOOP, EXT, K, WM_LINE_SC1>(
                 frames, stride, frame_len, n, code, csum, flags, ext, s);
-        const int hy = tx_hybrid();
-        constexpr u32 FPB = kBlock / G * K;
-        const u32 m = (u32)(line_wb_bytes() / 128) / FPB * FPB;
-        if (hy && stride % 128 == 0 && !(flags & GCS_CF_SECTOR_WB) && m > 0 && m < n) {
-            auto part = [&](u32 a, u32 b, bool line) -> hipError_t {
-                uint8_t* f = frames + (uint64_t)a * stride;
-                uint8_t* c = code ? code + a : nullptr;
-                uint32_t* k = csum ? csum + a : nullptr;
-                if (line)
-                    return launch_fixed_wm<G, U, COMPUTE, LOOP, EXT, K, WM_LINE_SC1>(
-                        f, stride, frame_len, b - a, c, k, flags, ext, s);
-                if (hy == 2 || hy == 4)
-                    return launch_fixed_wm<G, U, COMPUTE, LOOP, EXT, K, WM_SECTOR_NT>(
-                        f, stride, frame_len, b - a, c, k, flags, ext, s);
-                return launch_fixed_wm<G, U, COMPUTE, LOOP, EXT, K>(f, stride, frame_len, b - a,
-                                                                    c, k, flags, ext, s);
-            };
-            const bool line_last = hy >= 3;
-            hipError_t e = line_last ? part(m, n, false) : part(0, m, true);
-            if (e != hipSuccess)
-                return e;
-            return line_last ? part(0, m, true) : part(m, n, false);
+        if constexpr (!EXT && K == 1) {
+            if (wb.mode >= 2) {
+                const dim3 grid((n + FPB - 1) / FPB);
+                if (wb.mode == 2)
+                    hipLaunchKernelGGL((k_fixed_tx2<G, U, LOOP, WM_LINE_SC1, WM_SECTOR_NT>), grid,
+                                       dim3(kBlock), 0, s, frames, stride, frame_len, n, code,
+                                       csum, flags, wb.split);
+                else
+                    hipLaunchKernelGGL((k_fixed_tx2<G, U, LOOP, WM_LINE_SC1, kWM>), grid,
+                                       dim3(kBlock), 0, s, frames, stride, frame_len, n, code,
+                                       csum, flags, wb.split);
+                return hipGetLastError();
+            }
         }
     }
     return launch_fixed_wm<G, U, COMPUTE, LOOP, EXT, K>(frames, stride, frame_len, n, code, csum,
@@ -2665,6 +2742,71 @@ static hipError_t dispatch_fixed(uint8_t* frames, uint64_t stride, u32 frame_len
     if (chunks <= 96)  return launch_fixed<32, 3, COMPUTE, false, EXT>(frames, stride, frame_len, n, code, csum, flags, ext, s);
     if (chunks <= 128) return launch_fixed<64, 2, COMPUTE, false, EXT>(frames, stride, frame_len, n, code, csum, flags, ext, s);
     return launch_fixed<64, 4, COMPUTE, true, EXT>(frames, stride, frame_len, n, code, csum, flags, ext, s);
+}
+
+template <int G, int U, bool LOOP>
+static hipError_t launch_step_gu(uint8_t* tx, uint64_t tx_stride, u32 tx_len, u32 ntx,
+                                 uint8_t* tx_code, uint32_t* tx_csum, u32 tx_flags, uint8_t* rx,
+                                 uint64_t rx_stride, u32 rx_len, u32 nrx, uint8_t* rx_code,
+                                 u32 rx_flags, hipStream_t s)
+{
+    constexpr u32 FPB = kBlock / G;
+    const u32 txb = ((ntx + FPB - 1) / FPB + 7) & ~7u;   // a multiple of 8 (XCD order)
+    const dim3 grid(txb + (nrx + FPB - 1) / FPB);
+    const TxWb wb = tx_wb(tx_stride, ntx, tx_flags, FPB);
+#define GCS_STEP_K(A_, B_, SPLIT_)                                                            \
+    hipLaunchKernelGGL((k_fixed_step<G, U, LOOP, A_, B_>), grid, dim3(kBlock), 0, s, tx,       \
+                       tx_stride, tx_len, ntx, tx_code, tx_csum, tx_flags, rx, rx_stride,     \
+                       rx_len, nrx, rx_code, rx_flags, txb, SPLIT_)
+    switch (wb.mode) {
+    case 1: GCS_STEP_K(WM_LINE_SC1, WM_LINE_SC1, txb); break;
+    case 2: GCS_STEP_K(WM_LINE_SC1, WM_SECTOR_NT, wb.split); break;
+    case 3: GCS_STEP_K(WM_LINE_SC1, kWM, wb.split); break;
+    default: GCS_STEP_K(kWM, kWM, 0u); break;
+    }
+#undef GCS_STEP_K
+    return hipGetLastError();
+}
+
+// The (G, U) shape dispatch_fixed picks for frames of `chunks` 16 B chunks
+// (0: <= 64 B, the one-lane / 4-lane kernels).
+static int fixed_shape(u32 chunks)
+{
+    return chunks <= 4 ? 0 : chunks <= 8 ? 1 : chunks <= 16 ? 2 : chunks <= 32 ? 3
+         : chunks <= 64 ? 4 : chunks <= 96 ? 5 : chunks <= 128 ? 6 : 7;
+}
+
+hipError_t launch_step_fixed(uint8_t* tx, uint64_t tx_stride, u32 tx_len, u32 ntx,
+                             uint8_t* tx_code, uint32_t* tx_csum, u32 tx_flags, uint8_t* rx,
+                             uint64_t rx_stride, u32 rx_len, u32 nrx, uint8_t* rx_code,
+                             u32 rx_flags, hipStream_t s)
+{
+    const int sh = fixed_shape((tx_len + 15) / 16);
+    // one launch when both batches take the same plain kernel shape; else
+    // (ICMP extensions, different shapes, frames <= 64 B) the two launches
+    // it stands for
+    if (ntx == 0 || nrx == 0 || sh == 0 || sh != fixed_shape((rx_len + 15) / 16) ||
+        (tx_flags & GCS_CF_ICMP) || (rx_flags & GCS_VF_ICMP)) {
+        hipError_t e = ntx ? launch_compute_fixed(tx, tx_stride, tx_len, ntx, tx_code, tx_csum,
+                                                  tx_flags, s)
+                           : hipSuccess;
+        if (e != hipSuccess || nrx == 0)
+            return e;
+        return launch_verify_fixed(rx, rx_stride, rx_len, nrx, rx_code, rx_flags, s);
+    }
+#define GCS_STEP(G_, U_, L_)                                                                      \
+    return launch_step_gu<G_, U_, L_>(tx, tx_stride, tx_len, ntx, tx_code, tx_csum, tx_flags, rx, \
+                                      rx_stride, rx_len, nrx, rx_code, rx_flags, s)
+    switch (sh) {
+    case 1: GCS_STEP(8, 1, false);
+    case 2: GCS_STEP(16, 1, false);
+    case 3: GCS_STEP(32, 1, false);
+    case 4: GCS_STEP(32, 2, false);
+    case 5: GCS_STEP(32, 3, false);
+    case 6: GCS_STEP(64, 2, false);
+    default: GCS_STEP(64, 4, true);
+    }
+#undef GCS_STEP
 }
 
 hipError_t launch_verify_fixed(uint8_t* frames, uint64_t stride, u32 frame_len, u32 n,

@@ -82,6 +82,8 @@ def lib() -> C.CDLL:
             "gcs_dev_free": (i, [vp, vp]),
             "gcs_verify_fixed_dev": (i, [vp, vp, u64, u32, u32, vp, u32, vp]),
             "gcs_compute_fixed_dev": (i, [vp, vp, u64, u32, u32, vp, vp, u32, vp]),
+            "gcs_step_fixed_dev": (i, [vp, vp, u64, u32, u32, vp, vp, u32, vp, u64, u32, u32,
+                                       vp, u32, vp]),
             "gcs_verify_dev": (i, [vp, vp, u64, vp, vp, u32, vp, u32, vp]),
             "gcs_compute_dev": (i, [vp, vp, u64, vp, vp, u32, vp, vp, u32, vp]),
             "gcs_tcp_checksum_dev": (i, [vp, vp, u64, vp, vp, vp, vp, u32, vp, vp]),
@@ -241,6 +243,20 @@ class Context:
         check(self.L.gcs_compute_fixed_dev(self.h, _daddr(frames), stride, frame_len, n,
                                            _daddr(status), _daddr(csums), flags, stream),
               "compute_fixed")
+
+    def step_fixed(self, tx, tx_stride, tx_len, n_tx, rx, rx_stride, rx_len, n_rx, verdict,
+                   tx_status=None, tx_csums=None, tx_flags=0, rx_flags=0, stream=None):
+        """gcs_step_fixed_dev: TX fill of `tx` and RX verify of `rx` in one launch."""
+        _torch_ordered(stream, tx, rx, verdict, tx_status, tx_csums)
+        self._need(tx, n_tx * tx_stride, "tx")
+        self._need(rx, n_rx * rx_stride, "rx")
+        self._need(verdict, n_rx, "verdict")
+        self._need(tx_status, n_tx, "tx_status")
+        self._need(tx_csums, 4 * n_tx, "tx_csums")
+        check(self.L.gcs_step_fixed_dev(self.h, _daddr(tx), tx_stride, tx_len, n_tx,
+                                        _daddr(tx_status), _daddr(tx_csums), tx_flags, _daddr(rx),
+                                        rx_stride, rx_len, n_rx, _daddr(verdict), rx_flags,
+                                        stream), "step_fixed")
 
     def verify(self, frames, off, lens, n, verdict, flags=0, stream=None, frames_bytes=None):
         _torch_ordered(stream, frames, off, lens, verdict)

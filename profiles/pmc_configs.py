@@ -11,9 +11,10 @@ WRITE_SIZE / duration per configuration -- per kernel AND per launch size,
 which bench.py then looks up for its roofline.traffic.
 
 Labels: <op>_<layout>_<frame_len|imix>_<frames per launch>, e.g.
-compute_fixed_1500_4194304 is the TX fill of a C4 shard; step_* are the two
-launches of the bench step (fill of one batch, then verify of another, back
-to back, as bench.py times them), each with its own label.
+compute_fixed_1500_4194304 is the TX fill of a C4 shard; step_fixed_* is the
+bench step's ONE launch (gcs_step_fixed_dev: the fill of one batch and the
+verify of another); split_step_* are the same step as two launches back to
+back (the round-5 bench step), each with its own label.
 
 --scrub writes, then reads, 1 GiB (four times the Infinity Cache) between
 launches, outside the HIP events, so each launch starts with nothing of its
@@ -83,7 +84,7 @@ def main():
         print(f"{label:36s} {med * 1e3:9.1f} us  {bytes_alg / (med * 1e-3) / 1e9:8.0f} GB/s",
               file=sys.stderr, flush=True)
 
-    def fixed(L, n, ops=("compute", "verify")):
+    def fixed(L, n, ops=("compute", "verify", "step")):
         tx, stride = synth.fixed_frames_device(n, L, seed=0x5EED ^ n ^ L)
         rx = tx.clone()
         setup(ctx.compute_fixed, rx, stride, L, n)
@@ -94,6 +95,10 @@ def main():
         if "verify" in ops:
             measure(f"verify_fixed_{L}_{n}",
                     lambda: ctx.verify_fixed(rx, stride, L, n, v, stream=stream), n * (L + 1))
+        if "step" in ops and L > 64:
+            measure(f"step_fixed_{L}_{n}",
+                    lambda: ctx.step_fixed(tx, stride, L, n, rx, stride, L, n, v, stream=stream),
+                    n * (2 * L + 5))
         torch.cuda.synchronize()
         assert int((v != 0).sum()) == 0
         return tx, rx, stride, v
@@ -121,16 +126,18 @@ def main():
             for _ in range(a.reps):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                manifest.extend([f"step_compute_fixed_{L}_{n}", f"step_verify_fixed_{L}_{n}"])
+                manifest.extend([f"split_step_compute_fixed_{L}_{n}",
+                                 f"split_step_verify_fixed_{L}_{n}"])
                 ctx.compute_fixed(tx, stride, L, n, stream=stream)
                 ctx.verify_fixed(rx, stride, L, n, v, stream=stream)
                 e1.record()
                 torch.cuda.synchronize()
                 ms.append(e0.elapsed_time(e1))
             med = float(np.median(ms))
-            timings[f"step_fixed_{L}_{n}"] = {"median_us": med * 1e3,
-                                              "bytes_algorithmic": n * (2 * L + 5)}
-            print(f"step_fixed_{L}_{n:<22d} {med * 1e3:9.1f} us", file=sys.stderr, flush=True)
+            timings[f"split_step_fixed_{L}_{n}"] = {"median_us": med * 1e3,
+                                                    "bytes_algorithmic": n * (2 * L + 5)}
+            print(f"split_step_fixed_{L}_{n:<16d} {med * 1e3:9.1f} us", file=sys.stderr,
+                  flush=True)
             assert int((v != 0).sum()) == 0
             del tx, rx
         elif c == "C2rooms":

@@ -22,3 +22,12 @@ c4 c4_nt_$r GCS_TX_HYBRID=nt
 c4 c4_sc1ll_$r GCS_TX_HYBRID=sc1_linelast
 c4 c4_ntll_$r GCS_TX_HYBRID=nt_linelast
 done
+sl() { local name=$1; shift; env "$@" timeout -k 10 180 python -u tools/server_lro.py > $O/$name.json 2> $O/$name.err || { tail -5 $O/$name.err; exit 1; }; cat $O/$name.json; }
+sl sl_t8_lds96 SL_THREADS=8
+sl sl_t8_lds0 SL_THREADS=8 GCS_SERVER_LDS_KB=0
+sl sl_t16_lds96 SL_THREADS=16
+sl sl_t16_lds0 SL_THREADS=16 GCS_SERVER_LDS_KB=0
+timeout -k 10 600 python -u -m pytest tests/test_gpu_step.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_step.log 2>&1 || { tail -40 $O/pytest_step.log; exit 1; }
+tail -2 $O/pytest_step.log
+for r in 1 2; do timeout -k 10 180 python -u tools/step_ab.py > $O/step_ab_$r.json 2> $O/step_ab_$r.err || { tail -5 $O/step_ab_$r.err; exit 1; }; cat $O/step_ab_$r.json; done
+SA_FRAMES=4194304 timeout -k 10 180 python -u tools/step_ab.py > $O/step_ab_4m.json 2> $O/step_ab_4m.err || { tail -5 $O/step_ab_4m.err; exit 1; }; cat $O/step_ab_4m.json
