@@ -124,12 +124,36 @@ __global__ void __launch_bounds__(kBlock)
 k_fixed_step(uint8_t* __restrict__ tx, uint64_t tx_stride, u32 tx_len, u32 ntx,
              uint8_t* __restrict__ tx_code, uint32_t* __restrict__ tx_csum, u32 tx_flags,
              uint8_t* __restrict__ rx, uint64_t rx_stride, u32 rx_len, u32 nrx,
-             uint8_t* __restrict__ rx_code, u32 rx_flags, u32 tx_blocks, u32 tx_split)
+             uint8_t* __restrict__ rx_code, u32 rx_flags, u32 tx_blocks, u32 tx_split,
+             u32 rx_blocks, u32 order)
 {
+    // which part this block serves, and its index in that part: order 0 =
+    // the TX blocks first, 1 = the RX blocks first, 2 = 8-block groups of
+    // the two alternating (both block counts are multiples of 8, so a block
+    // keeps its XCD, b % 8, in its part)
+    uint32_t b = blockIdx.x;
+    bool is_tx;
+    if (order == 0) {
+        is_tx = b < tx_blocks;
+        b = is_tx ? b : b - tx_blocks;
+    } else if (order == 1) {
+        is_tx = b >= rx_blocks;
+        b = is_tx ? b - rx_blocks : b;
+    } else {
+        const uint32_t g = b / 8, gt = tx_blocks / 8, gr = rx_blocks / 8;
+        const uint32_t both = gt < gr ? gt : gr;
+        if (g < 2 * both) {
+            is_tx = (g & 1) == 0;
+            b = (g / 2) * 8 + b % 8;
+        } else {
+            is_tx = gt > gr;
+            b = (both + g - 2 * both) * 8 + b % 8;
+        }
+    }
     // the fill's write-back as launch_fixed picks it (k_fixed_tx2): WMA for
     // its logical blocks [0, tx_split), WMB after
-    if (blockIdx.x < tx_blocks) {
-        const uint32_t blk = xcd_block(blockIdx.x, tx_blocks);
+    if (is_tx) {
+        const uint32_t blk = xcd_block(b, tx_blocks);
         if (blk < tx_split)
             fixed_frame<G, U, true, LOOP, kNT, WMA, false, false>(tx, tx_stride, tx_len, ntx,
                                                                   tx_code, tx_csum, tx_flags,
@@ -140,9 +164,8 @@ k_fixed_step(uint8_t* __restrict__ tx, uint64_t tx_stride, u32 tx_len, u32 ntx,
                                                                   Ext{}, blk, tx_blocks);
     } else {
         fixed_frame<G, U, false, LOOP, kNT, kWM, kXCD, false>(rx, rx_stride, rx_len, nrx, rx_code,
-                                                              nullptr, rx_flags, Ext{},
-                                                              blockIdx.x - tx_blocks,
-                                                              gridDim.x - tx_blocks);
+                                                              nullptr, rx_flags, Ext{}, b,
+                                                              rx_blocks);
     }
 }
 
@@ -2751,13 +2774,19 @@ static hipError_t launch_step_gu(uint8_t* tx, uint64_t tx_stride, u32 tx_len, u3
                                  u32 rx_flags, hipStream_t s)
 {
     constexpr u32 FPB = kBlock / G;
-    const u32 txb = ((ntx + FPB - 1) / FPB + 7) & ~7u;   // a multiple of 8 (XCD order)
-    const dim3 grid(txb + (nrx + FPB - 1) / FPB);
+    const u32 txb = ((ntx + FPB - 1) / FPB + 7) & ~7u;   // multiples of 8 (XCD order)
+    const u32 rxb = ((nrx + FPB - 1) / FPB + 7) & ~7u;
+    const dim3 grid(txb + rxb);
     const TxWb wb = tx_wb(tx_stride, ntx, tx_flags, FPB);
+    // GCS_STEP_ORDER (A/B knob, read once): tx (default), rx, mix
+    static const u32 order = [] {
+        const char* e = std::getenv("GCS_STEP_ORDER");
+        return !e ? 0u : std::strcmp(e, "rx") == 0 ? 1u : std::strcmp(e, "mix") == 0 ? 2u : 0u;
+    }();
 #define GCS_STEP_K(A_, B_, SPLIT_)                                                            \
     hipLaunchKernelGGL((k_fixed_step<G, U, LOOP, A_, B_>), grid, dim3(kBlock), 0, s, tx,       \
                        tx_stride, tx_len, ntx, tx_code, tx_csum, tx_flags, rx, rx_stride,     \
-                       rx_len, nrx, rx_code, rx_flags, txb, SPLIT_)
+                       rx_len, nrx, rx_code, rx_flags, txb, SPLIT_, rxb, order)
     switch (wb.mode) {
     case 1: GCS_STEP_K(WM_LINE_SC1, WM_LINE_SC1, txb); break;
     case 2: GCS_STEP_K(WM_LINE_SC1, WM_SECTOR_NT, wb.split); break;
