@@ -441,6 +441,74 @@ def test_async_fill_without_server_is_synchronous(torch_dev):
     np.testing.assert_array_equal(buf, ref)
 
 
+def test_server_requests_of_every_size_and_mode_over_the_slots(torch_dev):
+    """ADVICE r05 (torn request lines): 1,600 async requests on ONE ring -- fills
+    and verifies at random, 1..64 frames each, verifies with and without the
+    tcp_in.c:1237 side effect -- so every one of the ring's 8 slots is reused
+    ~200 times with n and mode changing each time.  A poll that took a line
+    half from the slot's previous request would serve the wrong count, the
+    wrong kind or the wrong frames; every status, check, verdict and frame
+    must equal the oracle's."""
+    import ctypes as C
+    L = gpucsum.lib()
+    L.gcs_verify_ptrs_async.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                        C.c_void_p, C.c_uint32, C.POINTER(C.c_uint64)]
+    L.gcs_compute_ptrs_async.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                         C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64)]
+    L.gcs_wait.argtypes = [C.c_void_p, C.c_uint64]
+    O = Oracle()
+    rng = np.random.default_rng(2606)
+    reqs = 1600
+    sizes = rng.integers(1, 65, size=reqs)
+    kinds = rng.integers(0, 3, size=reqs)          # 0 fill, 1 verify, 2 verify + side effect
+    n = int(sizes.sum())
+    buf, off, lens = synth.packed_frames(synth.imix_lengths(n, seed=2607), seed=2608)
+    is_rx = np.repeat(kinds != 0, sizes)
+    rx_idx = np.nonzero(is_rx)[0]
+    O.compute_batch(buf, off[rx_idx], lens[rx_idx])   # RX frames carry valid checks ...
+    synth.corrupt(buf, off[rx_idx], lens[rx_idx], frac_log2=3, seed=2609)   # ... some broken
+    ref = buf.copy()
+    exp_code = np.zeros(n, np.uint8)
+    exp_cs = np.zeros(n, np.uint32)
+    i = 0
+    for m, k in zip(sizes, kinds):
+        sl = slice(i, i + int(m))
+        if k == 0:
+            exp_code[sl], exp_cs[sl] = O.compute_batch(ref, off[sl], lens[sl])
+        else:
+            exp_code[sl] = O.verify_batch(ref, off[sl], lens[sl], flags=1 if k == 2 else 0)
+        i += int(m)
+    ptrs = (C.c_void_p * n)(*[buf.ctypes.data + int(o) for o in off])
+    code = np.full(n, 0xEE, np.uint8)
+    cs = np.zeros(n, np.uint32)
+    with gpucsum.Context(0, max_frames=4096, max_bytes=8 << 20) as c:
+        c.set_burst_server(True)
+        tickets = []
+        i = 0
+        for r, (m, k) in enumerate(zip(sizes, kinds)):
+            m = int(m)
+            t = C.c_uint64()
+            p = C.cast(C.byref(ptrs, 8 * i), C.c_void_p)
+            if k == 0:
+                gpucsum.check(L.gcs_compute_ptrs_async(c.h, p, lens.ctypes.data + 2 * i, m,
+                                                       code.ctypes.data + i, cs.ctypes.data + 4 * i,
+                                                       C.byref(t)))
+            else:
+                gpucsum.check(L.gcs_verify_ptrs_async(c.h, p, lens.ctypes.data + 2 * i, m,
+                                                      code.ctypes.data + i, 1 if k == 2 else 0,
+                                                      C.byref(t)))
+            assert t.value != 0
+            tickets.append(t.value)
+            i += m
+            if r % 37 == 36:
+                gpucsum.check(L.gcs_wait(c.h, tickets[-int(rng.integers(1, 9))]))
+        gpucsum.check(L.gcs_wait(c.h, tickets[-1]))
+    np.testing.assert_array_equal(code, exp_code)
+    tx = ~is_rx
+    np.testing.assert_array_equal(cs[tx], exp_cs[tx])
+    np.testing.assert_array_equal(buf, ref)
+
+
 def test_failed_wait_reports_later_requests_to_their_own_wait(torch_dev, monkeypatch):
     """A failed gcs_wait reports the cancelled fills up to its ticket; fills
     posted after that ticket stay cancelled and fail their OWN wait once
