@@ -1114,35 +1114,39 @@ def main():
         "corrupted_frames_detected": bad_seen,
     }
     if rank == 0 and world == 1:
+        def side(key, fn):
+            """A side measurement: its failure is reported in the line, never
+            allowed to cost the line itself (printed after all of them)."""
+            try:
+                line[key] = fn()
+            except Exception as e:   # noqa: BLE001
+                line[key] = {"error": repr(e)[:300]}
+            torch.cuda.empty_cache()
+
         if args.cpu_seconds > 0:
-            line["cpu_baseline"] = cpu_baseline(tx, rx, stride, L, args.cpu_seconds,
-                                                args.cpu_sample, torch)
+            side("cpu_baseline", lambda: cpu_baseline(tx, rx, stride, L, args.cpu_seconds,
+                                                      args.cpu_sample, torch))
         if not args.no_extras:
-            line["c2_sector_wb"] = c2_sector_wb(ctx, torch, tx, stride, L, n)
-            sec = line["c2_sector_wb"]
-            line["roofline"]["sector_wb_frac"] = sec["sector_frac_peak"]
-            line["c2_fresh_cold"] = c2_fresh_cold(ctx, torch, tx, stride, L, n)
-            line["roofline"]["fresh_cold_frac"] = line["c2_fresh_cold"]["compute_frac_peak"]
+            side("c2_sector_wb", lambda: c2_sector_wb(ctx, torch, tx, stride, L, n))
+            if "sector_frac_peak" in line["c2_sector_wb"]:
+                line["roofline"]["sector_wb_frac"] = line["c2_sector_wb"]["sector_frac_peak"]
+            side("c2_fresh_cold", lambda: c2_fresh_cold(ctx, torch, tx, stride, L, n))
+            if "compute_frac_peak" in line["c2_fresh_cold"]:
+                line["roofline"]["fresh_cold_frac"] = line["c2_fresh_cold"]["compute_frac_peak"]
             del tx, rx
-            torch.cuda.empty_cache()
-            line["c4_shard"] = c4_shard(ctx, torch, args.steps, args.warmup, args.settle_s)
-            torch.cuda.empty_cache()
-            line["c1_64B"] = c1_small_frames(ctx, torch)
-            line["c1_64B_8M"] = c1_small_frames(ctx, torch, n=8 << 20)
-            line["c2_1514B"] = c2_max_frame(ctx, torch)
-            torch.cuda.empty_cache()
-            line["c3_imix"] = c3_imix(ctx, torch)
-            torch.cuda.empty_cache()
-            line["c2_rooms"] = c2_rooms(ctx, torch)
-            torch.cuda.empty_cache()
-            line["rows_8f"] = rows_8f(ctx, torch)
-            torch.cuda.empty_cache()
-            line["pcie_inclusive"] = pcie_inclusive(gpucsum, torch)
-            line["plugin_bursts"] = plugin_bursts(gpucsum)
-            line["plugin_threads"] = plugin_threads()
-            line["plugin_tx_async"] = plugin_tx_async()
-            line["plugin_rx_async"] = plugin_rx_async()
-            line["server_poll_cost"] = server_poll_cost()
+            side("c4_shard", lambda: c4_shard(ctx, torch, args.steps, args.warmup, args.settle_s))
+            side("c1_64B", lambda: c1_small_frames(ctx, torch))
+            side("c1_64B_8M", lambda: c1_small_frames(ctx, torch, n=8 << 20))
+            side("c2_1514B", lambda: c2_max_frame(ctx, torch))
+            side("c3_imix", lambda: c3_imix(ctx, torch))
+            side("c2_rooms", lambda: c2_rooms(ctx, torch))
+            side("rows_8f", lambda: rows_8f(ctx, torch))
+            side("pcie_inclusive", lambda: pcie_inclusive(gpucsum, torch))
+            side("plugin_bursts", lambda: plugin_bursts(gpucsum))
+            side("plugin_threads", plugin_threads)
+            side("plugin_tx_async", plugin_tx_async)
+            side("plugin_rx_async", plugin_rx_async)
+            side("server_poll_cost", server_poll_cost)
     ctx.close()
     if rank == 0:
         extras = None
