@@ -687,8 +687,13 @@ static void gpucsum_destroy_handle(struct mtcp_thread_context *ctx)
 	pthread_mutex_unlock(&g_lock);
 	if (t_cache == g)
 		t_cache = NULL;
-	if (g->gcs)
-		gcs_ctx_destroy(g->gcs);
+	if (g->gcs) {
+		/* the context drains its ring and streams first: a device fault that
+		 * surfaces there is this thread's, reported as a GPU failure */
+		int rc = gcs_ctx_destroy(g->gcs);
+		if (rc)
+			gpu_failed(g, "context teardown", 0, rc);
+	}
 	for (i = 0; i < GPUCSUM_MAX_IFS; i++) {
 		if (g->rx[i]) {
 			free(g->rx[i]->ptr);
