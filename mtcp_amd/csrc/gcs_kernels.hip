@@ -369,14 +369,14 @@ __device__ __forceinline__ uint64_t clock_after_vmem()
     return __builtin_amdgcn_s_memrealtime();
 }
 
-template <int G, int U, bool PROF>
-__global__ void __launch_bounds__(kBlock)
+template <int G, int U, bool PROF, int BT = kBlock>
+__global__ void __launch_bounds__(BT)
 k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, uint64_t life_ticks,
                uint64_t hot_ticks, uint64_t hot_max_ticks, uint32_t max_polls, uint32_t naps,
                uint32_t opts)
 {
     enum { IDLE = 0, WORK = 1, EXIT = 2, SKIP = 3 };
-    constexpr int FPB = kBlock / G;
+    constexpr int FPB = BT / G;
     static_assert(FPB == kServerFPB, "the mailbox's frames per block and pass");
     constexpr int kPass = kServerBlocks * FPB;          // frames of one request per pass
     constexpr int kLanes = 2 + FPB;                     // lines of a poll
@@ -767,6 +767,8 @@ hipError_t launch_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, int gro
         return e ? std::atoi(e) : kLdsMaxGroups;
     }();
     const size_t lds = groups <= lds_groups ? lds_kb << 10 : 0;
+    // (a 512-thread shape, 64 lanes x 2 chunks per frame, measured no faster:
+    // RX frame phase 4.16-4.20 vs 4.01-4.02 us per 64 x 1500 B)
     if (lds > 65536) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_burst_server<32, 3, true>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
