@@ -26,13 +26,17 @@
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-__global__ void k_pull(const u32x4* __restrict__ src, uint64_t chunks, uint32_t* __restrict__ out)
+// rooms: chunk c of the burst is chunk c % 96 of frame c / 96, frames one per
+// 2 KiB room (the server's layout) instead of packed
+__global__ void k_pull(const u32x4* __restrict__ src, uint64_t chunks, uint32_t* __restrict__ out,
+                       int rooms)
 {
     uint32_t s = 0;
 #pragma unroll 8
     for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < chunks;
          c += (uint64_t)gridDim.x * blockDim.x) {
-        const u32x4 v = __builtin_nontemporal_load(&src[c]);
+        const uint64_t a = rooms ? (c / 96) * 128 + c % 96 : c;
+        const u32x4 v = __builtin_nontemporal_load(&src[a]);
         s += v.x ^ v.y ^ v.z ^ v.w;
     }
     s = __reduce_add_sync(0xFFFFFFFFFFFFFFFFull, s);
@@ -43,8 +47,9 @@ __global__ void k_pull(const u32x4* __restrict__ src, uint64_t chunks, uint32_t*
 int main(int argc, char** argv)
 {
     const bool cached = argc > 1 && std::strcmp(argv[1], "cached") == 0;
+    const int rooms = argc > 2 && std::strcmp(argv[2], "rooms") == 0;
     const size_t bytes = 64 * 1536;
-    const size_t alloc = bytes + 8192;
+    const size_t alloc = 64 * 2048 + 8192;
     uint8_t* host = static_cast<uint8_t*>(std::aligned_alloc(4096, alloc));
     std::memset(host, 0x5A, alloc);
     CHECK(hipHostRegister(host, alloc, cached ? hipHostRegisterMapped
@@ -56,17 +61,17 @@ int main(int argc, char** argv)
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
     CHECK(hipEventCreate(&e1));
-    std::printf("{\"region\": \"%s\", \"bytes\": %zu, \"rows\": [", cached ? "cached" : "uncached",
-                bytes);
+    std::printf("{\"region\": \"%s\", \"layout\": \"%s\", \"bytes\": %zu, \"rows\": [",
+                cached ? "cached" : "uncached", rooms ? "rooms" : "packed", bytes);
     bool first = true;
     for (int threads : {256, 1024}) {
         for (int blocks : {1, 2, 4, 8, 16, 32, 64, 128}) {
             std::vector<float> ms;
             for (int r = 0; r < 220; r++) {
-                std::memset(host, r & 0xFF, bytes);          // fresh frames, as a NIC writes them
+                std::memset(host, r & 0xFF, 64 * 2048);      // fresh frames, as a NIC writes them
                 CHECK(hipEventRecord(e0, 0));
                 hipLaunchKernelGGL(k_pull, dim3(blocks), dim3(threads), 0, 0,
-                                   reinterpret_cast<const u32x4*>(dev), bytes / 16, out);
+                                   reinterpret_cast<const u32x4*>(dev), bytes / 16, out, rooms);
                 CHECK(hipEventRecord(e1, 0));
                 CHECK(hipEventSynchronize(e1));
                 float t = 0;
@@ -86,7 +91,7 @@ int main(int argc, char** argv)
     for (int r = 0; r < 220; r++) {
         CHECK(hipEventRecord(e0, 0));
         hipLaunchKernelGGL(k_pull, dim3(8), dim3(256), 0, 0, reinterpret_cast<const u32x4*>(dev),
-                           (uint64_t)0, out);
+                           (uint64_t)0, out, 0);
         CHECK(hipEventRecord(e1, 0));
         CHECK(hipEventSynchronize(e1));
         float t = 0;
