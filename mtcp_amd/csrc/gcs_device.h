@@ -189,10 +189,17 @@ __device__ __forceinline__ u32 group_bcast(u32 x)
 }
 
 // One global_load_dwordx4; NT adds the non-temporal (streaming) cache hint.
+// Frames are always global memory (HBM or registered host memory); the cast to
+// address space 1 makes that explicit, so a pointer the compiler cannot trace
+// (one read from LDS or a request ring) still gets global_load, not flat_load
+// (a flat op also waits on lgkmcnt and takes the aperture check).
+typedef const __attribute__((address_space(1))) u32x4 gu32x4;
+typedef const __attribute__((address_space(1))) uint8_t gu8;
+
 template <bool NT>
 __device__ __forceinline__ uint4 ldg16(const uint8_t* p)
 {
-    const u32x4* q = reinterpret_cast<const u32x4*>(p);
+    gu32x4* q = (gu32x4*)(p);
     u32x4 r = NT ? __builtin_nontemporal_load(q) : *q;
     return make_uint4(r.x, r.y, r.z, r.w);
 }
@@ -228,7 +235,7 @@ __device__ __forceinline__ uint4 load_chunk(const uint8_t* p, int64_t avail)
     uint8_t b[16];
 #pragma unroll
     for (int k = 0; k < 16; k++)
-        b[k] = (k < avail) ? p[k] : 0;
+        b[k] = (k < avail) ? ((gu8*)p)[k] : 0;
     uint4 v;
     v.x = b[0] | (b[1] << 8) | (b[2] << 16) | ((u32)b[3] << 24);
     v.y = b[4] | (b[5] << 8) | (b[6] << 16) | ((u32)b[7] << 24);
