@@ -442,8 +442,10 @@ class ServerHub {
         // GCS_SERVER_ACQUIRE (A/B knobs, gcs_internal.h kServerAcq*): agent =
         // every acquire at agent scope (frames in registered host memory may
         // then be read from a stale L2 line); none = no acquire for frames in
-        // device staging.  Default: agent scope for device frames, system
-        // scope for host frames.
+        // device staging or in an uncached registered region (A/B only: a
+        // CU's L1 may still hold an earlier request's lines).  Default: agent
+        // scope for device frames, the L1 invalidate for uncached host frames,
+        // system scope for other host frames.
         const char* acq = std::getenv("GCS_SERVER_ACQUIRE");
         opts_ = !acq                         ? 0u
                 : std::strcmp(acq, "agent") == 0 ? gcs::kServerAcqAgent

@@ -214,8 +214,9 @@ hipError_t launch_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, int gro
 // host writes over the BAR and the XCD L2s keep coherent) takes an
 // agent-scope acquire (the CU's L1 only), one whose frames are in host memory
 // a system-scope one (which also invalidates the L2's non-coherent lines: a
-// registered mbuf pool).  kServerAcqAgent: agent scope always; kServerAcqNone:
-// no acquire for device frames.
+// registered mbuf pool), and one in an uncached registered region
+// (kModeUncachedFrames) the CU's L1 invalidate alone.  kServerAcqAgent: agent
+// scope always; kServerAcqNone: no acquire for device or uncached frames.
 constexpr uint32_t kServerAcqAgent = 1u;
 constexpr uint32_t kServerAcqNone = 2u;
 

@@ -596,7 +596,7 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
             const uint4 a = s_line[0], b = s_line[1];
             const bool dev = (a.w & kModeDevFrames) != 0;   // block-uniform
             const bool unc = (a.w & kModeUncachedFrames) != 0;
-            if (dev && (opts & kServerAcqNone))
+            if ((dev || unc) && (opts & kServerAcqNone))
                 ;
             else if (unc && !(opts & kServerAcqAgent))
                 asm volatile("buffer_inv sc0" ::: "memory");   // the CU's L1 only
