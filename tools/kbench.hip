@@ -192,6 +192,32 @@ __global__ void __launch_bounds__(256) k_line_writes(uint8_t* __restrict__ buf, 
         return;
     stg16<WM>(buf + line + 16ull * c, make_uint4((u32)f, c, 0x1173u, 0u));
 }
+// (d): the check fields alone -- the 2 B IP check at +24 and the 2 B TCP check
+// at +50 of each frame -- one lane per frame, two 2 B stores (0 plain, 1 nt,
+// 2 sc1): whether partial sectors write back cheaper than whole ones.
+template <int P>
+__global__ void __launch_bounds__(256) k_field_writes(uint8_t* __restrict__ buf,
+                                                      const uint64_t* __restrict__ off, u32 n)
+{
+    const uint64_t f = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (f >= n)
+        return;
+    uint16_t* a = reinterpret_cast<uint16_t*>(buf + off[f] + 24);
+    uint16_t* b = reinterpret_cast<uint16_t*>(buf + off[f] + 50);
+    const uint16_t x = (uint16_t)f, y = (uint16_t)(f >> 16);
+    if constexpr (P == 1) {
+        __builtin_nontemporal_store(x, a);
+        __builtin_nontemporal_store(y, b);
+    } else if constexpr (P == 2) {
+        asm volatile("global_store_short %0, %1, off sc1\n\ts_nop 1" : : "v"(a), "v"((u32)x)
+                     : "memory");
+        asm volatile("global_store_short %0, %1, off sc1\n\ts_nop 1" : : "v"(b), "v"((u32)y)
+                     : "memory");
+    } else {
+        *a = x;
+        *b = y;
+    }
+}
 // (c): as many bytes as k_sector_writes stores (64 B per frame), contiguous.
 template <int WM>
 __global__ void __launch_bounds__(256) k_contig_writes(uint8_t* __restrict__ buf, uint64_t chunks)
@@ -1985,6 +2011,16 @@ int imix_main(uint64_t n, int rounds)
             hipLaunchKernelGGL((k_line_writes<WM_SECTOR_NT>), dim3((8ull * n + 255) / 256),
                                dim3(256), 0, st, wbuf, total, doff, (u32)n);
         }});
+#define FIELDS(P_, NAME_)                                                                    \
+        vs.push_back({"write fields: 2 x 2 B checks per frame, " NAME_ " (no reads)", 4.0 * n,  \
+                      [&](hipStream_t st) {                                                  \
+            hipLaunchKernelGGL((k_field_writes<P_>), dim3((n + 255) / 256), dim3(256), 0, st, \
+                               wbuf, doff, (u32)n);                                          \
+        }});
+        FIELDS(0, "plain")
+        FIELDS(1, "nt")
+        FIELDS(2, "sc1")
+#undef FIELDS
         vs.push_back({"write contiguous: 64 B x frames, sc1", 64.0 * n, [&](hipStream_t st) {
             hipLaunchKernelGGL((k_contig_writes<WM_SECTOR_SC1>), dim3((4ull * n + 255) / 256),
                                dim3(256), 0, st, wbuf, 4ull * n);
