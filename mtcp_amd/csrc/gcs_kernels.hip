@@ -254,8 +254,8 @@ k_small_x(uint8_t* __restrict__ frames, uint64_t stride, u32 frame_len, u32 n,
 }
 
 // Descriptor batch: frame i at frames + off[i], length len[i], one frame per
-// G-lane group (longer frames in further batches of G*U chunks).  Direct-mode
-// host batches (launch_desc_spread), and device batches with the rooms hint
+// G-lane group (longer frames in further batches of G*U chunks).  Device
+// batches with the rooms hint
 // (GCS_VF_ROOMS / GCS_CF_ROOMS: frames one per mbuf room, which the packed
 // stream cannot stream; XCD-contiguous blocks, and for a fill of lines that
 // fit the Infinity Cache the whole-line write-back of k_fixed).
