@@ -1009,7 +1009,7 @@ struct gcs_ctx {
     uint32_t max_frames = 0;   // per slot
     uint64_t max_bytes = 0;    // per slot
     uint64_t direct_max = 0;   // host batches up to this many staged bytes: direct mode
-    bool direct_spread = true; // direct mode on k_desc (8 frames per block), not k_desc_mixed
+    bool direct_spread = true; // direct mode 8 frames per block (server / k_desc_rec), not k_desc_mixed
     Slot slot[kSlots];
     std::unique_ptr<GatherPool> pool;
     std::unique_ptr<BurstServer> server;   // gcs_ctx_set_burst_server / GCS_BURST_SERVER
