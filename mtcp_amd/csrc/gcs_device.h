@@ -204,6 +204,13 @@ __device__ __forceinline__ uint4 ldg16(const uint8_t* p)
     return make_uint4(r.x, r.y, r.z, r.w);
 }
 
+// A 2 B store into a frame (always global memory: global_store_short even
+// where the compiler cannot trace the pointer, as in the burst server).
+__device__ __forceinline__ void stg_u16(uint8_t* p, uint16_t v)
+{
+    *(__attribute__((address_space(1))) uint16_t*)(p) = v;
+}
+
 // One global_store_dwordx4 with the cache policy of write mode WM.
 template <int WM>
 __device__ __forceinline__ void stg16(uint8_t* p, uint4 v)
@@ -620,7 +627,7 @@ __device__ __forceinline__ void epilogue(const Hdr& h, Acc a, uint8_t* __restric
             return;
         u32 vd = rx_verdict<EXT>(h, a, len, desc_ok, flags, l4sum);
         if (vd == GCS_V_DROP_TCPCSUM && (flags & GCS_VF_ZERO_BAD_TCP_CHECK) && ts + 18u <= len)
-            *reinterpret_cast<uint16_t*>(f + ts + 16) = 0;         // tcp_in.c:1237
+            stg_u16(f + ts + 16, 0);         // tcp_in.c:1237
         out_code[0] = (uint8_t)vd;
         if constexpr (EXT) {
             const bool acc = vd == GCS_V_ACCEPT;
@@ -676,11 +683,11 @@ __device__ __forceinline__ void epilogue(const Hdr& h, Acc a, uint8_t* __restric
     if (!(flags & GCS_CF_NO_INPLACE) && wip) {
         if constexpr (WM == WM_HALFWORD) {
             if (sub == 0) {
-                *reinterpret_cast<uint16_t*>(f + 24) = (uint16_t)ipc;
+                stg_u16(f + 24, (uint16_t)ipc);
                 if (wtcp)
-                    *reinterpret_cast<uint16_t*>(f + ts + 16) = (uint16_t)l4c;
+                    stg_u16(f + ts + 16, (uint16_t)l4c);
                 if (wicmp)
-                    *reinterpret_cast<uint16_t*>(f + ts + 2) = (uint16_t)l4c;
+                    stg_u16(f + ts + 2, (uint16_t)l4c);
             }
         } else {
             const int nchunks = (int)((len + 15) >> 4);
@@ -708,11 +715,11 @@ __device__ __forceinline__ void epilogue(const Hdr& h, Acc a, uint8_t* __restric
                     continue;
                 if (16 * c + 16 > wl) {                      // chunk crosses the buffer end
                     if (has_ip)
-                        *reinterpret_cast<uint16_t*>(f + 24) = (uint16_t)ipc;
+                        stg_u16(f + 24, (uint16_t)ipc);
                     if (has_tcp)
-                        *reinterpret_cast<uint16_t*>(f + ts + 16) = (uint16_t)l4c;
+                        stg_u16(f + ts + 16, (uint16_t)l4c);
                     if (has_icmp)
-                        *reinterpret_cast<uint16_t*>(f + ts + 2) = (uint16_t)l4c;
+                        stg_u16(f + ts + 2, (uint16_t)l4c);
                     continue;
                 }
                 uint4 w = v[j];

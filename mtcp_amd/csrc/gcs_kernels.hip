@@ -464,8 +464,8 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
                     src = leader ? reinterpret_cast<const volatile u32x4*>(&rq->cmd.v)
                                  : reinterpret_cast<const volatile u32x4*>(&pub->exit[r].v);
                 u32x4 v = {0, 0, 0, 0};
-                if (src)
-                    v = *src;
+                if (src)                         // global_load (the lines are never LDS)
+                    v = *(const volatile __attribute__((address_space(1))) u32x4*)src;
                 // Whole lines only (gcs_internal.h: the host's 16 B lines may
                 // land as two 8 B halves).  A line A whose halves name
                 // different requests reads as the request before the one
@@ -629,7 +629,8 @@ k_burst_server(HubMailbox* mb, HubReqs* rq, HubPub* pub, uint64_t idle_ticks, ui
                 uint4 d = d0;
                 if (pass != 0 && here) {
                     // written before line A's fence: whole once A was seen
-                    const u32x4 w = *reinterpret_cast<const volatile u32x4*>(&sl->desc[i]);
+                    const u32x4 w = *(const volatile __attribute__((address_space(1))) u32x4*)
+                                         &sl->desc[i];
                     d = make_uint4(w.x, w.y, w.z, w.w);
                 }
                 const uint64_t o = (uint64_t)d.x | ((uint64_t)(d.y & 0xFFFFu) << 32);
