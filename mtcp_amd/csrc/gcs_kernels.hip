@@ -1125,7 +1125,7 @@ __device__ __forceinline__ void
 desc_fallback_block(uint8_t* __restrict__ frames, uint64_t frames_bytes,
                     const uint64_t* __restrict__ off, const uint16_t* __restrict__ lens,
                     uint64_t f0, int nf, uint8_t* __restrict__ out_code,
-                    uint32_t* __restrict__ out_csum, u32 flags, uint8_t* spare)
+                    uint32_t* __restrict__ out_csum, u32 flags)
 {
     const int sub = threadIdx.x & (G - 1);
     for (int k = threadIdx.x / G; k < nf; k += kBlock / G) {     // group-uniform
@@ -1136,7 +1136,10 @@ desc_fallback_block(uint8_t* __restrict__ frames, uint64_t frames_bytes,
         uint8_t* f = frames + (ok ? o : 0);
         do_frame<G, U, COMPUTE, true, true, kNT, WM_SECTOR_SC1>(
             f, len, ok ? (int64_t)(frames_bytes - o) : 0, ok, sub, flags,
-            out_code ? out_code + i : spare + k, out_csum ? out_csum + i : nullptr);
+            // RX: the verdict array is never null (every C-ABI entry checks it),
+            // so the store is a global one; a TX status array may be absent
+            COMPUTE ? (out_code ? out_code + i : nullptr) : out_code + i,
+            out_csum ? out_csum + i : nullptr);
     }
 }
 
@@ -1155,7 +1158,7 @@ k_desc_stream(uint8_t* __restrict__ frames, uint64_t frames_bytes,
     __shared__ uint64_t bm[RW];            // bit c: a frame starts at region chunk c
     __shared__ uint16_t rbase[RW];         // frames starting before chunk 64 * row
     __shared__ u32 wtot[NW];
-    __shared__ uint8_t codes[F];           // TX statuses (the write-back's test); RX spare
+    __shared__ uint8_t codes[F];           // TX statuses (the write-back's test)
     __shared__ u32 nchunks_s, pbase_s;     // the pass region's chunks; its first, in the block's
 
     const uint32_t blk = XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
@@ -1205,7 +1208,7 @@ k_desc_stream(uint8_t* __restrict__ frames, uint64_t frames_bytes,
     if (!__syncthreads_and(sok)) {         // block-uniform: nothing written
         if (pass == 0)
             desc_fallback_block<T::FG, T::FU, COMPUTE>(frames, frames_bytes, off, lens, f0, nf,
-                                                       out_code, out_csum, flags, codes);
+                                                       out_code, out_csum, flags);
         return;
     }
     int p0 = 0, p1 = 0;
@@ -1313,8 +1316,7 @@ k_desc_stream(uint8_t* __restrict__ frames, uint64_t frames_bytes,
     const bool fast = !in || ((NH == 4 ? ihl <= 8 : ihl == 5) && (te <= HB || te == (int)len));
     if (!__syncthreads_and(fast)) {    // block-uniform: this pass wrote nothing yet
         desc_fallback_block<T::FG, T::FU, COMPUTE>(frames, frames_bytes, off, lens, f0 + p0,
-                                                   fb_hi - p0, out_code, out_csum, flags,
-                                                   codes + p0);
+                                                   fb_hi - p0, out_code, out_csum, flags);
         return;
     }
     // wave-uniform: every frame of the wave has ihl == 5, so the stash's
@@ -1352,7 +1354,7 @@ k_desc_stream(uint8_t* __restrict__ frames, uint64_t frames_bytes,
         const uint64_t o = r0 + 16ull * (pb + rs);
         epilogue<1, 4, COMPUTE, WM, false>(
             h, a, frames + o, len, (int64_t)(frames_bytes - o), true, 0, flags,
-            COMPUTE ? codes + t : (out_code ? out_code + f0 + t : codes + t),
+            COMPUTE ? codes + t : out_code + f0 + t,        // RX: never null (C ABI)
             COMPUTE && out_csum ? out_csum + f0 + t : nullptr, true, h4, XFrame{},
             COMPUTE ? reinterpret_cast<uint8_t*>(hdr + 4 * t) : nullptr);
     }
@@ -1379,10 +1381,9 @@ k_desc_stream(uint8_t* __restrict__ frames, uint64_t frames_bytes,
             out_code[f0 + t] = codes[t];
     }
     if (fb_hi > p1) {
-        __syncthreads();                   // codes[] is the per-frame path's spare
+        __syncthreads();                   // every wave done with the pass
         desc_fallback_block<T::FG, T::FU, COMPUTE>(frames, frames_bytes, off, lens, f0 + p1,
-                                                   fb_hi - p1, out_code, out_csum, flags,
-                                                   codes + p1);
+                                                   fb_hi - p1, out_code, out_csum, flags);
     }
 }
 
