@@ -810,6 +810,23 @@ class BurstServer {
         spin_ = std::chrono::nanoseconds((long)(1000.0 * (e ? std::max(0.0, std::atof(e)) : 4.0)));
         e = std::getenv("GCS_SERVER_SLEEP_NS");
         sleep_ns_ = e ? std::clamp(std::atol(e), 1L, 1000000L) : 1000L;
+        e = std::getenv("GCS_SERVER_PRESLEEP_NS");
+        presleep_ns_ = e ? std::clamp(std::atol(e), 0L, 100000L) : 0L;
+    }
+
+    // GCS_SERVER_PRESLEEP_NS: sleep this long right after posting, before the
+    // spin -- no request completes sooner than the grid's round trip, so a
+    // thread that sleeps through part of it gives that CPU time back to the
+    // other mTCP threads of a CPU quota without waiting longer itself, as long
+    // as its wake-up comes before the records (timer slack 1 ns).
+    void presleep()
+    {
+        if (!slack_set_) {
+            (void)prctl(PR_SET_TIMERSLACK, 1UL, 0UL, 0UL, 0UL);
+            slack_set_ = true;
+        }
+        const struct timespec ts = {0, presleep_ns_};
+        nanosleep(&ts, nullptr);
     }
 
     // Wait until request r is done (its records, and for an in-place request
@@ -821,6 +838,9 @@ class BurstServer {
         const int nb = (int)std::min<uint32_t>(gcs::kServerBlocks,
                                                (r.n + gcs::kServerFPB - 1) / gcs::kServerFPB);
         const auto t0 = std::chrono::steady_clock::now();
+        if (presleep_ns_ && r.have == 0 && r.n &&
+            (__atomic_load_n(&sl.rec[0], __ATOMIC_ACQUIRE) >> 48) != (tag >> 48))
+            presleep();
         for (;;) {
             while (r.have < r.n &&
                    (__atomic_load_n(&sl.rec[r.have], __ATOMIC_ACQUIRE) >> 48) == (tag >> 48))
@@ -982,6 +1002,7 @@ class BurstServer {
     int wait_mode_ = kWaitSpin;           // GCS_SERVER_WAIT (idle)
     std::chrono::nanoseconds spin_{4000};
     long sleep_ns_ = 1000;
+    long presleep_ns_ = 0;                // GCS_SERVER_PRESLEEP_NS (complete)
     bool slack_set_ = false;
     ServerHub* hub_ = nullptr;
     int r_ = -1;                          // ring index in the hub
