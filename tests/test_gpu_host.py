@@ -160,6 +160,32 @@ def test_burst_server_matches_oracle(torch_dev, monkeypatch, idle_us, life_us, g
                 time.sleep(gap_s)
 
 
+@pytest.mark.parametrize("wait,spin_us,presleep_ns", [("yield", "0", "0"), ("sleep", "0", "0"),
+                                                      ("spin", "4", "2000")])
+def test_burst_server_wait_policies(torch_dev, monkeypatch, wait, spin_us, presleep_ns):
+    """The host's wait policies (GCS_SERVER_WAIT / _SPIN_US / _PRESLEEP_NS,
+    read when the context joins the grid) change how a thread waits, never
+    what it gets: every burst is exact."""
+    monkeypatch.setenv("GCS_SERVER_WAIT", wait)
+    monkeypatch.setenv("GCS_SERVER_SPIN_US", spin_us)
+    monkeypatch.setenv("GCS_SERVER_PRESLEEP_NS", presleep_ns)
+    O = Oracle()
+    with gpucsum.Context(0, max_frames=1024, max_bytes=4 << 20) as c:
+        c.set_burst_server(True)
+        for k, (buf, off, lens) in enumerate(bursts(20, 64, 700)):
+            b1 = buf.copy()
+            st, cs = c.compute_host(b1, off, lens)
+            ref = buf.copy()
+            rst, rcs = O.compute_batch(ref, off, lens)
+            np.testing.assert_array_equal(st, rst)
+            np.testing.assert_array_equal(cs, rcs)
+            np.testing.assert_array_equal(b1, ref)
+            bad = synth.corrupt(ref, off, lens, frac_log2=2, seed=k)
+            v = c.verify_host(ref.copy(), off, lens, flags=1)
+            np.testing.assert_array_equal(v, O.verify_batch(ref.copy(), off, lens, flags=1))
+            assert (v[bad] != 0).all()
+
+
 def test_burst_server_yields_to_large_batches(torch_dev):
     """With the server on, a batch too large for direct mode takes the DMA
     path (the grid leaves first), and bursts after it are served again."""
